@@ -1,0 +1,363 @@
+#!/usr/bin/env python3
+"""Generate the committed golden fixtures for the WebP decode path.
+
+Test infrastructure only -- runs in the build container, never on the GPU box.
+
+The reference (DaanV2/go-webp) is an unbuildable Go translation of libwebp 1.6.0
+(``pkg/vp8/constants.go:18-20`` pins DEC_MAJ/MIN/REV_VERSION = 1/6/0; SURVEY.md
+§0, §8(c)).  The upstream it translates is available offline here as Pillow's
+bundled ``libwebp`` (``WebPGetDecoderVersion() == 0x010600``).  We load it with
+ctypes, force its *plain-C* DSP kernels (``VP8GetCPUInfo = NULL``: exactly the
+functions ``pkg/libwebp/dsp/dec.c.go``, ``upsampling.c.go`` and ``lossless.go``
+translate) and write, per bitstream:
+
+* lossy:  post-filter Y/U/V planes (``WebPDecodeYUV``), recon-only planes
+  (``bypass_filtering=1``), fancy-upsampled RGBA (``WebPDecodeRGBA``, the
+  default ``EmitFancyRGB`` path, ``io_dec.c.go:65-115``) and point-sampled
+  RGBA (``no_fancy_upsampling=1``, ``EmitSampledRGB`` ``io_dec.c.go:53-59``);
+* lossless: RGBA.
+
+Small cases are stored as ``.webp`` + compressed ``.npz``; the large bench
+frames (SURVEY.md §8(d), Appendix B generators) are stored as ``.webp`` plus
+SHA-256 of their decodes in ``manifest.json``.  Every decode is also checked
+against libwebp's SIMD path (must be byte-identical) before it is written.
+
+Usage:  python tests/golden/make_golden.py   (rewrites tests/golden/{lossy,lossless,bench}/)
+"""
+import ctypes as C
+import glob
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PIL_LIBS = "/usr/local/lib/python3.10/dist-packages/pillow.libs/"
+ABI = 0x0210  # WEBP_{ENCODER,DECODER}_ABI_VERSION of 1.6.0 (pkg/constants/versions.go:4-5)
+
+MODE_RGBA = 1
+MODE_YUV = 11
+
+
+def load_libwebp():
+    C.CDLL(glob.glob(PIL_LIBS + "libsharpyuv-*.so*")[0], mode=C.RTLD_GLOBAL)
+    lib = C.CDLL(glob.glob(PIL_LIBS + "libwebp-*.so*")[0])
+    assert lib.WebPGetDecoderVersion() == 0x010600, hex(lib.WebPGetDecoderVersion())
+    lib.WebPDecodeRGBA.restype = C.c_void_p
+    lib.WebPDecodeYUV.restype = C.c_void_p
+    lib.WebPFree.argtypes = [C.c_void_p]
+    lib.WebPMemoryWriterClear.argtypes = [C.c_void_p]
+    return lib
+
+
+LIB = load_libwebp()
+_CPU = C.c_void_p.in_dll(LIB, "VP8GetCPUInfo")
+_SIMD = _CPU.value
+
+
+def _plain_c(on):
+    _CPU.value = None if on else _SIMD
+
+
+# ----------------------------------------------------------------------------- encode
+def encode(img, quality=75.0, lossless=0, method=4, segments=4, sns=50, filter_strength=60,
+           sharpness=0, filter_type=1, autofilter=0, partitions=0, low_memory=0, exact=0):
+    """img: HxWx3 or HxWx4 uint8.  Returns the encoded RIFF bytes."""
+    h, w, ch = img.shape
+    cfg = (C.c_int32 * 64)()
+    assert LIB.WebPConfigInitInternal(cfg, 0, C.c_float(quality), ABI)
+    cfgf = C.cast(cfg, C.POINTER(C.c_float))
+    cfg[0] = lossless
+    cfgf[1] = quality
+    cfg[2] = method
+    cfg[6] = segments
+    cfg[7] = sns
+    cfg[8] = filter_strength
+    cfg[9] = sharpness
+    cfg[10] = filter_type
+    cfg[11] = autofilter
+    cfg[18] = partitions
+    cfg[22] = low_memory
+    cfg[24] = exact
+    assert LIB.WebPValidateConfig(cfg), "bad config"
+    pic = (C.c_uint8 * 512)()
+    assert LIB.WebPPictureInitInternal(pic, ABI)
+    pi = C.cast(pic, C.POINTER(C.c_int32))
+    pi[0] = 1 if lossless else 0  # use_argb
+    pi[2] = w
+    pi[3] = h
+    wr = (C.c_uint8 * 64)()
+    LIB.WebPMemoryWriterInit(wr)
+    pp = C.cast(pic, C.POINTER(C.c_void_p))
+    pp[96 // 8] = C.cast(LIB.WebPMemoryWrite, C.c_void_p).value
+    pp[104 // 8] = C.addressof(wr)
+    buf = np.ascontiguousarray(img)
+    if ch == 3:
+        ok = LIB.WebPPictureImportRGB(pic, buf.ctypes.data_as(C.c_void_p), w * 3)
+    else:
+        ok = LIB.WebPPictureImportRGBA(pic, buf.ctypes.data_as(C.c_void_p), w * 4)
+    assert ok
+    ok = LIB.WebPEncode(cfg, pic)
+    err = pi[136 // 4]
+    assert ok, f"encode failed err={err}"
+    wp = C.cast(wr, C.POINTER(C.c_void_p))
+    size = C.cast(wr, C.POINTER(C.c_size_t))[1]
+    out = C.string_at(wp[0], size)
+    LIB.WebPMemoryWriterClear(wr)
+    LIB.WebPPictureFree(pic)
+    return out
+
+
+# ----------------------------------------------------------------------------- decode
+def _decode_cfg(data, colorspace, bypass=0, no_fancy=0):
+    cfg = (C.c_uint8 * 512)()
+    assert LIB.WebPInitDecoderConfigInternal(cfg, ABI)
+    ci = C.cast(cfg, C.POINTER(C.c_int32))
+    ci[40 // 4] = colorspace
+    ci[160 // 4] = bypass
+    ci[164 // 4] = no_fancy
+    st = LIB.WebPDecode(data, C.c_size_t(len(data)), cfg)
+    assert st == 0, f"WebPDecode status {st}"
+    w, h = ci[44 // 4], ci[48 // 4]
+    cp = C.cast(cfg, C.POINTER(C.c_void_p))
+    if colorspace == MODE_YUV:
+        ys, us, vs = ci[88 // 4], ci[92 // 4], ci[96 // 4]
+        uw, uh = (w + 1) // 2, (h + 1) // 2
+
+        def plane(ptr, stride, pw, ph):
+            raw = np.frombuffer(C.string_at(ptr, stride * (ph - 1) + pw), np.uint8)
+            return np.stack([raw[r * stride:r * stride + pw] for r in range(ph)])
+
+        out = (plane(cp[56 // 8], ys, w, h), plane(cp[64 // 8], us, uw, uh),
+               plane(cp[72 // 8], vs, uw, uh))
+    else:
+        stride = ci[64 // 4]
+        raw = np.frombuffer(C.string_at(cp[56 // 8], stride * h), np.uint8)
+        out = raw.reshape(h, stride)[:, :w * 4].reshape(h, w, 4).copy()
+    LIB.WebPFreeDecBuffer(C.byref(cfg, 40))
+    return out
+
+
+def decode_all(data, lossy=True):
+    """Decode with plain-C kernels; assert SIMD path is identical."""
+    res = {}
+    for plain in (True, False):
+        _plain_c(plain)
+        r = {"rgba": _decode_cfg(data, MODE_RGBA)}
+        if lossy:
+            r["rgba_point"] = _decode_cfg(data, MODE_RGBA, no_fancy=1)
+            y, u, v = _decode_cfg(data, MODE_YUV)
+            r.update(y=y, u=u, v=v)
+            y, u, v = _decode_cfg(data, MODE_YUV, bypass=1)
+            r.update(y_nofilter=y, u_nofilter=u, v_nofilter=v)
+            r["rgba_nofilter"] = _decode_cfg(data, MODE_RGBA, bypass=1)
+        if plain:
+            res = r
+        else:
+            for k in r:
+                assert np.array_equal(r[k], res[k]), f"plain-C != SIMD for {k}"
+    _plain_c(True)
+    return res
+
+
+# ----------------------------------------------------------------------------- header probe
+class _Bool:  # RFC 6386 §7 bool decoder, used to label fixtures
+    def __init__(s, b):
+        s.b = b; s.p = 2; s.value = (b[0] << 8) | b[1]; s.range = 255; s.bit_count = 0
+
+    def bit(s, prob):
+        split = 1 + (((s.range - 1) * prob) >> 8); big = split << 8
+        if s.value >= big:
+            r = 1; s.range -= split; s.value -= big
+        else:
+            r = 0; s.range = split
+        while s.range < 128:
+            s.value <<= 1; s.range <<= 1; s.bit_count += 1
+            if s.bit_count == 8:
+                s.bit_count = 0
+                if s.p < len(s.b):
+                    s.value |= s.b[s.p]
+                s.p += 1
+        return r
+
+    def lit(s, n):
+        v = 0
+        for _ in range(n):
+            v = (v << 1) | s.bit(128)
+        return v
+
+    def sval(s, n):
+        v = s.lit(n)
+        return -v if s.bit(128) else v
+
+
+def vp8_header(data):
+    i = data.find(b"VP8 ")
+    f = data[i + 8:]
+    p0 = (f[0] | (f[1] << 8) | (f[2] << 16)) >> 5
+    br = _Bool(f[10:10 + p0]); br.bit(128); br.bit(128)
+    segs = 0
+    if br.bit(128):
+        segs = 1
+        upd_map = br.bit(128)
+        if br.bit(128):
+            br.bit(128)
+            [br.sval(7) if br.bit(128) else 0 for _ in range(4)]
+            [br.sval(6) if br.bit(128) else 0 for _ in range(4)]
+        if upd_map:
+            [br.lit(8) if br.bit(128) else 255 for _ in range(3)]
+    simple = br.bit(128); level = br.lit(6); sharp = br.lit(3)
+    if br.bit(128) and br.bit(128):
+        for _ in range(8):
+            if br.bit(128):
+                br.sval(6)
+    parts = 1 << br.lit(2)
+    return dict(segments=segs, simple=simple, level=level, sharpness=sharp, partitions=parts)
+
+
+# ----------------------------------------------------------------------------- synthetic images
+def synth(H, W, seed, sigma):  # SURVEY.md Appendix B (lossy C1-C4)
+    rng = np.random.default_rng(seed); yy, xx = np.mgrid[0:H, 0:W]
+    base = np.stack([(xx * 255) // W, (yy * 255) // H, (((xx // 64) + (yy // 64)) % 2) * 160 + 40], -1)
+    return np.clip(base + rng.normal(0, sigma, (H, W, 3)), 0, 255).astype(np.uint8)
+
+
+def corr_luma(H, W, seed):  # SURVEY.md Appendix B (lossless C5)
+    rng = np.random.default_rng(seed); yy, xx = np.mgrid[0:H, 0:W]
+    lum = 128 + 100 * np.sin(xx / 37.0) * np.cos(yy / 53.0) + rng.normal(0, 4, (H, W))
+    return np.clip(np.stack([lum + 10, lum, lum - 15 + 20 * np.sin(yy / 91.0)], -1), 0, 255).astype(np.uint8)
+
+
+def smooth(H, W, seed):  # i16-heavy content
+    rng = np.random.default_rng(seed); yy, xx = np.mgrid[0:H, 0:W]
+    r = 128 + 90 * np.sin(xx / 23.0 + seed) * np.cos(yy / 31.0)
+    g = 128 + 80 * np.cos((xx + yy) / 41.0)
+    b = 64 + (xx * 127) // max(W - 1, 1)
+    return np.clip(np.stack([r, g, b], -1) + rng.normal(0, 1.0, (H, W, 3)), 0, 255).astype(np.uint8)
+
+
+def noise(H, W, seed, sigma=60):  # i4x4-heavy content, many coefficients
+    rng = np.random.default_rng(seed)
+    img = synth(H, W, seed, 0).astype(np.float64)
+    return np.clip(img + rng.normal(0, sigma, (H, W, 3)), 0, 255).astype(np.uint8)
+
+
+def palette_img(H, W, seed, ncol):
+    rng = np.random.default_rng(seed)
+    pal = rng.integers(0, 256, (ncol, 4), dtype=np.uint8)
+    pal[:, 3] = 255
+    yy, xx = np.mgrid[0:H, 0:W]
+    idx = ((xx // 3) + (yy // 5) * 7 + rng.integers(0, 2, (H, W))) % ncol
+    return pal[idx]
+
+
+def with_alpha(img, seed):
+    rng = np.random.default_rng(seed)
+    H, W, _ = img.shape
+    yy, xx = np.mgrid[0:H, 0:W]
+    a = np.clip(128 + 127 * np.sin(xx / 13.0) * np.cos(yy / 7.0) + rng.normal(0, 3, (H, W)), 0, 255)
+    a[: H // 4, : W // 4] = 0
+    return np.concatenate([img, a.astype(np.uint8)[..., None]], -1)
+
+
+# ----------------------------------------------------------------------------- cases
+LOSSY_CASES = [
+    # name, image-fn, encoder kwargs
+    ("synth_17x9", lambda: synth(9, 17, 1, 6), {}),
+    ("synth_1x1", lambda: synth(1, 1, 2, 6), {}),
+    ("synth_2x3", lambda: synth(3, 2, 2, 6), {}),
+    ("synth_80x96", lambda: synth(96, 80, 3, 6), {}),
+    ("synth_128x128_q90", lambda: synth(128, 128, 4, 6), {"quality": 90}),
+    ("synth_481x270", lambda: synth(270, 481, 5, 6), {}),
+    ("noise_96x64_complex_s0", lambda: noise(64, 96, 6), {"sharpness": 0}),
+    ("noise_96x64_complex_s3", lambda: noise(64, 96, 7), {"sharpness": 3, "filter_strength": 80}),
+    ("noise_96x64_complex_s7", lambda: noise(64, 96, 8), {"sharpness": 7, "filter_strength": 100}),
+    ("noise_96x64_simple", lambda: noise(64, 96, 9), {"filter_type": 0, "filter_strength": 70}),
+    ("noise_96x64_simple_s5", lambda: noise(64, 96, 10), {"filter_type": 0, "sharpness": 5, "filter_strength": 50}),
+    ("noise_96x64_nofilter", lambda: noise(64, 96, 11), {"filter_strength": 0}),
+    ("noise_97x63_q20", lambda: noise(63, 97, 12, 40), {"quality": 20, "filter_strength": 100}),
+    ("noise_64x64_q100", lambda: noise(64, 64, 13, 80), {"quality": 100}),
+    ("smooth_160x112", lambda: smooth(112, 160, 14), {}),
+    ("smooth_161x113_simple", lambda: smooth(113, 161, 15), {"filter_type": 0}),
+    ("synth_200x150_seg1", lambda: synth(150, 200, 16, 12), {"segments": 1}),
+    ("synth_200x150_part4", lambda: synth(150, 200, 17, 12), {"partitions": 2, "method": 2}),
+    ("synth_200x150_part8", lambda: synth(150, 200, 18, 12), {"partitions": 3, "low_memory": 1}),
+    ("noise_130x70_q5", lambda: noise(70, 130, 19, 30), {"quality": 5, "filter_strength": 100}),
+    ("synth_256x256_sns100", lambda: synth(256, 256, 20, 20), {"sns": 100, "filter_strength": 40}),
+    ("alpha_64x48", lambda: with_alpha(synth(48, 64, 21, 6), 21), {}),
+]
+
+LOSSLESS_CASES = [
+    ("ll_corr_64x64", lambda: corr_luma(64, 64, 1), {"method": 4}),
+    ("ll_corr_123x77", lambda: corr_luma(77, 123, 2), {"method": 6, "quality": 100}),
+    ("ll_synth_90x33_m0", lambda: synth(33, 90, 3, 10), {"method": 0}),
+    ("ll_noise_50x50", lambda: noise(50, 50, 4, 30), {"method": 4}),
+    ("ll_pal2_64x40", lambda: palette_img(40, 64, 5, 2), {}),
+    ("ll_pal4_63x41", lambda: palette_img(41, 63, 6, 4), {}),
+    ("ll_pal16_65x39", lambda: palette_img(39, 65, 7, 16), {}),
+    ("ll_pal200_70x30", lambda: palette_img(30, 70, 8, 200), {}),
+    ("ll_alpha_48x48", lambda: with_alpha(corr_luma(48, 48, 9), 9), {"exact": 1}),
+    ("ll_smooth_100x60_q0", lambda: smooth(60, 100, 10), {"quality": 0, "method": 1}),
+]
+
+BENCH_CASES = [
+    # name, H, W, seeds, kwargs, generator  
+    ("c1_512", 512, 512, [0], {}, "synth6"),
+    ("c2_1080p", 1080, 1920, list(range(8)), {}, "synth6"),
+    ("c3_4k", 2160, 3840, list(range(8)), {"filter_type": 1, "filter_strength": 60}, "synth6"),
+    ("c5_ll2048", 2048, 2048, [0], {"lossless": 1}, "corr"),
+]
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def main():
+    os.makedirs(os.path.join(HERE, "lossy"), exist_ok=True)
+    os.makedirs(os.path.join(HERE, "lossless"), exist_ok=True)
+    os.makedirs(os.path.join(HERE, "bench"), exist_ok=True)
+    manifest = {"libwebp": "1.6.0 (Pillow 12.2.0 bundle, plain-C DSP)", "lossy": {}, "lossless": {}, "bench": {}}
+    for name, fn, kw in LOSSY_CASES:
+        img = fn()
+        data = encode(img, **kw)
+        r = decode_all(data, lossy=True)
+        with open(os.path.join(HERE, "lossy", name + ".webp"), "wb") as f:
+            f.write(data)
+        np.savez_compressed(os.path.join(HERE, "lossy", name + ".npz"), **r)
+        hdr = vp8_header(data)
+        manifest["lossy"][name] = dict(bytes=len(data), width=img.shape[1], height=img.shape[0],
+                                       header=hdr, encoder=kw)
+        print(name, len(data), hdr, flush=True)
+    for name, fn, kw in LOSSLESS_CASES:
+        img = fn()
+        data = encode(img, lossless=1, **kw)
+        r = decode_all(data, lossy=False)
+        with open(os.path.join(HERE, "lossless", name + ".webp"), "wb") as f:
+            f.write(data)
+        np.savez_compressed(os.path.join(HERE, "lossless", name + ".npz"), **r)
+        manifest["lossless"][name] = dict(bytes=len(data), width=img.shape[1], height=img.shape[0], encoder=kw)
+        print(name, len(data), flush=True)
+    for name, H, W, seeds, kw, gen in BENCH_CASES:
+        for s in seeds:
+            img = synth(H, W, s, 6) if gen == "synth6" else corr_luma(H, W, s)
+            lossless = kw.get("lossless", 0)
+            data = encode(img, **kw)
+            r = decode_all(data, lossy=not lossless)
+            fn = f"{name}_s{s}.webp"
+            with open(os.path.join(HERE, "bench", fn), "wb") as f:
+                f.write(data)
+            ent = dict(bytes=len(data), width=W, height=H, bpp=8.0 * len(data) / (W * H),
+                       sha256={k: sha(v) for k, v in r.items()})
+            if not lossless:
+                ent["header"] = vp8_header(data)
+            manifest["bench"][fn] = ent
+            print(fn, len(data), flush=True)
+    with open(os.path.join(HERE, "manifest.json"), "w") as f:
+        json.dump(manifest, f, indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    sys.exit(main())
