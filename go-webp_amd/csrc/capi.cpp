@@ -1,0 +1,431 @@
+// extern "C" boundary of libgowebp_amd.so (declared in include/gowebp_amd.h).
+//
+// Host orchestration of the batch decode: a host thread pool runs the entropy
+// stage (one frame per task), inputs are packed into one pinned staging buffer and
+// copied to HBM in one transfer, then K1 (reconstruct + deblock) and K2
+// (YUV420 -> RGBA) each run as ONE launch over the whole batch.  Mirrors the call
+// structure of DecodeInto / WebPDecode (pkg/libwebp/decoder/webp.go:483-556,
+// 870-909) with the per-row VP8Io.put chain replaced by whole-frame kernels.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstring>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "../../include/gowebp_amd.h"
+#include "device/kernels.h"
+#include "device_format.h"
+#include "host/host.h"
+
+using wg::FrameDesc;
+using wg::MbRec;
+
+struct wg_ctx {
+  int device = 0;
+  int host_threads = 1;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+};
+
+namespace {
+
+constexpr size_t kAlign = 256;
+inline size_t align_up(size_t v) { return (v + kAlign - 1) & ~(kAlign - 1); }
+
+struct FrameParse {
+  int status = WG_STATUS_OK;
+  wg::SparseFrame sf;
+  size_t off_recs = 0, off_rows = 0, off_blocks = 0;  // within the input buffer
+  size_t off_y = 0, off_u = 0, off_v = 0;            // within the plane buffer
+  size_t off_rgba = 0;                                // within the RGBA buffer
+};
+
+struct Timing {
+  hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+};
+
+int parse_one(const uint8_t* data, size_t size, int flags, FrameParse* fp) {
+  wg::Container c;
+  wg_features feat{};
+  int st = wg::parse_container(data, size, &c, &feat);
+  if (st != WG_STATUS_OK) return st;
+  if (c.is_lossless) return WG_STATUS_UNSUPPORTED_FEATURE;  // VP8L: next row of SURVEY §8(f)
+  if (c.alpha_size > 0) return WG_STATUS_UNSUPPORTED_FEATURE;  // ALPH: next row (f2)
+  st = wg::vp8_parse(data, size, flags, nullptr, nullptr, &fp->sf);
+  if (st != WG_STATUS_OK) return st;
+  if (fp->sf.info.mb_w > wg::vp8_recon_max_mb_w()) return WG_STATUS_UNSUPPORTED_FEATURE;
+  return WG_STATUS_OK;
+}
+
+void parse_all(const uint8_t* const* data, const size_t* sizes, int n, int flags, int threads,
+               std::vector<FrameParse>& out) {
+  out.resize(n);
+  std::atomic<int> next{0};
+  auto work = [&]() {
+    for (;;) {
+      const int i = next.fetch_add(1);
+      if (i >= n) break;
+      if (data[i] == nullptr) {
+        out[i].status = WG_STATUS_INVALID_PARAM;
+        continue;
+      }
+      out[i].status = parse_one(data[i], sizes[i], flags, &out[i]);
+    }
+  };
+  const int t = std::max(1, std::min(threads, n));
+  if (t == 1) {
+    work();
+  } else {
+    std::vector<std::thread> pool;
+    for (int k = 0; k < t; ++k) pool.emplace_back(work);
+    for (auto& th : pool) th.join();
+  }
+}
+
+}  // namespace
+
+struct wg_batch {
+  wg_ctx* ctx = nullptr;
+  int n = 0;
+  int flags = 0;
+  std::vector<FrameParse> fp;
+  std::vector<FrameDesc> desc;
+  FrameDesc* d_desc = nullptr;
+  uint8_t* d_in = nullptr;
+  uint8_t* d_planes = nullptr;
+  uint8_t* d_rgba = nullptr;
+  size_t in_bytes = 0, plane_bytes = 0, rgba_bytes = 0;
+  int max_mb_w = 1, max_w = 1, max_h = 1;
+  int n_valid = 0;
+  int64_t pixels = 0;
+  double kbytes[2] = {0, 0};
+  std::vector<Timing> timings;  // one per run since the last query
+  size_t n_runs_pending = 0;
+};
+
+extern "C" {
+
+int wg_version(void) { return 0x000100; }
+
+int wg_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int wg_get_features(const uint8_t* data, size_t size, wg_features* out) {
+  if (out == nullptr) return WG_STATUS_INVALID_PARAM;
+  std::memset(out, 0, sizeof(*out));
+  wg::Container c;
+  const int st = wg::parse_container(data, size, &c, out);
+  // animated files: WebPGetFeatures reports the VP8X features with OK
+  if (st == WG_STATUS_UNSUPPORTED_FEATURE && c.has_animation) return WG_STATUS_OK;
+  return st;
+}
+
+int wg_vp8_parse(const uint8_t* data, size_t size, int flags, wg_vp8_info* info, wg_vp8_mb* mbs) {
+  if (data == nullptr) return WG_STATUS_INVALID_PARAM;
+  return wg::vp8_parse(data, size, flags, info, mbs, nullptr);
+}
+
+wg_ctx* wg_ctx_create(int device, int host_threads) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return nullptr;
+  if (hipSetDevice(device) != hipSuccess) return nullptr;
+  wg_ctx* c = new wg_ctx();
+  c->device = device;
+  c->host_threads = host_threads > 0 ? host_threads : (int)std::max(1u, std::thread::hardware_concurrency());
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return nullptr;
+  }
+  return c;
+}
+
+void wg_ctx_destroy(wg_ctx* c) {
+  if (!c) return;
+  hipSetDevice(c->device);
+  if (c->stream) hipStreamDestroy(c->stream);
+  delete c;
+}
+
+void wg_batch_destroy(wg_batch* b) {
+  if (!b) return;
+  hipSetDevice(b->ctx->device);
+  hipStreamSynchronize(b->ctx->stream);
+  for (auto& t : b->timings)
+    for (auto& e : t.ev)
+      if (e) hipEventDestroy(e);
+  if (b->d_desc) hipFree(b->d_desc);
+  if (b->d_in) hipFree(b->d_in);
+  if (b->d_planes) hipFree(b->d_planes);
+  if (b->d_rgba) hipFree(b->d_rgba);
+  delete b;
+}
+
+wg_batch* wg_batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t* sizes, int n, int32_t flags,
+                          int32_t* status) {
+  if (!ctx || !data || !sizes || n <= 0) return nullptr;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  if (hipSetDevice(ctx->device) != hipSuccess) return nullptr;
+  wg_batch* b = new wg_batch();
+  b->ctx = ctx;
+  b->n = n;
+  b->flags = flags;
+  parse_all(data, sizes, n, flags, ctx->host_threads, b->fp);
+  // layout
+  size_t in_b = 0, pl_b = 0, rg_b = 0;
+  double k1 = 0, k2 = 0;
+  for (int i = 0; i < n; ++i) {
+    FrameParse& f = b->fp[i];
+    if (status) status[i] = f.status;
+    if (f.status != WG_STATUS_OK) continue;
+    const wg_vp8_info& inf = f.sf.info;
+    const size_t nmb = (size_t)inf.mb_w * inf.mb_h;
+    f.off_recs = in_b;
+    in_b = align_up(in_b + nmb * sizeof(MbRec));
+    f.off_rows = in_b;
+    in_b = align_up(in_b + (size_t)inf.mb_h * 4);
+    f.off_blocks = in_b;
+    in_b = align_up(in_b + f.sf.blocks.size() * 2);
+    f.off_y = pl_b;
+    pl_b = align_up(pl_b + nmb * 256);
+    f.off_u = pl_b;
+    pl_b = align_up(pl_b + nmb * 64);
+    f.off_v = pl_b;
+    pl_b = align_up(pl_b + nmb * 64);
+    f.off_rgba = rg_b;
+    rg_b = align_up(rg_b + (size_t)inf.width * inf.height * 4);
+    b->max_mb_w = std::max(b->max_mb_w, inf.mb_w);
+    b->max_w = std::max(b->max_w, inf.width);
+    b->max_h = std::max(b->max_h, inf.height);
+    b->n_valid++;
+    b->pixels += (int64_t)inf.width * inf.height;
+    // algorithmic bytes: K1 reads records + coefficients, writes MB-padded
+    // planes; K2 reads cropped planes, writes RGBA.
+    const double px = (double)inf.width * inf.height;
+    const double uvpx = 2.0 * ((inf.width + 1) / 2) * (double)((inf.height + 1) / 2);
+    k1 += (double)nmb * sizeof(MbRec) + inf.mb_h * 4.0 + f.sf.blocks.size() * 2.0 + nmb * 384.0;
+    k2 += px + uvpx + 4.0 * px;
+  }
+  b->kbytes[0] = k1;
+  b->kbytes[1] = k2;
+  b->in_bytes = std::max<size_t>(in_b, kAlign);
+  b->plane_bytes = std::max<size_t>(pl_b, kAlign);
+  b->rgba_bytes = std::max<size_t>(rg_b, kAlign);
+  auto fail = [&](int st) {
+    if (status)
+      for (int i = 0; i < n; ++i)
+        if (status[i] == WG_STATUS_OK) status[i] = st;
+    wg_batch_destroy(b);
+    return (wg_batch*)nullptr;
+  };
+  if (hipMalloc(&b->d_in, b->in_bytes) != hipSuccess || hipMalloc(&b->d_planes, b->plane_bytes) != hipSuccess ||
+      hipMalloc(&b->d_rgba, b->rgba_bytes) != hipSuccess ||
+      hipMalloc(&b->d_desc, sizeof(FrameDesc) * (size_t)n) != hipSuccess)
+    return fail(WG_STATUS_OUT_OF_MEMORY);
+  // stage inputs in pinned memory, one H2D copy
+  uint8_t* h_in = nullptr;
+  if (hipHostMalloc(reinterpret_cast<void**>(&h_in), b->in_bytes, hipHostMallocDefault) != hipSuccess)
+    return fail(WG_STATUS_OUT_OF_MEMORY);
+  b->desc.assign(n, FrameDesc{});
+  for (int i = 0; i < n; ++i) {
+    FrameParse& f = b->fp[i];
+    FrameDesc& d = b->desc[i];
+    if (f.status != WG_STATUS_OK) continue;
+    const wg_vp8_info& inf = f.sf.info;
+    std::memcpy(h_in + f.off_recs, f.sf.mbs.data(), f.sf.mbs.size() * sizeof(MbRec));
+    std::memcpy(h_in + f.off_rows, f.sf.row_block0.data(), f.sf.row_block0.size() * 4);
+    if (!f.sf.blocks.empty()) std::memcpy(h_in + f.off_blocks, f.sf.blocks.data(), f.sf.blocks.size() * 2);
+    d.mbs = reinterpret_cast<const MbRec*>(b->d_in + f.off_recs);
+    d.row_block0 = reinterpret_cast<const uint32_t*>(b->d_in + f.off_rows);
+    d.blocks = reinterpret_cast<const int16_t*>(b->d_in + f.off_blocks);
+    d.y = b->d_planes + f.off_y;
+    d.u = b->d_planes + f.off_u;
+    d.v = b->d_planes + f.off_v;
+    d.rgba = b->d_rgba + f.off_rgba;
+    d.width = inf.width;
+    d.height = inf.height;
+    d.mb_w = inf.mb_w;
+    d.mb_h = inf.mb_h;
+    d.y_stride = 16 * inf.mb_w;
+    d.uv_stride = 8 * inf.mb_w;
+    d.rgba_stride = 4 * inf.width;
+    d.filter_type = inf.filter_type;
+    d.flags = flags;
+    d.valid = 1;
+    // release host-side copies of the parsed data: the device owns them now
+    std::vector<MbRec>().swap(f.sf.mbs);
+    std::vector<int16_t>().swap(f.sf.blocks);
+    std::vector<uint32_t>().swap(f.sf.row_block0);
+  }
+  hipError_t e = hipMemcpyAsync(b->d_in, h_in, b->in_bytes, hipMemcpyHostToDevice, ctx->stream);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(b->d_desc, b->desc.data(), sizeof(FrameDesc) * (size_t)n, hipMemcpyHostToDevice,
+                       ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  hipHostFree(h_in);
+  if (e != hipSuccess) return fail(WG_STATUS_OUT_OF_MEMORY);
+  return b;
+}
+
+int wg_batch_run(wg_batch* b, void* stream) {
+  if (!b) return WG_STATUS_INVALID_PARAM;
+  if (b->n_valid == 0) return WG_STATUS_OK;
+  hipSetDevice(b->ctx->device);
+  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : b->ctx->stream;
+  if (b->n_runs_pending >= b->timings.size()) {
+    Timing t;
+    for (auto& e : t.ev)
+      if (hipEventCreate(&e) != hipSuccess) return WG_STATUS_OUT_OF_MEMORY;
+    b->timings.push_back(t);
+  }
+  Timing& t = b->timings[b->n_runs_pending++];
+  hipEventRecord(t.ev[0], s);
+  hipError_t e = wg::launch_vp8_recon_filter(b->d_desc, b->n, b->max_mb_w, s);
+  if (e != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
+  hipEventRecord(t.ev[1], s);
+  e = wg::launch_yuv_to_rgba(b->d_desc, nullptr, b->n, b->max_w, b->max_h,
+                             (b->flags & WG_FLAG_NO_FANCY_UPSAMPLING) ? 0 : 1, s);
+  if (e != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
+  hipEventRecord(t.ev[2], s);
+  return WG_STATUS_OK;
+}
+
+int wg_batch_kernel_ms(const wg_batch* bc, float* ms, int n_ms) {
+  wg_batch* b = const_cast<wg_batch*>(bc);
+  if (!b || !ms || n_ms < 2) return WG_STATUS_INVALID_PARAM;
+  ms[0] = ms[1] = 0.f;
+  if (b->n_runs_pending == 0) return WG_STATUS_OK;
+  double s0 = 0, s1 = 0;
+  for (size_t i = 0; i < b->n_runs_pending; ++i) {
+    Timing& t = b->timings[i];
+    if (hipEventSynchronize(t.ev[2]) != hipSuccess) return WG_STATUS_USER_ABORT;
+    float a = 0, c = 0;
+    hipEventElapsedTime(&a, t.ev[0], t.ev[1]);
+    hipEventElapsedTime(&c, t.ev[1], t.ev[2]);
+    s0 += a;
+    s1 += c;
+  }
+  ms[0] = (float)(s0 / b->n_runs_pending);
+  ms[1] = (float)(s1 / b->n_runs_pending);
+  b->n_runs_pending = 0;
+  return WG_STATUS_OK;
+}
+
+int wg_batch_kernel_bytes(const wg_batch* b, double* bytes, int n_bytes) {
+  if (!b || !bytes || n_bytes < 2) return WG_STATUS_INVALID_PARAM;
+  bytes[0] = b->kbytes[0];
+  bytes[1] = b->kbytes[1];
+  return WG_STATUS_OK;
+}
+
+int wg_batch_size(const wg_batch* b) { return b ? b->n : 0; }
+
+int64_t wg_batch_pixels(const wg_batch* b) { return b ? b->pixels : 0; }
+
+int wg_batch_frame_dims(const wg_batch* b, int i, int32_t* width, int32_t* height) {
+  if (!b || i < 0 || i >= b->n) return WG_STATUS_INVALID_PARAM;
+  if (b->fp[i].status != WG_STATUS_OK) return b->fp[i].status;
+  if (width) *width = b->desc[i].width;
+  if (height) *height = b->desc[i].height;
+  return WG_STATUS_OK;
+}
+
+int wg_batch_download_rgba(wg_batch* b, int i, uint8_t* rgba, int stride) {
+  if (!b || i < 0 || i >= b->n || !rgba) return WG_STATUS_INVALID_PARAM;
+  if (b->fp[i].status != WG_STATUS_OK) return b->fp[i].status;
+  const FrameDesc& d = b->desc[i];
+  if (stride < 4 * d.width) return WG_STATUS_INVALID_PARAM;
+  hipSetDevice(b->ctx->device);
+  hipError_t e = hipStreamSynchronize(b->ctx->stream);
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e == hipSuccess)
+    e = hipMemcpy2D(rgba, stride, d.rgba, d.rgba_stride, 4 * (size_t)d.width, d.height, hipMemcpyDeviceToHost);
+  return e == hipSuccess ? WG_STATUS_OK : WG_STATUS_USER_ABORT;
+}
+
+int wg_batch_download_yuv(wg_batch* b, int i, uint8_t* y, uint8_t* u, uint8_t* v) {
+  if (!b || i < 0 || i >= b->n) return WG_STATUS_INVALID_PARAM;
+  if (b->fp[i].status != WG_STATUS_OK) return b->fp[i].status;
+  const FrameDesc& d = b->desc[i];
+  hipSetDevice(b->ctx->device);
+  hipError_t e = hipDeviceSynchronize();
+  const int uw = (d.width + 1) / 2, uh = (d.height + 1) / 2;
+  if (e == hipSuccess && y) e = hipMemcpy2D(y, d.width, d.y, d.y_stride, d.width, d.height, hipMemcpyDeviceToHost);
+  if (e == hipSuccess && u) e = hipMemcpy2D(u, uw, d.u, d.uv_stride, uw, uh, hipMemcpyDeviceToHost);
+  if (e == hipSuccess && v) e = hipMemcpy2D(v, uw, d.v, d.uv_stride, uw, uh, hipMemcpyDeviceToHost);
+  return e == hipSuccess ? WG_STATUS_OK : WG_STATUS_USER_ABORT;
+}
+
+int wg_decode_rgba_batch(wg_ctx* ctx, const uint8_t* const* data, const size_t* sizes, int n,
+                         uint8_t* const* rgba, const int32_t* strides, int32_t* status, int32_t flags) {
+  if (!ctx || !data || !sizes || !rgba || !strides || !status || n <= 0) return WG_STATUS_INVALID_PARAM;
+  wg_batch* b = wg_batch_create(ctx, data, sizes, n, flags, status);
+  if (!b) return WG_STATUS_OUT_OF_MEMORY;
+  int st = wg_batch_run(b, nullptr);
+  if (st == WG_STATUS_OK && hipStreamSynchronize(ctx->stream) != hipSuccess) st = WG_STATUS_USER_ABORT;
+  if (st == WG_STATUS_OK) {
+    for (int i = 0; i < n; ++i) {
+      if (status[i] != WG_STATUS_OK) continue;
+      if (rgba[i] == nullptr || strides[i] < 4 * b->desc[i].width) {
+        status[i] = WG_STATUS_INVALID_PARAM;
+        continue;
+      }
+      status[i] = wg_batch_download_rgba(b, i, rgba[i], strides[i]);
+    }
+  }
+  wg_batch_destroy(b);
+  return st;
+}
+
+int wg_decode_rgba_into(const uint8_t* data, size_t size, uint8_t* rgba, size_t cap, int stride, int flags) {
+  static std::mutex mu;
+  static wg_ctx* ctx = nullptr;
+  if (!data || !rgba) return WG_STATUS_INVALID_PARAM;
+  wg_features f{};
+  int st = wg_get_features(data, size, &f);
+  if (st != WG_STATUS_OK) return st;
+  if (stride < 4 * f.width || (size_t)stride * (f.height - 1) + 4 * (size_t)f.width > cap)
+    return WG_STATUS_INVALID_PARAM;
+  {
+    std::lock_guard<std::mutex> lock(mu);
+    if (!ctx) ctx = wg_ctx_create(0, 1);
+  }
+  if (!ctx) return WG_STATUS_UNSUPPORTED_FEATURE;  // no GPU: no CPU fallback by design
+  const uint8_t* d[1] = {data};
+  const size_t s[1] = {size};
+  uint8_t* o[1] = {rgba};
+  const int32_t str[1] = {stride};
+  int32_t fs[1] = {0};
+  st = wg_decode_rgba_batch(ctx, d, s, 1, o, str, fs, flags);
+  return st != WG_STATUS_OK ? st : fs[0];
+}
+
+int wg_yuv420_to_rgba_device(const uint8_t* y, const uint8_t* u, const uint8_t* v, int y_stride, int uv_stride,
+                             uint8_t* rgba, int rgba_stride, int width, int height, int fancy, void* stream) {
+  if (!y || !u || !v || !rgba || width <= 0 || height <= 0 || rgba_stride < 4 * width || y_stride < width ||
+      uv_stride < (width + 1) / 2 || (y_stride & 7) || (uv_stride & 3) ||
+      (reinterpret_cast<uintptr_t>(y) & 7) || (reinterpret_cast<uintptr_t>(u) & 3) ||
+      (reinterpret_cast<uintptr_t>(v) & 3))
+    return WG_STATUS_INVALID_PARAM;
+  FrameDesc d{};
+  d.y = const_cast<uint8_t*>(y);
+  d.u = const_cast<uint8_t*>(u);
+  d.v = const_cast<uint8_t*>(v);
+  d.rgba = rgba;
+  d.width = width;
+  d.height = height;
+  d.y_stride = y_stride;
+  d.uv_stride = uv_stride;
+  d.rgba_stride = rgba_stride;
+  d.valid = 1;
+  const hipError_t e = wg::launch_yuv_to_rgba(nullptr, &d, 1, width, height, fancy,
+                                              reinterpret_cast<hipStream_t>(stream));
+  return e == hipSuccess ? WG_STATUS_OK : WG_STATUS_INVALID_PARAM;
+}
+
+}  // extern "C"

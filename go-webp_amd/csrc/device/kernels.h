@@ -1,0 +1,21 @@
+// Launchers of the device kernels (host-callable).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+
+#include "../device_format.h"
+
+namespace wg {
+
+// K1: fused reconstruction + loop filter, one 1024-thread workgroup per frame.
+size_t vp8_recon_lds_bytes(int mb_w);
+int vp8_recon_max_mb_w();
+hipError_t launch_vp8_recon_filter(const FrameDesc* d_frames, int n_frames, int max_mb_w,
+                                   hipStream_t stream);
+
+// K2: YUV420 -> RGBA (fancy 9-3-3-1 upsampling or point sampling) over a batch.
+// `single` (when non-null, n_frames == 1) is passed by value instead of d_frames.
+hipError_t launch_yuv_to_rgba(const FrameDesc* d_frames, const FrameDesc* single, int n_frames,
+                              int max_w, int max_h, int fancy, hipStream_t stream);
+
+}  // namespace wg

@@ -1,0 +1,49 @@
+// Layout of the batched, device-resident decode inputs/outputs (shared host/device).
+//
+// One lossy frame in HBM:
+//   MbRec[mb_h][mb_w]          16 B per macroblock (modes, non-zero block mask,
+//                              filter strengths) -- what the reference keeps in
+//                              VP8MBData + VP8FInfo (pkg/vp8/models.go:66-107)
+//   row_block0[mb_h]           index of the first coefficient block of each MB row
+//   blocks[n_nonzero][16]      int16 coefficients of every non-zero 4x4 block in MB
+//                              raster order, blocks 0..15 Y, 16..19 U, 20..23 V,
+//                              stored column-major (blocks[4*c + k] = coeff[4*k + c])
+//                              so lane c of the IDCT reads its column with one load
+//   Y/U/V planes               16*mb_w x 16*mb_h and 8*mb_w x 8*mb_h (MB padded)
+//   RGBA                       width x height x 4
+#pragma once
+#include <stdint.h>
+
+namespace wg {
+
+// MbRec.flags bit fields
+constexpr uint32_t kNzMask = 0x00ffffffu;  // bit b set: 4x4 block b has coefficients
+constexpr int kI4Shift = 24;                // is_i4x4
+constexpr int kYModeShift = 25;             // i16 mode (B_DC/TM/VE/HE = 0..3)
+constexpr int kUVModeShift = 27;            // chroma mode (0..3)
+
+struct MbRec {
+  uint32_t flags;
+  uint32_t imodes_lo;  // 4 bits per i4x4 block, blocks 0..7
+  uint32_t imodes_hi;  // blocks 8..15
+  uint32_t finfo;      // f_limit | f_ilevel << 8 | f_inner << 16 | hev_thresh << 24
+};
+static_assert(sizeof(MbRec) == 16, "MbRec must be 16 bytes");
+
+struct FrameDesc {
+  const MbRec* mbs;
+  const uint32_t* row_block0;
+  const int16_t* blocks;
+  uint8_t* y;
+  uint8_t* u;
+  uint8_t* v;
+  uint8_t* rgba;
+  uint64_t pad0;
+  int32_t width, height, mb_w, mb_h;
+  int32_t y_stride, uv_stride, rgba_stride, filter_type;
+  int32_t flags, valid, pad1, pad2;
+  int32_t pad3[4];
+};
+static_assert(sizeof(FrameDesc) == 128, "FrameDesc must be 128 bytes");
+
+}  // namespace wg

@@ -1,0 +1,39 @@
+// Host-side stages of the WebP decode path: container parsing and the VP8 entropy
+// stage (modes + residual tokens).  Their output is the batched per-macroblock
+// record / coefficient stream consumed by the device kernels (device_format.h).
+#pragma once
+#include <cstddef>
+#include <cstdint>
+#include <vector>
+
+#include "../../../include/gowebp_amd.h"
+#include "../device_format.h"
+
+namespace wg {
+
+// Result of ParseHeadersInternal (pkg/libwebp/decoder/webp.go:300-440) with
+// have_all_data = 1.
+struct Container {
+  int format = 0;  // 1 lossy, 2 lossless
+  int width = 0, height = 0;
+  int has_alpha = 0, has_animation = 0;
+  size_t payload_off = 0, payload_size = 0;  // VP8 / VP8L bitstream
+  size_t alpha_off = 0, alpha_size = 0;      // ALPH chunk payload (0 size = none)
+  int is_lossless = 0;
+};
+
+int parse_container(const uint8_t* data, size_t size, Container* c, wg_features* feat);
+
+// Parsed lossy frame in the device layout.
+struct SparseFrame {
+  wg_vp8_info info{};
+  std::vector<MbRec> mbs;              // mb_w * mb_h, raster order
+  std::vector<uint32_t> row_block0;    // first coefficient block of each MB row
+  std::vector<int16_t> blocks;         // 16 int16 per non-zero 4x4 block, column-major
+};
+
+// Entropy-decode one lossy frame.  `dense` (mb_w*mb_h) and/or `sparse` may be null.
+int vp8_parse(const uint8_t* data, size_t size, int flags, wg_vp8_info* info,
+              wg_vp8_mb* dense, SparseFrame* sparse);
+
+}  // namespace wg

@@ -1,0 +1,295 @@
+"""webp_amd -- Python host binding of the MI355X-native WebP decode path.
+
+Thin ctypes layer over ``libgowebp_amd.so`` (the C ABI in ``include/gowebp_amd.h``).
+It mirrors the reference's public decode surface (``decode.go:8-14``):
+
+* :func:`decode_config`  <- ``webp.DecodeConfig(r)``  (WebPGetFeatures, host only)
+* :func:`decode`         <- ``webp.Decode(r)``        (GPU decode, RGBA ndarray)
+
+plus the batch API the GPU path is built around (:class:`Context`, :class:`Batch`).
+There is deliberately no CPU fallback: if the HIP library or a GPU is missing the
+decode calls raise.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+__all__ = [
+    "Status", "WebPError", "FLAG_BYPASS_FILTERING", "FLAG_NO_FANCY_UPSAMPLING", "Features",
+    "lib", "features", "decode_config", "decode", "Context", "Batch", "vp8_parse", "MB_DTYPE",
+    "VP8Info", "device_count", "yuv420_to_rgba_device",
+]
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libgowebp_amd.so")
+
+FLAG_BYPASS_FILTERING = 1
+FLAG_NO_FANCY_UPSAMPLING = 2
+
+
+class Status:
+    """VP8StatusCode values (pkg/vp8/enums.go:20-31)."""
+    OK = 0
+    OUT_OF_MEMORY = 1
+    INVALID_PARAM = 2
+    BITSTREAM_ERROR = 3
+    UNSUPPORTED_FEATURE = 4
+    SUSPENDED = 5
+    USER_ABORT = 6
+    NOT_ENOUGH_DATA = 7
+    NAMES = {0: "OK", 1: "OUT_OF_MEMORY", 2: "INVALID_PARAM", 3: "BITSTREAM_ERROR",
+             4: "UNSUPPORTED_FEATURE", 5: "SUSPENDED", 6: "USER_ABORT", 7: "NOT_ENOUGH_DATA"}
+
+
+class WebPError(Exception):
+    def __init__(self, status, what=""):
+        self.status = status
+        super().__init__(f"{what}: {Status.NAMES.get(status, status)}")
+
+
+class Features(C.Structure):
+    """WebPBitstreamFeatures (pkg/libwebp/webp/decode.go:33-41)."""
+    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("has_alpha", C.c_int32),
+                ("has_animation", C.c_int32), ("format", C.c_int32)]
+
+
+class VP8Info(C.Structure):
+    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("mb_w", C.c_int32), ("mb_h", C.c_int32),
+                ("filter_type", C.c_int32), ("num_parts", C.c_int32), ("use_segment", C.c_int32),
+                ("frame_offset", C.c_int32)]
+
+
+# wg_vp8_mb: VP8MBData + VP8FInfo (pkg/vp8/models.go:66-107)
+MB_DTYPE = np.dtype([("coeffs", "<i2", (384,)), ("non_zero_y", "<u4"), ("non_zero_uv", "<u4"),
+                     ("is_i4x4", "u1"), ("uvmode", "u1"), ("segment", "u1"), ("skip", "u1"),
+                     ("imodes", "u1", (16,)), ("f_limit", "u1"), ("f_ilevel", "u1"), ("f_inner", "u1"),
+                     ("hev_thresh", "u1")])
+assert MB_DTYPE.itemsize == 800
+
+_lib = None
+
+_P = C.c_void_p
+_SIGS = {
+    "wg_version": (C.c_int, []),
+    "wg_device_count": (C.c_int, []),
+    "wg_get_features": (C.c_int, [_P, C.c_size_t, C.POINTER(Features)]),
+    "wg_decode_rgba_into": (C.c_int, [_P, C.c_size_t, _P, C.c_size_t, C.c_int, C.c_int]),
+    "wg_ctx_create": (_P, [C.c_int, C.c_int]),
+    "wg_ctx_destroy": (None, [_P]),
+    "wg_decode_rgba_batch": (C.c_int, [_P, _P, _P, C.c_int, _P, _P, _P, C.c_int32]),
+    "wg_batch_create": (_P, [_P, _P, _P, C.c_int, C.c_int32, _P]),
+    "wg_batch_destroy": (None, [_P]),
+    "wg_batch_run": (C.c_int, [_P, _P]),
+    "wg_batch_kernel_ms": (C.c_int, [_P, _P, C.c_int]),
+    "wg_batch_kernel_bytes": (C.c_int, [_P, _P, C.c_int]),
+    "wg_batch_size": (C.c_int, [_P]),
+    "wg_batch_frame_dims": (C.c_int, [_P, C.c_int, _P, _P]),
+    "wg_batch_pixels": (C.c_int64, [_P]),
+    "wg_batch_download_rgba": (C.c_int, [_P, C.c_int, _P, C.c_int]),
+    "wg_batch_download_yuv": (C.c_int, [_P, C.c_int, _P, _P, _P]),
+    "wg_yuv420_to_rgba_device": (C.c_int, [_P, _P, _P, C.c_int, C.c_int, _P, C.c_int, C.c_int, C.c_int,
+                                           C.c_int, _P]),
+    "wg_vp8_parse": (C.c_int, [_P, C.c_size_t, C.c_int, C.POINTER(VP8Info), _P]),
+}
+EXPORTED = tuple(_SIGS)
+
+
+def lib():
+    """Load libgowebp_amd.so (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} not built: run `make -C go-webp_amd/csrc` or __graft_entry__.build()")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _buf(data):
+    if isinstance(data, np.ndarray):
+        data = data.tobytes()
+    return bytes(data)
+
+
+def device_count():
+    return lib().wg_device_count()
+
+
+def features(data):
+    f = Features()
+    b = _buf(data)
+    st = lib().wg_get_features(b, len(b), C.byref(f))
+    if st != Status.OK:
+        raise WebPError(st, "wg_get_features")
+    return f
+
+
+def decode_config(data):
+    """Mirror of webp.DecodeConfig: returns (width, height, has_alpha)."""
+    f = features(data)
+    return f.width, f.height, bool(f.has_alpha)
+
+
+def decode(data, flags=0):
+    """Mirror of webp.Decode: GPU decode of one frame to an HxWx4 uint8 RGBA array."""
+    b = _buf(data)
+    f = features(b)
+    out = np.empty((f.height, f.width, 4), np.uint8)
+    st = lib().wg_decode_rgba_into(b, len(b), out.ctypes.data, out.nbytes, 4 * f.width, flags)
+    if st != Status.OK:
+        raise WebPError(st, "wg_decode_rgba_into")
+    return out
+
+
+def vp8_parse(data, flags=0, with_mbs=True):
+    """Host entropy stage only: (VP8Info, structured ndarray of MB_DTYPE or None)."""
+    b = _buf(data)
+    info = VP8Info()
+    L = lib()
+    st = L.wg_vp8_parse(b, len(b), flags, C.byref(info), None)
+    if st != Status.OK:
+        raise WebPError(st, "wg_vp8_parse")
+    if not with_mbs:
+        return info, None
+    mbs = np.zeros(info.mb_w * info.mb_h, MB_DTYPE)
+    st = L.wg_vp8_parse(b, len(b), flags, C.byref(info), mbs.ctypes.data)
+    if st != Status.OK:
+        raise WebPError(st, "wg_vp8_parse")
+    return info, mbs
+
+
+def _ptr_arrays(datas):
+    bufs = [_buf(d) for d in datas]
+    n = len(bufs)
+    ptrs = (C.c_void_p * n)(*[C.cast(C.c_char_p(b), C.c_void_p).value for b in bufs])
+    sizes = (C.c_size_t * n)(*[len(b) for b in bufs])
+    return bufs, ptrs, sizes
+
+
+class Batch:
+    """Device-resident batch: host parse + H2D once, then run() the device path many times."""
+
+    def __init__(self, ctx, datas, flags=0):
+        self._bufs, ptrs, sizes = _ptr_arrays(datas)
+        n = len(self._bufs)
+        self.status = np.zeros(n, np.int32)
+        self._h = lib().wg_batch_create(ctx._h, ptrs, sizes, n, flags, self.status.ctypes.data)
+        if not self._h:
+            raise WebPError(int(self.status.max() or Status.OUT_OF_MEMORY), "wg_batch_create")
+        self.n = n
+        self.flags = flags
+
+    def run(self, stream=None):
+        st = lib().wg_batch_run(self._h, stream)
+        if st != Status.OK:
+            raise WebPError(st, "wg_batch_run")
+
+    def kernel_ms(self):
+        ms = (C.c_float * 2)()
+        st = lib().wg_batch_kernel_ms(self._h, ms, 2)
+        if st != Status.OK:
+            raise WebPError(st, "wg_batch_kernel_ms")
+        return float(ms[0]), float(ms[1])
+
+    def kernel_bytes(self):
+        b = (C.c_double * 2)()
+        lib().wg_batch_kernel_bytes(self._h, b, 2)
+        return float(b[0]), float(b[1])
+
+    @property
+    def pixels(self):
+        return int(lib().wg_batch_pixels(self._h))
+
+    def dims(self, i):
+        w, h = C.c_int32(), C.c_int32()
+        st = lib().wg_batch_frame_dims(self._h, i, C.byref(w), C.byref(h))
+        if st != Status.OK:
+            raise WebPError(st, "wg_batch_frame_dims")
+        return w.value, h.value
+
+    def rgba(self, i):
+        w, h = self.dims(i)
+        out = np.empty((h, w, 4), np.uint8)
+        st = lib().wg_batch_download_rgba(self._h, i, out.ctypes.data, 4 * w)
+        if st != Status.OK:
+            raise WebPError(st, "wg_batch_download_rgba")
+        return out
+
+    def yuv(self, i):
+        w, h = self.dims(i)
+        y = np.empty((h, w), np.uint8)
+        u = np.empty(((h + 1) // 2, (w + 1) // 2), np.uint8)
+        v = np.empty_like(u)
+        st = lib().wg_batch_download_yuv(self._h, i, y.ctypes.data, u.ctypes.data, v.ctypes.data)
+        if st != Status.OK:
+            raise WebPError(st, "wg_batch_download_yuv")
+        return y, u, v
+
+    def close(self):
+        if self._h:
+            lib().wg_batch_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Context:
+    """One decode context per HIP device (wg_ctx)."""
+
+    def __init__(self, device=0, host_threads=0):
+        self._h = lib().wg_ctx_create(device, host_threads)
+        if not self._h:
+            raise WebPError(Status.UNSUPPORTED_FEATURE, f"wg_ctx_create(device={device}) (no GPU?)")
+        self.device = device
+
+    def batch(self, datas, flags=0):
+        return Batch(self, datas, flags)
+
+    def decode_batch(self, datas, flags=0):
+        """Decode a list of WebP files; returns (list of RGBA arrays or None, status array)."""
+        bufs, ptrs, sizes = _ptr_arrays(datas)
+        n = len(bufs)
+        outs, optr, strides = [], (C.c_void_p * n)(), (C.c_int32 * n)()
+        for i, b in enumerate(bufs):
+            try:
+                f = features(b)
+                a = np.empty((f.height, f.width, 4), np.uint8)
+            except WebPError:
+                a = np.empty((1, 1, 4), np.uint8)
+            outs.append(a)
+            optr[i] = a.ctypes.data
+            strides[i] = a.shape[1] * 4
+        status = np.zeros(n, np.int32)
+        st = lib().wg_decode_rgba_batch(self._h, ptrs, sizes, n, optr, strides, status.ctypes.data, flags)
+        if st != Status.OK:
+            raise WebPError(st, "wg_decode_rgba_batch")
+        return [o if s == Status.OK else None for o, s in zip(outs, status)], status
+
+    def close(self):
+        if self._h:
+            lib().wg_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def yuv420_to_rgba_device(y_ptr, u_ptr, v_ptr, y_stride, uv_stride, rgba_ptr, rgba_stride, width, height,
+                          fancy=True, stream=None):
+    """Stage entry point on device pointers (ints), e.g. torch tensors' data_ptr()."""
+    st = lib().wg_yuv420_to_rgba_device(y_ptr, u_ptr, v_ptr, y_stride, uv_stride, rgba_ptr, rgba_stride,
+                                        width, height, 1 if fancy else 0, stream)
+    if st != Status.OK:
+        raise WebPError(st, "wg_yuv420_to_rgba_device")

@@ -1,0 +1,160 @@
+/*
+ * gowebp_amd.h -- C ABI of the MI355X-native WebP decode path.
+ *
+ * This is the drop-in boundary that replaces everything below libwebp's
+ * DecodeInto() in the reference (pkg/libwebp/decoder/webp.go:483-556): the VP8
+ * per-macroblock DSP loop (frame_dec.c.go ReconstructRow/DoFilter,
+ * dsp/dec.c.go) and the YUV420->RGBA emitters (io_dec.c.go EmitFancyRGB /
+ * EmitSampledRGB, dsp/upsampling.c.go, pkg/color/yuv/conversion.go).  The
+ * RIFF/VP8 bool-decoder entropy stage runs on host cores; reconstruction,
+ * in-loop deblocking and colour conversion run as HIP kernels on gfx950.
+ *
+ * Conventions (mirroring libwebp / the reference):
+ *   - every int-returning call returns a wg_status (== VP8StatusCode values,
+ *     pkg/vp8/enums.go:20-31); "first error wins" per frame;
+ *   - no caller pointer is retained after a call returns (cgo pointer rule);
+ *   - plain pointers and sizes only; no HIP or torch types in signatures
+ *     (streams are passed as opaque `void*`, NULL = the context's stream);
+ *   - output RGBA is byte order R,G,B,A, alpha 0xff for opaque lossy input
+ *     (VP8YuvToRgba semantics, dsp/yuv.go).
+ */
+#ifndef GOWEBP_AMD_H_
+#define GOWEBP_AMD_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes: VP8StatusCode (pkg/vp8/enums.go:20-31) ------------------------------ */
+typedef enum {
+  WG_STATUS_OK = 0,
+  WG_STATUS_OUT_OF_MEMORY = 1,
+  WG_STATUS_INVALID_PARAM = 2,
+  WG_STATUS_BITSTREAM_ERROR = 3,
+  WG_STATUS_UNSUPPORTED_FEATURE = 4,
+  WG_STATUS_SUSPENDED = 5,
+  WG_STATUS_USER_ABORT = 6,
+  WG_STATUS_NOT_ENOUGH_DATA = 7
+} wg_status;
+
+/* ---- decode flags: subset of WebPDecoderOptions (pkg/libwebp/webp/decode.go:59-76) ------ */
+#define WG_FLAG_BYPASS_FILTERING    1 /* options.bypass_filtering    */
+#define WG_FLAG_NO_FANCY_UPSAMPLING 2 /* options.no_fancy_upsampling */
+
+/* ---- bitstream features: WebPBitstreamFeatures (pkg/libwebp/webp/decode.go:33-41) ------- */
+typedef struct {
+  int32_t width;
+  int32_t height;
+  int32_t has_alpha;
+  int32_t has_animation;
+  int32_t format; /* 0 = undefined/mixed, 1 = lossy (VP8), 2 = lossless (VP8L) */
+} wg_features;
+
+/* Library version, libwebp-style packed 0xMMmmrr. */
+int wg_version(void);
+
+/* Number of HIP devices visible (0 when no GPU). */
+int wg_device_count(void);
+
+/* Replaces WebPGetFeatures (pkg/libwebp/webp/decode.go:54-56 -> webp.go:764-779,
+ * ParseHeadersInternal webp.go:300-440).  Host only, no GPU needed.
+ * Backs Go's webp.DecodeConfig (decode.go:12-14). */
+int wg_get_features(const uint8_t* data, size_t size, wg_features* out);
+
+/* Replaces WebPDecodeRGBAInto (webp.go:592-594): decode one frame on the GPU
+ * (device 0 context, created lazily) into caller memory of `cap` bytes with
+ * row `stride` (>= 4*width).  flags = WG_FLAG_*.  Backs Go's webp.Decode
+ * (decode.go:8-10).  Fails with UNSUPPORTED_FEATURE when no GPU is present:
+ * there is no CPU fallback for the DSP path. */
+int wg_decode_rgba_into(const uint8_t* data, size_t size, uint8_t* rgba, size_t cap,
+                        int stride, int flags);
+
+/* ---- batched decode: one context per device ------------------------------------------ */
+typedef struct wg_ctx wg_ctx;
+
+/* Create a decode context bound to HIP device `device` (host threads for the entropy
+ * stage = `host_threads`, 0 = hardware concurrency).  NULL on failure. */
+wg_ctx* wg_ctx_create(int device, int host_threads);
+void wg_ctx_destroy(wg_ctx* ctx);
+
+/* Decode n independent frames in one batch: entropy stage on host threads, then one
+ * launch of each DSP kernel over the whole batch.  Per-frame status in status[i]; a bad
+ * frame does not abort the batch.  Returns OK if the batch ran (check status[]). */
+int wg_decode_rgba_batch(wg_ctx* ctx, const uint8_t* const* data, const size_t* sizes, int n,
+                         uint8_t* const* rgba, const int32_t* strides, int32_t* status,
+                         int32_t flags);
+
+/* ---- device-resident batch (benchmarks, tests) -------------------------------------- */
+typedef struct wg_batch wg_batch;
+
+/* Parse n frames on host and upload their coefficient/mode buffers to HBM; allocates the
+ * device YUV planes and RGBA outputs.  Subsequent wg_batch_run() calls execute only the
+ * device path (inputs resident in HBM).  NULL on failure (status[] says why per frame). */
+wg_batch* wg_batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t* sizes, int n,
+                          int32_t flags, int32_t* status);
+void wg_batch_destroy(wg_batch* b);
+
+/* Run the device DSP path for the whole batch on `stream` (NULL = ctx stream):
+ * K1 reconstruct+deblock wavefront, K2 YUV420->RGBA.  Kernel durations of the last run
+ * (HIP events on that stream) are available from wg_batch_kernel_ms(). */
+int wg_batch_run(wg_batch* b, void* stream);
+
+/* ms[0] = reconstruct+filter kernel, ms[1] = yuv->rgba kernel (last run). */
+int wg_batch_kernel_ms(const wg_batch* b, float* ms, int n_ms);
+
+/* Algorithmic HBM bytes per launch of each kernel. */
+int wg_batch_kernel_bytes(const wg_batch* b, double* bytes, int n_bytes);
+
+int wg_batch_size(const wg_batch* b);
+int wg_batch_frame_dims(const wg_batch* b, int i, int32_t* width, int32_t* height);
+int64_t wg_batch_pixels(const wg_batch* b);
+
+/* Copy results of frame i back to host: RGBA (stride >= 4*width) and/or the cropped
+ * Y/U/V planes (strides width, (width+1)/2). */
+int wg_batch_download_rgba(wg_batch* b, int i, uint8_t* rgba, int stride);
+int wg_batch_download_yuv(wg_batch* b, int i, uint8_t* y, uint8_t* u, uint8_t* v);
+
+/* ---- stage entry point: YUV420 -> RGBA on device pointers ---------------------------- */
+/* Fancy (fancy!=0, UpsampleRgbaLinePair, upsampling.c.go:43-107) or point-sampled
+ * (EmitSampledRGB, io_dec.c.go:53-59) conversion of one frame; all pointers are device
+ * pointers.  Asynchronous on `stream`. */
+int wg_yuv420_to_rgba_device(const uint8_t* y, const uint8_t* u, const uint8_t* v,
+                             int y_stride, int uv_stride, uint8_t* rgba, int rgba_stride,
+                             int width, int height, int fancy, void* stream);
+
+/* ---- host entropy stage in the libwebp data model (tests / CPU checker) --------------- */
+/* One macroblock as libwebp keeps it after parsing: VP8MBData (pkg/vp8/models.go:89-107)
+ * plus the VP8FInfo filter strengths (models.go:66-71). */
+typedef struct {
+  int16_t coeffs[384];  /* dequantized, de-zigzagged, int16-wrapped; Y 0..15, U 16..19, V 20..23 */
+  uint32_t non_zero_y;  /* 2-bit transform codes, block 0 in bits 31:30 (NzCodeBits)           */
+  uint32_t non_zero_uv; /* U codes bits 7:0, V codes bits 15:8                                  */
+  uint8_t is_i4x4;
+  uint8_t uvmode;       /* DC=0 TM=1 V=2 H=3                                                    */
+  uint8_t segment;
+  uint8_t skip;
+  uint8_t imodes[16];   /* i4x4: B_* modes 0..9 raster order; i16: imodes[0] = ymode           */
+  uint8_t f_limit, f_ilevel, f_inner, hev_thresh;
+} wg_vp8_mb;
+
+typedef struct {
+  int32_t width, height;     /* picture size                                             */
+  int32_t mb_w, mb_h;        /* macroblocks                                              */
+  int32_t filter_type;       /* 0 none, 1 simple, 2 complex (after bypass_filtering)    */
+  int32_t num_parts;         /* token partitions                                         */
+  int32_t use_segment;
+  int32_t frame_offset;      /* byte offset of the VP8 frame inside `data`               */
+} wg_vp8_info;
+
+/* Parse container + VP8 headers + modes + residual tokens of a lossy frame on the host.
+ * `mbs` (mb_w*mb_h entries, raster order) may be NULL to only fill `info`. */
+int wg_vp8_parse(const uint8_t* data, size_t size, int flags, wg_vp8_info* info, wg_vp8_mb* mbs);
+
+#ifdef __cplusplus
+}  /* extern "C" */
+#endif
+
+#endif /* GOWEBP_AMD_H_ */

@@ -1,0 +1,77 @@
+"""ctypes binding of the CPU oracle (oracle/build/liboracle.so) + golden-fixture loaders.
+
+Test infrastructure: only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+leg use this module.
+"""
+import ctypes as C
+import glob
+import json
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_SO = os.path.join(ROOT, "oracle", "build", "liboracle.so")
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+_lib = None
+
+
+def oracle():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(ORACLE_SO):
+            subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+        L = C.CDLL(ORACLE_SO)
+        P = C.c_void_p
+        L.oracle_vp8_decode.argtypes = [P, P, P, P, P, P, C.c_int]
+        L.oracle_vp8_reconstruct.argtypes = [P, P, P, P, P]
+        L.oracle_yuv_to_rgba_fancy.argtypes = [P, C.c_int, P, P, C.c_int, P, C.c_int, C.c_int, C.c_int]
+        L.oracle_yuv_to_rgba_point.argtypes = [P, C.c_int, P, P, C.c_int, P, C.c_int, C.c_int, C.c_int]
+        L.oracle_transform_block.argtypes = [P, P, C.c_int]
+        L.oracle_transform_block.restype = None
+        _lib = L
+    return _lib
+
+
+def oracle_decode(info, mbs, fancy=True):
+    """CPU decode of a parsed frame -> dict(y, u, v, rgba)."""
+    w, h = info.width, info.height
+    uw, uh = (w + 1) // 2, (h + 1) // 2
+    y = np.empty((h, w), np.uint8)
+    u = np.empty((uh, uw), np.uint8)
+    v = np.empty((uh, uw), np.uint8)
+    rgba = np.empty((h, w, 4), np.uint8)
+    st = oracle().oracle_vp8_decode(C.addressof(info), mbs.ctypes.data, y.ctypes.data, u.ctypes.data,
+                                    v.ctypes.data, rgba.ctypes.data, 1 if fancy else 0)
+    assert st == 0
+    return dict(y=y, u=u, v=v, rgba=rgba)
+
+
+def oracle_yuv_to_rgba(y, u, v, fancy=True):
+    h, w = y.shape
+    rgba = np.empty((h, w, 4), np.uint8)
+    y = np.ascontiguousarray(y); u = np.ascontiguousarray(u); v = np.ascontiguousarray(v)
+    fn = oracle().oracle_yuv_to_rgba_fancy if fancy else oracle().oracle_yuv_to_rgba_point
+    fn(y.ctypes.data, y.strides[0], u.ctypes.data, v.ctypes.data, u.strides[0], rgba.ctypes.data, 4 * w, w, h)
+    return rgba
+
+
+def manifest():
+    with open(os.path.join(GOLDEN, "manifest.json")) as f:
+        return json.load(f)
+
+
+def lossy_cases():
+    return sorted(os.path.basename(p)[:-5] for p in glob.glob(os.path.join(GOLDEN, "lossy", "*.webp")))
+
+
+def load_lossy(name):
+    with open(os.path.join(GOLDEN, "lossy", name + ".webp"), "rb") as f:
+        data = f.read()
+    return data, dict(np.load(os.path.join(GOLDEN, "lossy", name + ".npz")))
+
+
+def bench_files(prefix):
+    return sorted(glob.glob(os.path.join(GOLDEN, "bench", prefix + "_s*.webp")))
