@@ -94,6 +94,7 @@ struct wg_batch {
   std::vector<FrameParse> fp;
   std::vector<FrameDesc> desc;
   FrameDesc* d_desc = nullptr;
+  int* d_err = nullptr;
   uint8_t* d_in = nullptr;
   uint8_t* d_planes = nullptr;
   uint8_t* d_rgba = nullptr;
@@ -160,6 +161,7 @@ void wg_batch_destroy(wg_batch* b) {
     for (auto& e : t.ev)
       if (e) hipEventDestroy(e);
   if (b->d_desc) hipFree(b->d_desc);
+  if (b->d_err) hipFree(b->d_err);
   if (b->d_in) hipFree(b->d_in);
   if (b->d_planes) hipFree(b->d_planes);
   if (b->d_rgba) hipFree(b->d_rgba);
@@ -225,7 +227,8 @@ wg_batch* wg_batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t*
   };
   if (hipMalloc(&b->d_in, b->in_bytes) != hipSuccess || hipMalloc(&b->d_planes, b->plane_bytes) != hipSuccess ||
       hipMalloc(&b->d_rgba, b->rgba_bytes) != hipSuccess ||
-      hipMalloc(&b->d_desc, sizeof(FrameDesc) * (size_t)n) != hipSuccess)
+      hipMalloc(&b->d_desc, sizeof(FrameDesc) * (size_t)n) != hipSuccess ||
+      hipMalloc(&b->d_err, sizeof(int)) != hipSuccess || hipMemset(b->d_err, 0, sizeof(int)) != hipSuccess)
     return fail(WG_STATUS_OUT_OF_MEMORY);
   // stage inputs in pinned memory, one H2D copy
   uint8_t* h_in = nullptr;
@@ -285,7 +288,7 @@ int wg_batch_run(wg_batch* b, void* stream) {
   }
   Timing& t = b->timings[b->n_runs_pending++];
   hipEventRecord(t.ev[0], s);
-  hipError_t e = wg::launch_vp8_recon_filter(b->d_desc, b->n, b->max_mb_w, s);
+  hipError_t e = wg::launch_vp8_recon_filter(b->d_desc, b->n, b->max_mb_w, b->d_err, s);
   if (e != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
   hipEventRecord(t.ev[1], s);
   e = wg::launch_yuv_to_rgba(b->d_desc, nullptr, b->n, b->max_w, b->max_h,
@@ -310,6 +313,8 @@ int wg_batch_kernel_ms(const wg_batch* bc, float* ms, int n_ms) {
     s0 += a;
     s1 += c;
   }
+  int err = 0;
+  if (hipMemcpy(&err, b->d_err, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess || err) return WG_STATUS_USER_ABORT;
   ms[0] = (float)(s0 / b->n_runs_pending);
   ms[1] = (float)(s1 / b->n_runs_pending);
   b->n_runs_pending = 0;
@@ -343,6 +348,9 @@ int wg_batch_download_rgba(wg_batch* b, int i, uint8_t* rgba, int stride) {
   hipSetDevice(b->ctx->device);
   hipError_t e = hipStreamSynchronize(b->ctx->stream);
   if (e == hipSuccess) e = hipDeviceSynchronize();
+  int err = 0;
+  if (e == hipSuccess) e = hipMemcpy(&err, b->d_err, sizeof(int), hipMemcpyDeviceToHost);
+  if (e == hipSuccess && err) return WG_STATUS_USER_ABORT;
   if (e == hipSuccess)
     e = hipMemcpy2D(rgba, stride, d.rgba, d.rgba_stride, 4 * (size_t)d.width, d.height, hipMemcpyDeviceToHost);
   return e == hipSuccess ? WG_STATUS_OK : WG_STATUS_USER_ABORT;

@@ -7,29 +7,33 @@
 //   intra predictors     pkg/libwebp/dsp/dec.c.go:178-474 (indexed by mode enum)
 //   loop filters         pkg/libwebp/dsp/dec.c.go:484-682
 //
-// Geometry: one 1024-thread workgroup per frame; wave w owns MB rows w, w+16, ...
-// (16 rows in flight).  Row y at column x waits (LDS progress counter) until row
-// y-1 has finished column min(x+1, mb_w-1): the classic t = x + 2y wavefront, since
-// both intra prediction (top-right samples) and the loop filter (MB (x+1,y-1)'s
-// left-edge writes) reach one MB up and to the right.
+// Geometry.  One 1024-thread workgroup per frame.  Wave w owns MB-row PAIRS
+// k = w, w+16, ...: half-wave 0 (lanes 0..31) decodes row 2k at column i while half 1
+// (lanes 32..63) decodes row 2k+1 at column i-2 -- the t = x + 2y wavefront, since
+// intra prediction (top-right samples) and the loop filter (MB (x+1,y-1)'s left-edge
+// writes) both reach one MB up and to the right.  Inside a pair the lockstep skew
+// satisfies the dependency; across pairs an LDS progress counter does (32 MB rows in
+// flight per frame).
 //
-// One macroblock = one wave: lane l owns pixel row (l & 3) of 4x4 block (l >> 2)
-// (a dword of the 16x16 luma block).  The IDCT's vertical pass runs per column
-// lane, a quad DPP transpose hands rows to lanes, the horizontal pass produces the
-// lane's 4 residuals.  Residuals are prediction-independent (STORE: dst + (v>>3)),
-// so all 16 blocks are transformed at once; i4x4 prediction then walks its
-// 10-step intra wavefront (block t = bx + 2*by) in the LDS workspace.
+// One macroblock = 32 lanes.  Lane l owns column/row q = l&3 of luma 4x4 blocks l>>2 and
+// (l>>2)+8 and of chroma block 16+(l>>2).  IDCT (TransformOne, all blocks at once since
+// the residual (v>>3) does not depend on the prediction): vertical pass per column lane,
+// quad DPP transpose, horizontal pass.  i16/chroma prediction: one pixel row per lane.
+// i4x4 prediction walks the 10-step intra wavefront (block t = bx + 2by) with ONE PIXEL
+// PER LANE: each pixel of each predictor is a 3-tap recipe of edge samples
+// (pred4_table.inc, generated from dec.c.go's DST() formulas), so no lane branches on
+// the mode.  A non-zero block always goes through TransformOne: TransformAC3 /
+// TransformDC / TransformDCUV are exact special cases of it
+// (tests/test_oracle.py::test_transform_shortcuts_exact).
 //
-// A non-zero 4x4 block always goes through TransformOne: libwebp's TransformAC3 /
-// TransformDC / TransformDCUV are exact special cases of it on their coefficient
-// patterns (tests/test_oracle.py::test_transform_shortcuts_exact), and TransformOne
-// of an all-zero block is the identity.
+// Loop filter (per MB, libwebp edge order): lanes 0..15 luma lines, 16..31 chroma
+// lines; branch-free FilterLoop26/24 / simple-filter math in a per-MB LDS window.
 //
-// Cross-wave data lives only in LDS (top samples `ytop`, filtered bottom rows
-// `fbot`, progress counters); every HBM byte of the Y/U/V planes is written exactly
-// once, when it is final.  Prediction uses UNFILTERED neighbours (ytop and the
-// recon workspace), the filter works in a separate per-wave window, exactly as
-// libwebp keeps yuv_t/yuv_b apart from its filtered cache rows.
+// Memory.  Cross-MB state lives in LDS only: the unfiltered top samples `ytop`
+// (VP8TopSamples), the final bottom rows `fbot` of each MB column for the next row's
+// top-edge filter, progress counters.  Every HBM byte of the Y/U/V planes is written
+// exactly once, when final.  MB records and coefficients are software-pipelined:
+// record x+2 and coefficients x+1 are in flight while MB x is processed.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -39,8 +43,10 @@
 namespace wg {
 namespace {
 
+#include "pred4_table.inc"
+
 constexpr int kWaves = 16;
-constexpr int BPS = 32;  // libwebp workspace stride
+constexpr int BPS = 32;  // libwebp workspace stride (vp8/constants.go BPS)
 constexpr int Y_OFF = BPS * 1 + 8;
 constexpr int U_OFF = Y_OFF + BPS * 16 + BPS;
 constexpr int V_OFF = U_OFF + 16;
@@ -49,71 +55,63 @@ constexpr int kWsBytes = 832;  // YUV_SIZE = BPS*17 + BPS*9
 constexpr int FWY = 20, FWC = 12;
 constexpr int kFwY = 0, kFwU = 400, kFwV = 544;
 constexpr int kFwBytes = 704;
-constexpr int kLeftBytes = 32;  // contiguous unfiltered left columns: Y 16, U 8, V 8
-constexpr int kWaveBytes = kWsBytes + kFwBytes + kLeftBytes;  // 1568
-constexpr int kProgBytes = 64;
+constexpr int kLeftBytes = 32;   // contiguous unfiltered left columns: Y 16, U 8, V 8
+constexpr int kResBytes = 512;   // i4x4 residuals, int16 [16 blocks][16 px]
+constexpr int kSlotBytes = kWsBytes + kFwBytes + kLeftBytes + kResBytes;  // 2080 per MB row
+constexpr int kProgBytes = 64;  // reserved (progress lives in a static __shared__ array)
+constexpr int kTabBytes = 640;
+constexpr int kHdrBytes = kProgBytes + kTabBytes;
 constexpr int kColBytes = 32 + 128;  // ytop (y16 u8 v8) + fbot (Y 4x16, U 4x8, V 4x8)
 
 __device__ __forceinline__ void lds_sync() {
-  // LDS ops of one wave complete in order; this makes every lane's earlier LDS
-  // write visible to every lane's later LDS read and stops compiler reordering.
+  // LDS ops of one wave complete in order; this makes every lane's earlier LDS write
+  // visible to every lane's later LDS read and stops compiler reordering.
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
 __device__ __forceinline__ int clamp255(int v) { return min(max(v, 0), 255); }
-__device__ __forceinline__ int avg3(int a, int b, int c) { return (a + 2 * b + c + 2) >> 2; }
-__device__ __forceinline__ int avg2(int a, int b) { return (a + b + 1) >> 1; }
 __device__ __forceinline__ uint32_t pack4(int a, int b, int c, int d) {
   return (uint32_t)a | ((uint32_t)b << 8) | ((uint32_t)c << 16) | ((uint32_t)d << 24);
 }
 __device__ __forceinline__ int byte_of(uint32_t w, int i) { return (w >> (8 * i)) & 0xff; }
-// 4 bytes starting at byte offset o (0..7) of the 12-byte little-endian string w0|w1|w2
-__device__ __forceinline__ uint32_t pick4(uint32_t w0, uint32_t w1, uint32_t w2, int o) {
-  const uint32_t lo = o < 4 ? w0 : w1;
-  const uint32_t hi = o < 4 ? w1 : w2;
-  const int s = o & 3;
-  return s ? ((lo >> (8 * s)) | (hi << (32 - 8 * s))) : lo;
-}
+__device__ __forceinline__ uint32_t ld32(const uint8_t* p) { return *reinterpret_cast<const uint32_t*>(p); }
+__device__ __forceinline__ void st32(uint8_t* p, uint32_t v) { *reinterpret_cast<uint32_t*>(p) = v; }
 
-// 32-bit wrapping MUL1/MUL2 (dsp.h.go WEBP_TRANSFORM_AC3_MUL1/2).  |a| < 2^23 for
-// any int16 input, so the 24-bit multiplier gives the exact low 32 bits.
+// 32-bit wrapping MUL1/MUL2 (dsp.h.go WEBP_TRANSFORM_AC3_MUL1/2).  |a| < 2^23 for any
+// int16 input, so the 24-bit multiplier gives the exact low 32 bits of a*c.
 __device__ __forceinline__ int mul1(int a) { return (__mul24(a, 20091) >> 16) + a; }
 __device__ __forceinline__ int mul2(int a) { return __mul24(a, 35468) >> 16; }
 
-// quad transpose helpers (DPP quad_perm)
 __device__ __forceinline__ int dpp_swap1(int v) { return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, true); }
 __device__ __forceinline__ int dpp_swap2(int v) { return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, true); }
 
-// IDCT of one 4x4 block spread over a lane quad.  In: column q = lane&3 of the
-// coefficients (c0..c3 = in[q], in[4+q], in[8+q], in[12+q]).  Out: residuals
-// (v >> 3) of pixel row q, x = 0..3.  TransformOne (dec.c.go:49-88).
-__device__ __forceinline__ void idct_quad(int q, int c0, int c1, int c2, int c3, int r[4]) {
+// TransformOne (dec.c.go:49-88) of a 4x4 block spread over a lane quad.  In: column q of
+// the coefficients (c0..c3 = in[q], in[4+q], in[8+q], in[12+q]).  Out: residuals
+// (v >> 3) of pixel row q, x = 0..3.
+__device__ __forceinline__ void idct_quad(int q, uint2 cv, int r[4]) {
+  const int c0 = (int16_t)(cv.x & 0xffff), c1 = (int16_t)(cv.x >> 16);
+  const int c2 = (int16_t)(cv.y & 0xffff), c3 = (int16_t)(cv.y >> 16);
   int t[4];
   {
     const int a = c0 + c2;
     const int b = c0 - c2;
     const int c = mul2(c1) - mul1(c3);
     const int d = mul1(c1) + mul2(c3);
-    t[0] = a + d;  // tmp[4q + 0]
+    t[0] = a + d;
     t[1] = b + c;
     t[2] = b - c;
     t[3] = a - d;
   }
-  // transpose: lane q ends with u[c] = tmp[4c + q]
-  {
+  {  // quad transpose: lane q ends with u[c] = tmp[4c + q]
     const bool o1 = q & 1;
-    int s = o1 ? t[0] : t[1];
-    int g = dpp_swap1(s);
+    int g = dpp_swap1(o1 ? t[0] : t[1]);
     if (o1) t[0] = g; else t[1] = g;
-    s = o1 ? t[2] : t[3];
-    g = dpp_swap1(s);
+    g = dpp_swap1(o1 ? t[2] : t[3]);
     if (o1) t[2] = g; else t[3] = g;
     const bool o2 = q & 2;
-    s = o2 ? t[0] : t[2];
-    g = dpp_swap2(s);
+    g = dpp_swap2(o2 ? t[0] : t[2]);
     if (o2) t[0] = g; else t[2] = g;
-    s = o2 ? t[1] : t[3];
-    g = dpp_swap2(s);
+    g = dpp_swap2(o2 ? t[1] : t[3]);
     if (o2) t[1] = g; else t[3] = g;
   }
   const int dc = t[0] + 4;
@@ -140,73 +138,15 @@ __device__ __forceinline__ int check_mode(int mb_x, int mb_y, int mode) {  // fr
   return mode;
 }
 
-// Row `r` (0..3) of a 4x4 intra predictor (dec.c.go:261-410), mode = B_* enum.
-// Edge samples: X = top-left, A..H = top row + top-right, I..L = left column.
-__device__ uint32_t pred4_row(int mode, int r, uint32_t top_lo, uint32_t top_hi, int X, uint32_t left) {
-  const int A = byte_of(top_lo, 0), B = byte_of(top_lo, 1), C = byte_of(top_lo, 2), D = byte_of(top_lo, 3);
-  const int E = byte_of(top_hi, 0), F = byte_of(top_hi, 1), G = byte_of(top_hi, 2), H = byte_of(top_hi, 3);
-  const int I = byte_of(left, 0), J = byte_of(left, 1), K = byte_of(left, 2), L = byte_of(left, 3);
-  switch (mode) {
-    case 0: {  // DC4
-      const int dc = (A + B + C + D + I + J + K + L + 4) >> 3;
-      return (uint32_t)dc * 0x01010101u;
-    }
-    case 1: {  // TM4
-      const int ly = byte_of(left, r);
-      return pack4(clamp255(A + ly - X), clamp255(B + ly - X), clamp255(C + ly - X), clamp255(D + ly - X));
-    }
-    case 2:  // VE4
-      return pack4(avg3(X, A, B), avg3(A, B, C), avg3(B, C, D), avg3(C, D, E));
-    case 3: {  // HE4
-      const int lm = r == 0 ? X : byte_of(left, r - 1);
-      const int lp = r == 3 ? L : byte_of(left, r + 1);
-      return (uint32_t)avg3(lm, byte_of(left, r), lp) * 0x01010101u;
-    }
-    case 4: {  // RD4: row r = d[4-r .. 7-r], d[k] = avg3(Z[k-1], Z[k], Z[k+1]), Z = L K J I X A B C D
-      const uint32_t w0 = pack4(avg3(L, K, J), avg3(K, J, I), avg3(J, I, X), avg3(I, X, A));
-      const uint32_t w1 = pack4(avg3(X, A, B), avg3(A, B, C), avg3(B, C, D), 0);
-      return pick4(w0, w1, 0, 3 - r);
-    }
-    case 5: {  // VR4
-      uint32_t w0, w1;
-      if (r & 1) {
-        w0 = pack4(avg3(K, J, I), avg3(I, X, A), avg3(X, A, B), avg3(A, B, C));
-        w1 = (uint32_t)avg3(B, C, D);
-      } else {
-        w0 = pack4(avg3(J, I, X), avg2(X, A), avg2(A, B), avg2(B, C));
-        w1 = (uint32_t)avg2(C, D);
-      }
-      return pick4(w0, w1, 0, r < 2 ? 1 : 0);
-    }
-    case 6: {  // LD4: row r = d[r .. r+3], d[k] = avg3(T[k], T[k+1], T[k+2]), T[8] = H
-      const uint32_t w0 = pack4(avg3(A, B, C), avg3(B, C, D), avg3(C, D, E), avg3(D, E, F));
-      const uint32_t w1 = pack4(avg3(E, F, G), avg3(F, G, H), avg3(G, H, H), 0);
-      return pick4(w0, w1, 0, r);
-    }
-    case 7: {  // VL4
-      uint32_t w0, w1;
-      if (r & 1) {
-        w0 = pack4(avg3(A, B, C), avg3(B, C, D), avg3(C, D, E), avg3(D, E, F));
-        w1 = (uint32_t)avg3(F, G, H);
-      } else {
-        w0 = pack4(avg2(A, B), avg2(B, C), avg2(C, D), avg2(D, E));
-        w1 = (uint32_t)avg3(E, F, G);
-      }
-      return pick4(w0, w1, 0, r >> 1);
-    }
-    case 8: {  // HD4: row r = S[6-2r .. 9-2r]
-      const uint32_t w0 = pack4(avg2(L, K), avg3(L, K, J), avg2(K, J), avg3(K, J, I));
-      const uint32_t w1 = pack4(avg2(J, I), avg3(J, I, X), avg2(I, X), avg3(I, X, A));
-      const uint32_t w2 = pack4(avg3(X, A, B), avg3(A, B, C), 0, 0);
-      return pick4(w0, w1, w2, 6 - 2 * r);
-    }
-    default: {  // 9, HU4: row r = U[2r .. 2r+3]
-      const uint32_t w0 = pack4(avg2(I, J), avg3(I, J, K), avg2(J, K), avg3(J, K, L));
-      const uint32_t w1 = pack4(avg2(K, L), avg3(K, L, L), L, L);
-      const uint32_t w2 = (uint32_t)L * 0x01010101u;
-      return pick4(w0, w1, w2, 2 * r);
-    }
-  }
+// One pixel row of the 16x16 luma / 8x8 chroma predictors (DC*, TM, VE, HE;
+// dec.c.go:178-249, 422-474); `dc` is the DC value computed by the caller.
+__device__ __forceinline__ uint32_t pred_row(int mode, uint32_t top, int left, int tl, int dc) {
+  if (mode == 2) return top;                                 // VE
+  if (mode == 3) return (uint32_t)left * 0x01010101u;        // HE
+  if (mode == 1)                                             // TM
+    return pack4(clamp255(byte_of(top, 0) + left - tl), clamp255(byte_of(top, 1) + left - tl),
+                 clamp255(byte_of(top, 2) + left - tl), clamp255(byte_of(top, 3) + left - tl));
+  return (uint32_t)dc * 0x01010101u;                         // DC variants
 }
 
 // ---------------------------------------------------------------- loop filter
@@ -215,450 +155,493 @@ struct Line { int p3, p2, p1, p0, q0, q1, q2, q3; };
 __device__ __forceinline__ int sclip1(int v) { return min(max(v, -128), 127); }
 __device__ __forceinline__ int sclip2(int v) { return min(max(v, -16), 15); }
 
-__device__ __forceinline__ void do_filter2(Line& l) {  // DoFilter2_C (dec.c.go:484-491)
-  const int a = 3 * (l.q0 - l.p0) + sclip1(l.p1 - l.q1);
-  const int a1 = sclip2((a + 4) >> 3);
-  const int a2 = sclip2((a + 3) >> 3);
-  l.p0 = clamp255(l.p0 + a2);
-  l.q0 = clamp255(l.q0 - a1);
-}
-__device__ __forceinline__ void do_filter4(Line& l) {  // DoFilter4_C (:494-504)
-  const int a = 3 * (l.q0 - l.p0);
-  const int a1 = sclip2((a + 4) >> 3);
-  const int a2 = sclip2((a + 3) >> 3);
-  const int a3 = (a1 + 1) >> 1;
-  l.p1 = clamp255(l.p1 + a3);
-  l.p0 = clamp255(l.p0 + a2);
-  l.q0 = clamp255(l.q0 - a1);
-  l.q1 = clamp255(l.q1 - a3);
-}
-__device__ __forceinline__ void do_filter6(Line& l) {  // DoFilter6_C (:507-521)
-  const int a = sclip1(3 * (l.q0 - l.p0) + sclip1(l.p1 - l.q1));
-  const int a1 = (27 * a + 63) >> 7;
-  const int a2 = (18 * a + 63) >> 7;
-  const int a3 = (9 * a + 63) >> 7;
-  l.p2 = clamp255(l.p2 + a3);
-  l.p1 = clamp255(l.p1 + a2);
-  l.p0 = clamp255(l.p0 + a1);
-  l.q0 = clamp255(l.q0 - a1);
-  l.q1 = clamp255(l.q1 - a2);
-  l.q2 = clamp255(l.q2 - a3);
-}
-__device__ __forceinline__ bool needs_filter(const Line& l, int t) {  // NeedsFilter_C (:530-533)
-  return 4 * abs(l.p0 - l.q0) + abs(l.p1 - l.q1) <= t;
-}
-__device__ __forceinline__ bool needs_filter2(const Line& l, int t, int it) {  // NeedsFilter2_C (:537-545)
-  if (4 * abs(l.p0 - l.q0) + abs(l.p1 - l.q1) > t) return false;
-  return abs(l.p3 - l.p2) <= it && abs(l.p2 - l.p1) <= it && abs(l.p1 - l.p0) <= it &&
-         abs(l.q3 - l.q2) <= it && abs(l.q2 - l.q1) <= it && abs(l.q1 - l.q0) <= it;
-}
-__device__ __forceinline__ bool hev(const Line& l, int thresh) {  // Hev (:523-526)
-  return abs(l.p1 - l.p0) > thresh || abs(l.q1 - l.q0) > thresh;
-}
-
-// kind: 0 simple (NeedsFilter + DoFilter2), 1 complex MB edge (FilterLoop26),
-// 2 complex inner edge (FilterLoop24).  thresh2 = 2*thresh + 1.
-__device__ __forceinline__ void filter_line(Line& l, int kind, int thresh2, int ilevel, int hev_t) {
-  if (kind == 0) {
-    if (needs_filter(l, thresh2)) do_filter2(l);
-  } else if (needs_filter2(l, thresh2, ilevel)) {
-    if (hev(l, hev_t)) do_filter2(l);
-    else if (kind == 1) do_filter6(l);
-    else do_filter4(l);
+// KIND 0: simple (NeedsFilter + DoFilter2, dec.c.go:552-586);
+// KIND 1: complex MB edge (FilterLoop26: hev ? DoFilter2 : DoFilter6, :592-606);
+// KIND 2: complex inner edge (FilterLoop24: hev ? DoFilter2 : DoFilter4, :608-622).
+// Branch-free: every variant is computed and selected.  t2 = 2*thresh + 1.
+template <int KIND>
+__device__ __forceinline__ void filter_line(Line& l, int t2, int it, int hev_t) {
+  const int d0 = l.q0 - l.p0;
+  const int sp = sclip1(l.p1 - l.q1);
+  const bool edge_ok = 4 * abs(d0) + abs(l.p1 - l.q1) <= t2;
+  // DoFilter2
+  const int a = 3 * d0 + sp;
+  const int f2p0 = clamp255(l.p0 + sclip2((a + 3) >> 3));
+  const int f2q0 = clamp255(l.q0 - sclip2((a + 4) >> 3));
+  if (KIND == 0) {
+    l.p0 = edge_ok ? f2p0 : l.p0;
+    l.q0 = edge_ok ? f2q0 : l.q0;
+    return;
+  }
+  const int in_p = max(max(abs(l.p3 - l.p2), abs(l.p2 - l.p1)), abs(l.p1 - l.p0));
+  const int in_q = max(max(abs(l.q3 - l.q2), abs(l.q2 - l.q1)), abs(l.q1 - l.q0));
+  const bool on = edge_ok && max(in_p, in_q) <= it;
+  const bool hv = max(abs(l.p1 - l.p0), abs(l.q1 - l.q0)) > hev_t;
+  const bool f2 = on && hv, fx = on && !hv;
+  if (KIND == 1) {  // DoFilter6
+    const int w = sclip1(a);
+    const int a1 = (27 * w + 63) >> 7, a2 = (18 * w + 63) >> 7, a3 = (9 * w + 63) >> 7;
+    const int np2 = clamp255(l.p2 + a3), np1 = clamp255(l.p1 + a2), np0 = clamp255(l.p0 + a1);
+    const int nq0 = clamp255(l.q0 - a1), nq1 = clamp255(l.q1 - a2), nq2 = clamp255(l.q2 - a3);
+    l.p2 = fx ? np2 : l.p2;
+    l.p1 = fx ? np1 : l.p1;
+    l.q1 = fx ? nq1 : l.q1;
+    l.q2 = fx ? nq2 : l.q2;
+    l.p0 = fx ? np0 : (f2 ? f2p0 : l.p0);
+    l.q0 = fx ? nq0 : (f2 ? f2q0 : l.q0);
+  } else {  // DoFilter4
+    const int a4 = 3 * d0;
+    const int a1 = sclip2((a4 + 4) >> 3), a2 = sclip2((a4 + 3) >> 3), a3 = (a1 + 1) >> 1;
+    const int np1 = clamp255(l.p1 + a3), np0 = clamp255(l.p0 + a2);
+    const int nq0 = clamp255(l.q0 - a1), nq1 = clamp255(l.q1 - a3);
+    l.p1 = fx ? np1 : l.p1;
+    l.q1 = fx ? nq1 : l.q1;
+    l.p0 = fx ? np0 : (f2 ? f2p0 : l.p0);
+    l.q0 = fx ? nq0 : (f2 ? f2q0 : l.q0);
   }
 }
 
-// Filter across a vertical edge at column e of a window row (horizontal step).
-__device__ __forceinline__ void filter_row(uint8_t* row_at_e /* &win[row][e] */, int kind, int t2, int il, int ht) {
-  const uint32_t lo = *reinterpret_cast<const uint32_t*>(row_at_e - 4);
-  const uint32_t hi = *reinterpret_cast<const uint32_t*>(row_at_e);
+// Across a vertical edge at window byte `row_at_e` (horizontal step): two dwords.
+template <int KIND>
+__device__ __forceinline__ void filter_row(uint8_t* row_at_e, int t2, int it, int ht) {
+  const uint32_t lo = ld32(row_at_e - 4), hi = ld32(row_at_e);
   Line l{byte_of(lo, 0), byte_of(lo, 1), byte_of(lo, 2), byte_of(lo, 3),
          byte_of(hi, 0), byte_of(hi, 1), byte_of(hi, 2), byte_of(hi, 3)};
-  filter_line(l, kind, t2, il, ht);
-  *reinterpret_cast<uint32_t*>(row_at_e - 4) = pack4(l.p3, l.p2, l.p1, l.p0);
-  *reinterpret_cast<uint32_t*>(row_at_e) = pack4(l.q0, l.q1, l.q2, l.q3);
+  filter_line<KIND>(l, t2, it, ht);
+  st32(row_at_e - 4, pack4(l.p3, l.p2, l.p1, l.p0));
+  st32(row_at_e, pack4(l.q0, l.q1, l.q2, l.q3));
 }
-// Filter across a horizontal edge (vertical step `s` = window stride).
-__device__ __forceinline__ void filter_col(uint8_t* p /* &win[e][col] */, int s, int kind, int t2, int il, int ht) {
+// Across a horizontal edge (vertical step `s` = window stride): eight bytes.
+template <int KIND>
+__device__ __forceinline__ void filter_col(uint8_t* p, int s, int t2, int it, int ht) {
   Line l{p[-4 * s], p[-3 * s], p[-2 * s], p[-s], p[0], p[s], p[2 * s], p[3 * s]};
-  filter_line(l, kind, t2, il, ht);
-  p[-3 * s] = (uint8_t)l.p2;
-  p[-2 * s] = (uint8_t)l.p1;
+  filter_line<KIND>(l, t2, it, ht);
+  if (KIND == 1) {
+    p[-3 * s] = (uint8_t)l.p2;
+    p[2 * s] = (uint8_t)l.q2;
+  }
+  if (KIND != 0) {
+    p[-2 * s] = (uint8_t)l.p1;
+    p[s] = (uint8_t)l.q1;
+  }
   p[-s] = (uint8_t)l.p0;
   p[0] = (uint8_t)l.q0;
-  p[s] = (uint8_t)l.q1;
-  p[2 * s] = (uint8_t)l.q2;
 }
 
-__device__ __forceinline__ uint32_t lds32(const uint8_t* p) { return *reinterpret_cast<const uint32_t*>(p); }
-__device__ __forceinline__ void st32(uint8_t* p, uint32_t v) { *reinterpret_cast<uint32_t*>(p) = v; }
+// The eight edge steps of DoFilter (frame_dec.c.go:204-251) for one MB per half-wave.
+// Lanes 0..15: luma line l; 16..31: chroma line (plane (l>>3)&1, index l&7), complex only.
+template <bool kComplex>
+__device__ __forceinline__ void filter_mb(uint8_t* fw, int l, bool on, bool fx, bool fy, bool fin, int limit,
+                                          int ilevel, int hev_t) {
+  constexpr int KMB = kComplex ? 1 : 0, KIN = kComplex ? 2 : 0;
+  const int t_mb = 2 * (limit + 4) + 1, t_in = 2 * limit + 1;
+  const bool luma = l < 16;
+  const bool chroma = kComplex && !luma;
+  const int li = l & 15, cl = l & 7;
+  uint8_t* cwin = fw + ((l >> 3) & 1 ? kFwV : kFwU);
+  uint8_t* yrow = fw + kFwY + (li + 4) * FWY;
+  uint8_t* crow = cwin + (cl + 4) * FWC;
+  const bool lx = on && fx, lin = on && fin, ly = on && fy;
+  if (lx && luma) filter_row<KMB>(yrow + 4, t_mb, ilevel, hev_t);  // HFilter16 / SimpleHFilter16
+  if (lx && chroma) filter_row<KMB>(crow + 4, t_mb, ilevel, hev_t);  // HFilter8
+  lds_sync();
+  if (lin && luma) filter_row<KIN>(yrow + 8, t_in, ilevel, hev_t);  // HFilter16i
+  if (lin && chroma) filter_row<KIN>(crow + 8, t_in, ilevel, hev_t);  // HFilter8i
+  lds_sync();
+  if (lin && luma) filter_row<KIN>(yrow + 12, t_in, ilevel, hev_t);
+  lds_sync();
+  if (lin && luma) filter_row<KIN>(yrow + 16, t_in, ilevel, hev_t);
+  lds_sync();
+  if (ly && luma) filter_col<KMB>(fw + kFwY + 4 * FWY + 4 + li, FWY, t_mb, ilevel, hev_t);  // VFilter16
+  if (ly && chroma) filter_col<KMB>(cwin + 4 * FWC + 4 + cl, FWC, t_mb, ilevel, hev_t);   // VFilter8
+  lds_sync();
+  if (lin && luma) filter_col<KIN>(fw + kFwY + 8 * FWY + 4 + li, FWY, t_in, ilevel, hev_t);  // VFilter16i
+  if (lin && chroma) filter_col<KIN>(cwin + 8 * FWC + 4 + cl, FWC, t_in, ilevel, hev_t);   // VFilter8i
+  lds_sync();
+  if (lin && luma) filter_col<KIN>(fw + kFwY + 12 * FWY + 4 + li, FWY, t_in, ilevel, hev_t);
+  lds_sync();
+  if (lin && luma) filter_col<KIN>(fw + kFwY + 16 * FWY + 4 + li, FWY, t_in, ilevel, hev_t);
+  lds_sync();
+}
+
+__device__ __forceinline__ MbRec load_rec(gptr<const uint32_t> mbs, int mb_w, int y, bool row_ok, int x) {
+  if (row_ok && x >= 0 && x < mb_w) {
+    const gptr<const uint32_t> p = mbs + 4 * ((size_t)y * mb_w + x);
+    return MbRec{p[0], p[1], p[2], p[3]};
+  }
+  return MbRec{0, 0, 0, 0};
+}
+
+struct Coefs { uint2 y0, y1, c; };
+
+__device__ __forceinline__ uint2 ld_blockcol(gptr<const uint32_t> blocks, uint32_t bi, int q) {
+  const gptr<const uint32_t> p = blocks + (size_t)bi * 8 + 2 * q;  // 16 int16 = 8 dwords per block
+  return make_uint2(p[0], p[1]);
+}
+
+__device__ __forceinline__ Coefs load_coefs(gptr<const uint32_t> blocks, uint32_t nz, uint32_t blk, int b0, int cb, int q) {
+  Coefs c{{0, 0}, {0, 0}, {0, 0}};
+  if ((nz >> b0) & 1) c.y0 = ld_blockcol(blocks, blk + __builtin_popcount(nz & ((1u << b0) - 1)), q);
+  if ((nz >> (b0 + 8)) & 1) c.y1 = ld_blockcol(blocks, blk + __builtin_popcount(nz & ((1u << (b0 + 8)) - 1)), q);
+  if ((nz >> cb) & 1) c.c = ld_blockcol(blocks, blk + __builtin_popcount(nz & ((1u << cb) - 1)), q);
+  return c;
+}
 
 }  // namespace
 
-__global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc* __restrict__ frames) {
+__global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc* __restrict__ frames, int* err) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  // Progress counters as a typed __shared__ array + relaxed workgroup atomics, so the spin
+  // is a ds_read (lgkmcnt) -- a volatile generic pointer became a flat load whose
+  // vmcnt(0) drained the record/coefficient prefetch every MB.
+  __shared__ uint32_t progress[kWaves];
   const FrameDesc* F = frames + blockIdx.x;
   if (!F->valid) return;
   const int mb_w = F->mb_w, mb_h = F->mb_h;
   const int ftype = F->filter_type;
   const int ys = F->y_stride, uvs = F->uv_stride;
-  const MbRec* __restrict__ mbs = F->mbs;
-  const int16_t* __restrict__ blocks = F->blocks;
-  uint8_t* __restrict__ Yp = F->y;
-  uint8_t* __restrict__ Up = F->u;
-  uint8_t* __restrict__ Vp = F->v;
+  const gptr<const uint32_t> mbs = as_global(reinterpret_cast<const uint32_t*>(F->mbs));
+  const gptr<const uint32_t> row_block0 = as_global(F->row_block0);
+  const gptr<const uint32_t> blocks = as_global(reinterpret_cast<const uint32_t*>(F->blocks));
+  const gptr<uint8_t> Yp = as_global(F->y);
+  const gptr<uint8_t> Up = as_global(F->u);
+  const gptr<uint8_t> Vp = as_global(F->v);
 
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
-  volatile uint32_t* progress = reinterpret_cast<volatile uint32_t*>(lds);
-  uint8_t* ws = lds + kProgBytes + wave * kWaveBytes;  // recon workspace (libwebp yuv_b)
-  uint8_t* fw = ws + kWsBytes;                          // filter window
-  uint8_t* left = fw + kFwBytes;                        // unfiltered left columns (contiguous)
-  uint8_t* cols = lds + kProgBytes + kWaves * kWaveBytes;
+  const int h = lane >> 5;  // half-wave: 0 = row 2k, 1 = row 2k+1
+  const int l = lane & 31;
+  uint32_t* tab = reinterpret_cast<uint32_t*>(lds + kProgBytes);
+  uint8_t* cols = lds + kHdrBytes + 2 * kWaves * kSlotBytes;
   // per MB column c: cols + c*kColBytes: [0..15] ytop Y, [16..23] U, [24..31] V, [32..159] fbot
   if (threadIdx.x < kWaves) progress[threadIdx.x] = 0;
+  for (int t = threadIdx.x; t < 160; t += blockDim.x) tab[t] = kPred4Table[t];
   __syncthreads();
 
-  // lane roles
-  const int lb = lane >> 2;       // luma block 0..15 (raster)
-  const int lq = lane & 3;        // row within block / coefficient column
-  const int lbx = lb & 3, lby = lb >> 2;
-  const int crow = 4 * lby + lq;  // luma pixel row of this lane
-  const int cpl = (lane >> 4) & 1;            // chroma plane (lanes 0..31)
-  const int cb = (lane >> 2) & 3;             // chroma block
-  const int cbx = cb & 1, cby = cb >> 1;
-  const int ccrow = 4 * cby + lq;             // chroma pixel row
-  const int coff = cpl ? V_OFF : U_OFF;
+  for (int k = wave; 2 * k < mb_h; k += kWaves) {
+    const int y = 2 * k + h;
+    const bool row_ok = y < mb_h;
+    const bool has_odd = 2 * k + 1 < mb_h;
+    const bool last_row = y == mb_h - 1;
+    const int nrows_y = last_row ? 16 : 13;  // luma rows of this MB row final after its pass
+    const int nrows_c = last_row ? 8 : 5;
+    uint32_t blk = row_ok ? row_block0[y] : 0u;
+    MbRec rc = load_rec(mbs, mb_w, y, row_ok, -2 * h);
+    MbRec rn = load_rec(mbs, mb_w, y, row_ok, -2 * h + 1);
+    Coefs cc = load_coefs(blocks, rc.flags & kNzMask, blk, (l >> 2), 16 + (l >> 2), l & 3);
+    // Retire the prologue loads here (visible to the waitcnt pass: 0x0F70 = vmcnt(0)), so the
+    // loop header has no pending loads on cc/rc/rn and the in-loop uses of cc do not
+    // conservatively drain the NEXT MB's prefetch with a vmcnt(0).
+    __builtin_amdgcn_s_waitcnt(0x0F70);
 
-  for (int y = wave; y < mb_h; y += kWaves) {
-    // ---- ReconstructRow prologue (frame_dec.c.go:79-98)
-    if (lane < 16) ws[Y_OFF + lane * BPS - 1] = 129;
-    else if (lane < 24) ws[U_OFF + (lane - 16) * BPS - 1] = 129;
-    else if (lane < 32) ws[V_OFF + (lane - 24) * BPS - 1] = 129;
-    if (lane < 32) left[lane] = 129;
-    if (y > 0) {
-      if (lane == 32) ws[Y_OFF - BPS - 1] = 129;
-      if (lane == 33) ws[U_OFF - BPS - 1] = 129;
-      if (lane == 34) ws[V_OFF - BPS - 1] = 129;
-    } else {
-      if (lane < 21) ws[Y_OFF - BPS - 1 + lane] = 127;
-      else if (lane < 30) ws[U_OFF - BPS - 1 + (lane - 21)] = 127;
-      else if (lane < 39) ws[V_OFF - BPS - 1 + (lane - 30)] = 127;
-    }
-    lds_sync();
-    uint32_t blk = F->row_block0[y];  // running index of this MB's first coefficient block
-    const int nrows_y = (y == mb_h - 1) ? 16 : 13;  // luma rows final after this row's pass
-    const int nrows_c = (y == mb_h - 1) ? 8 : 5;
+    for (int i = 0; i < mb_w + 2; ++i) {
+      // Lane roles, recomputed every iteration from an opaque lane id: hoisted out of the
+      // loop, the ~40 lane-constant LDS addresses derived from them spill (rule from
+      // cdna_hip_programming.md: recompute per block with v_mbcnt).
+      int lid;
+      asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lid));
+      const int l = lid & 31;
+      uint8_t* ws = lds + kHdrBytes + (wave * 2 + h) * kSlotBytes;  // recon workspace (libwebp yuv_b)
+      uint8_t* fw = ws + kWsBytes;                                  // filter window
+      uint8_t* left = fw + kFwBytes;                                // unfiltered left columns
+      int16_t* res = reinterpret_cast<int16_t*>(left + kLeftBytes);  // i4x4 residuals
+      const int q = l & 3;
+      const int b0 = l >> 2;              // luma blocks b0 and b0+8
+      const int lbx = b0 & 3, lby = b0 >> 2;
+      const int cpl = (l >> 4) & 1, cbk = (l >> 2) & 3;
+      const int cbx = cbk & 1, cby = cbk >> 1;
+      const int cb = 16 + cpl * 4 + cbk;  // chroma block index
+      const int coff = cpl ? V_OFF : U_OFF;
+      const int ps = l >> 4, pp = l & 15, ppx = pp & 3, ppy = pp >> 2;  // i4x4 pixel lanes
+      const int x = i - 2 * h;
+      const bool act = row_ok && x >= 0 && x < mb_w;
+      const bool last_x = x == mb_w - 1;
+      // ---- software pipeline: record x+2 and coefficients x+1 in flight during MB x
+      const MbRec rnn = load_rec(mbs, mb_w, y, row_ok, x + 2);
+      const uint32_t blk_next = blk + __builtin_popcount(rc.flags & kNzMask);
+      const Coefs cn = load_coefs(blocks, rn.flags & kNzMask, blk_next, b0, cb, q);
 
-    for (int x = 0; x < mb_w; ++x) {
-      const MbRec rec = mbs[(size_t)y * mb_w + x];
-      const uint32_t flags = __builtin_amdgcn_readfirstlane(rec.flags);
-      const uint32_t im_lo = __builtin_amdgcn_readfirstlane(rec.imodes_lo);
-      const uint32_t im_hi = __builtin_amdgcn_readfirstlane(rec.imodes_hi);
-      const uint32_t finfo = __builtin_amdgcn_readfirstlane(rec.finfo);
-      const uint32_t nz = flags & kNzMask;
-      const bool is_i4 = (flags >> kI4Shift) & 1;
-
-      // ---- coefficient loads (one column of one block per lane)
-      int yc[4] = {0, 0, 0, 0}, uc[4] = {0, 0, 0, 0};
-      if ((nz >> lb) & 1) {
-        const uint32_t bi = blk + __builtin_popcount(nz & ((1u << lb) - 1));
-        const uint2 v = *reinterpret_cast<const uint2*>(blocks + (size_t)bi * 16 + 4 * lq);
-        yc[0] = (int16_t)(v.x & 0xffff); yc[1] = (int16_t)(v.x >> 16);
-        yc[2] = (int16_t)(v.y & 0xffff); yc[3] = (int16_t)(v.y >> 16);
+      // ---- wait for the previous pair's odd row (t = x + 2y wavefront)
+      if (k > 0 && i < mb_w) {
+        const uint32_t need = ((uint32_t)(k - 1) << 16) | (uint32_t)min(i + 2, mb_w);
+        uint32_t* pr = progress + ((k - 1) & (kWaves - 1));
+        if (__hip_atomic_load(pr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
+          const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+          while (__hip_atomic_load(pr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
+            __builtin_amdgcn_s_sleep(2);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s: give up, flag
+              if (lane == 0) atomicOr(err, 1);
+              return;
+            }
+          }
+        }
       }
-      const int cbi = 16 + cpl * 4 + cb;  // lanes 0..31: chroma blocks 16..23
-      if (lane < 32 && ((nz >> cbi) & 1)) {
-        const uint32_t bi = blk + __builtin_popcount(nz & ((1u << cbi) - 1));
-        const uint2 v = *reinterpret_cast<const uint2*>(blocks + (size_t)bi * 16 + 4 * lq);
-        uc[0] = (int16_t)(v.x & 0xffff); uc[1] = (int16_t)(v.x >> 16);
-        uc[2] = (int16_t)(v.y & 0xffff); uc[3] = (int16_t)(v.y >> 16);
-      }
-      blk += __builtin_popcount(nz);
-
-      // ---- wait for the row above (t = x + 2y wavefront)
-      if (y > 0) {
-        const uint32_t need = (uint32_t)(y - 1) * mb_w + min(x + 2, mb_w);
-        volatile uint32_t* pr = progress + ((y - 1) & (kWaves - 1));
-        while (*pr < need) __builtin_amdgcn_s_sleep(1);
-      }
+      const uint32_t fl = rc.flags;
+      const bool i4 = (fl >> kI4Shift) & 1;
       uint8_t* col = cols + x * kColBytes;
 
+      // ---- ReconstructRow prologue at the row's first MB (frame_dec.c.go:79-98)
+      if (act && x == 0) {
+        if (l < 16) ws[Y_OFF + l * BPS - 1] = 129;
+        else if (l < 24) ws[U_OFF + (l - 16) * BPS - 1] = 129;
+        else ws[V_OFF + (l - 24) * BPS - 1] = 129;
+        left[l] = 129;
+        if (y > 0) {
+          if (l == 0) ws[Y_OFF - BPS - 1] = 129;
+          if (l == 1) ws[U_OFF - BPS - 1] = 129;
+          if (l == 2) ws[V_OFF - BPS - 1] = 129;
+        } else {
+          if (l < 21) ws[Y_OFF - BPS - 1 + l] = 127;
+          if (l < 18) ws[(l < 9 ? U_OFF - BPS - 1 + l : V_OFF - BPS - 1 + (l - 9))] = 127;
+        }
+      }
+      lds_sync();
       // ---- top samples (frame_dec.c.go:122-142)
-      if (y > 0) {
-        if (lane < 4) st32(ws + Y_OFF - BPS + 4 * lane, lds32(col + 4 * lane));
-        else if (lane < 6) st32(ws + U_OFF - BPS + 4 * (lane - 4), lds32(col + 16 + 4 * (lane - 4)));
-        else if (lane < 8) st32(ws + V_OFF - BPS + 4 * (lane - 6), lds32(col + 24 + 4 * (lane - 6)));
-        else if (lane == 8 && is_i4) {
-          const uint32_t tr = (x >= mb_w - 1) ? (uint32_t)col[15] * 0x01010101u : lds32(col + kColBytes);
-          st32(ws + Y_OFF - BPS + 16, tr);
-        }
+      if (act && y > 0) {
+        if (l < 4) st32(ws + Y_OFF - BPS + 4 * l, ld32(col + 4 * l));
+        else if (l < 6) st32(ws + U_OFF - BPS + 4 * (l - 4), ld32(col + 16 + 4 * (l - 4)));
+        else if (l < 8) st32(ws + V_OFF - BPS + 4 * (l - 6), ld32(col + 24 + 4 * (l - 6)));
+        else if (l == 8 && i4)
+          st32(ws + Y_OFF - BPS + 16, last_x ? (uint32_t)col[15] * 0x01010101u : ld32(col + kColBytes));
       }
       lds_sync();
-      if (is_i4 && lane < 3) st32(ws + Y_OFF + (3 + 4 * lane) * BPS + 16, lds32(ws + Y_OFF - BPS + 16));
-      lds_sync();
+      if (act && i4 && l < 3) st32(ws + Y_OFF + (3 + 4 * l) * BPS + 16, ld32(ws + Y_OFF - BPS + 16));
 
-      // ---- luma residuals (all 16 blocks at once)
-      int ry[4];
-      idct_quad(lq, yc[0], yc[1], yc[2], yc[3], ry);
-      uint8_t* my = ws + Y_OFF + crow * BPS + 4 * lbx;
-      if (!is_i4) {
-        const int mode = check_mode(x, y, (flags >> kYModeShift) & 3);
-        uint32_t pred;
-        const uint32_t top = lds32(ws + Y_OFF - BPS + 4 * lbx);
-        const int l = left[crow];
-        if (mode == 2) {
-          pred = top;
-        } else if (mode == 3) {
-          pred = (uint32_t)l * 0x01010101u;
-        } else if (mode == 1) {
-          const int tl = ws[Y_OFF - BPS - 1];
-          pred = pack4(clamp255(byte_of(top, 0) + l - tl), clamp255(byte_of(top, 1) + l - tl),
-                       clamp255(byte_of(top, 2) + l - tl), clamp255(byte_of(top, 3) + l - tl));
-        } else {
+      // ---- residuals of all blocks (prediction-independent)
+      int ry0[4], ry1[4], rcr[4];
+      idct_quad(q, cc.y0, ry0);
+      idct_quad(q, cc.y1, ry1);
+      idct_quad(q, cc.c, rcr);
+
+      // ---- luma prediction + residual
+      const int row_a = 4 * lby + q, row_b = row_a + 8;
+      uint8_t* dst_a = ws + Y_OFF + row_a * BPS + 4 * lbx;
+      uint8_t* dst_b = ws + Y_OFF + row_b * BPS + 4 * lbx;
+      if (act && !i4) {
+        const int mode = check_mode(x, y, (fl >> kYModeShift) & 3);
+        const uint32_t top = ld32(ws + Y_OFF - BPS + 4 * lbx);
+        const int tl = ws[Y_OFF - BPS - 1];
+        int dc = 0x80;
+        if (mode == 0 || mode == 4 || mode == 5) {
           uint32_t st = 0, sl = 0;
-          for (int k = 0; k < 4; ++k) {
-            st = __builtin_amdgcn_sad_u8(lds32(ws + Y_OFF - BPS + 4 * k), 0, st);
-            sl = __builtin_amdgcn_sad_u8(lds32(left + 4 * k), 0, sl);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            st = __builtin_amdgcn_sad_u8(ld32(ws + Y_OFF - BPS + 4 * j), 0, st);
+            sl = __builtin_amdgcn_sad_u8(ld32(left + 4 * j), 0, sl);
           }
-          int dc;
-          if (mode == 0) dc = (int)(st + sl + 16) >> 5;
-          else if (mode == 4) dc = (int)(sl + 8) >> 4;   // no top
-          else if (mode == 5) dc = (int)(st + 8) >> 4;   // no left
-          else dc = 0x80;
-          pred = (uint32_t)dc * 0x01010101u;
+          dc = mode == 0 ? (int)(st + sl + 16) >> 5 : mode == 4 ? (int)(sl + 8) >> 4 : (int)(st + 8) >> 4;
         }
-        lds_sync();
-        st32(my, add_res(pred, ry));
-      } else {
-        const int mode = ((lb < 8 ? im_lo >> (4 * lb) : im_hi >> (4 * (lb - 8)))) & 0xf;
-        const int tstep = lbx + 2 * lby;
+        const uint32_t pa = pred_row(mode, top, left[row_a], tl, dc);
+        const uint32_t pb = pred_row(mode, top, left[row_b], tl, dc);
+        st32(dst_a, add_res(pa, ry0));
+        st32(dst_b, add_res(pb, ry1));
+      }
+      if (act && i4) {  // stage residuals for the pixel-per-lane wavefront
+        *reinterpret_cast<uint2*>(res + b0 * 16 + q * 4) =
+            make_uint2((ry0[0] & 0xffff) | (ry0[1] << 16), (ry0[2] & 0xffff) | (ry0[3] << 16));
+        *reinterpret_cast<uint2*>(res + (b0 + 8) * 16 + q * 4) =
+            make_uint2((ry1[0] & 0xffff) | (ry1[1] << 16), (ry1[2] & 0xffff) | (ry1[3] << 16));
+      }
+      lds_sync();
+      if (__any(act && i4)) {
+        const uint32_t im_lo = rc.imodes_lo, im_hi = rc.imodes_hi;
         for (int t = 0; t < 10; ++t) {
-          if (tstep == t) {
-            const uint8_t* b0 = ws + Y_OFF + 4 * lby * BPS + 4 * lbx;  // block origin
-            const uint32_t tlo = lds32(b0 - BPS);
-            const uint32_t thi = lds32(b0 - BPS + 4);
-            const int X = b0[-BPS - 1];
-            const uint32_t lft = pack4(b0[-1], b0[BPS - 1], b0[2 * BPS - 1], b0[3 * BPS - 1]);
-            const uint32_t pred = pred4_row(mode, lq, tlo, thi, X, lft);
-            st32(my, add_res(pred, ry));
+          const int by = max(0, (t - 2) >> 1) + ps;
+          const int bx = t - 2 * by;
+          if (act && i4 && by <= min(3, t >> 1) && bx >= 0) {
+            const int bi = by * 4 + bx;
+            const int mode = (bi < 8 ? im_lo >> (4 * bi) : im_hi >> (4 * (bi - 8))) & 0xf;
+            const uint32_t e = tab[mode * 16 + pp];
+            uint8_t* org = ws + Y_OFF + 4 * by * BPS + 4 * bx;
+            const int kind = e >> 24;
+            const int a = org[(int8_t)(e & 0xff)];
+            const int b = org[(int8_t)((e >> 8) & 0xff)];
+            const int c = org[(int8_t)((e >> 16) & 0xff)];
+            int v;
+            if (kind == 3) {  // DC4
+              const uint32_t s = __builtin_amdgcn_sad_u8(ld32(org - BPS), 0, 0);
+              v = (int)(s + org[-1] + org[BPS - 1] + org[2 * BPS - 1] + org[3 * BPS - 1] + 4) >> 3;
+            } else {
+              const int avg3 = (a + 2 * b + c + 2) >> 2;
+              const int avg2 = (a + b + 1) >> 1;
+              const int tm = clamp255(a + b - c);
+              v = kind == 0 ? avg3 : kind == 1 ? avg2 : tm;
+            }
+            org[ppy * BPS + ppx] = (uint8_t)clamp255(v + res[bi * 16 + pp]);
           }
           lds_sync();
         }
       }
 
-      // ---- chroma (lanes 0..31)
-      int rc[4];
-      idct_quad(lq, uc[0], uc[1], uc[2], uc[3], rc);
-      if (lane < 32) {
-        const int mode = check_mode(x, y, (flags >> kUVModeShift) & 3);
+      // ---- chroma prediction + residual (lane = one pixel row of one 4x4 chroma block)
+      if (act) {
+        const int mode = check_mode(x, y, (fl >> kUVModeShift) & 3);
         const uint8_t* base = ws + coff;
-        const uint32_t top = lds32(base - BPS + 4 * cbx);
-        const int l = left[16 + 8 * cpl + ccrow];
-        uint32_t pred;
-        if (mode == 2) {
-          pred = top;
-        } else if (mode == 3) {
-          pred = (uint32_t)l * 0x01010101u;
-        } else if (mode == 1) {
-          const int tl = base[-BPS - 1];
-          pred = pack4(clamp255(byte_of(top, 0) + l - tl), clamp255(byte_of(top, 1) + l - tl),
-                       clamp255(byte_of(top, 2) + l - tl), clamp255(byte_of(top, 3) + l - tl));
-        } else {
-          uint32_t st = 0, sl = 0;
-          for (int k = 0; k < 2; ++k) {
-            st = __builtin_amdgcn_sad_u8(lds32(base - BPS + 4 * k), 0, st);
-            sl = __builtin_amdgcn_sad_u8(lds32(left + 16 + 8 * cpl + 4 * k), 0, sl);
-          }
-          int dc;
-          if (mode == 0) dc = (int)(st + sl + 8) >> 4;
-          else if (mode == 4) dc = (int)(sl + 4) >> 3;
-          else if (mode == 5) dc = (int)(st + 4) >> 3;
-          else dc = 0x80;
-          pred = (uint32_t)dc * 0x01010101u;
+        const int row = 4 * cby + q;
+        const uint32_t top = ld32(base - BPS + 4 * cbx);
+        const int tl = base[-BPS - 1];
+        int dc = 0x80;
+        if (mode == 0 || mode == 4 || mode == 5) {
+          uint32_t st = __builtin_amdgcn_sad_u8(ld32(base - BPS), 0, 0);
+          st = __builtin_amdgcn_sad_u8(ld32(base - BPS + 4), 0, st);
+          uint32_t sl = __builtin_amdgcn_sad_u8(ld32(left + 16 + 8 * cpl), 0, 0);
+          sl = __builtin_amdgcn_sad_u8(ld32(left + 16 + 8 * cpl + 4), 0, sl);
+          dc = mode == 0 ? (int)(st + sl + 8) >> 4 : mode == 4 ? (int)(sl + 4) >> 3 : (int)(st + 4) >> 3;
         }
-        lds_sync();
-        st32(ws + coff + ccrow * BPS + 4 * cbx, add_res(pred, rc));
+        const uint32_t pred = pred_row(mode, top, left[16 + 8 * cpl + row], tl, dc);
+        st32(ws + coff + row * BPS + 4 * cbx, add_res(pred, rcr));
       }
       lds_sync();
 
-      // ---- stash top samples for the row below (frame_dec.c.go:175-179)
-      if (y < mb_h - 1) {
-        if (lane < 4) st32(col + 4 * lane, lds32(ws + Y_OFF + 15 * BPS + 4 * lane));
-        else if (lane < 6) st32(col + 16 + 4 * (lane - 4), lds32(ws + U_OFF + 7 * BPS + 4 * (lane - 4)));
-        else if (lane < 8) st32(col + 24 + 4 * (lane - 6), lds32(ws + V_OFF + 7 * BPS + 4 * (lane - 6)));
-      }
-      // ---- fill the filter window: MB body from the workspace, rows above from fbot
-      {
-        const int r = lane >> 2, d = lane & 3;
-        st32(fw + kFwY + (r + 4) * FWY + 4 + 4 * d, lds32(ws + Y_OFF + r * BPS + 4 * d));
-        if (lane < 32) {
-          const int p = lane >> 4, rr = (lane >> 1) & 7, dd = lane & 1;
-          st32(fw + (p ? kFwV : kFwU) + (rr + 4) * FWC + 4 + 4 * dd,
-               lds32(ws + (p ? V_OFF : U_OFF) + rr * BPS + 4 * dd));
-        } else if (y > 0) {
-          const int k = lane - 32;  // 0..31
-          if (k < 16) {             // luma rows -4..-1
-            st32(fw + kFwY + (k >> 2) * FWY + 4 + 4 * (k & 3), lds32(col + 32 + 4 * k));
-          } else {                  // chroma rows -4..-1
-            const int p = (k - 16) >> 3, rr = ((k - 16) >> 1) & 3, dd = k & 1;
-            st32(fw + (p ? kFwV : kFwU) + rr * FWC + 4 + 4 * dd, lds32(col + 96 + 32 * p + 8 * rr + 4 * dd));
-          }
+      if (act) {
+        // ---- stash unfiltered bottom samples for the row below (frame_dec.c.go:175-179)
+        if (!last_row) {
+          if (l < 4) st32(col + 4 * l, ld32(ws + Y_OFF + 15 * BPS + 4 * l));
+          else if (l < 6) st32(col + 16 + 4 * (l - 4), ld32(ws + U_OFF + 7 * BPS + 4 * (l - 4)));
+          else if (l < 8) st32(col + 24 + 4 * (l - 6), ld32(ws + V_OFF + 7 * BPS + 4 * (l - 6)));
         }
-      }
-      lds_sync();
-
-      // ---- loop filter (DoFilter, frame_dec.c.go:204-251) on the window
-      const int limit = finfo & 0xff;
-      if (ftype > 0 && limit > 0) {
-        const int ilevel = (finfo >> 8) & 0xff;
-        const int inner = (finfo >> 16) & 0xff;
-        const int hev_t = (finfo >> 24) & 0xff;
-        const int kmb = ftype == 1 ? 0 : 1, kin = ftype == 1 ? 0 : 2;
-        const int t_mb = 2 * (limit + 4) + 1, t_in = 2 * limit + 1;
-        // lanes 0..15: luma line; 16..23: U line; 24..31: V line (complex only)
-        const bool luma = lane < 16;
-        const bool chroma = lane >= 16 && lane < 32 && ftype == 2;
-        const int li = lane & 15;
-        const int cli = lane & 7;
-        uint8_t* cwin = fw + ((lane >> 3) & 1 ? kFwV : kFwU);
-        if (x > 0) {  // left MB edge (HFilter16 / HFilter8)
-          if (luma) filter_row(fw + kFwY + (li + 4) * FWY + 4, kmb, t_mb, ilevel, hev_t);
-          if (chroma) filter_row(cwin + (cli + 4) * FWC + 4, kmb, t_mb, ilevel, hev_t);
-          lds_sync();
-        }
-        if (inner) {  // inner vertical edges (HFilter16i / HFilter8i)
-          if (luma) filter_row(fw + kFwY + (li + 4) * FWY + 8, kin, t_in, ilevel, hev_t);
-          if (chroma) filter_row(cwin + (cli + 4) * FWC + 8, kin, t_in, ilevel, hev_t);
-          lds_sync();
-          if (luma) filter_row(fw + kFwY + (li + 4) * FWY + 12, kin, t_in, ilevel, hev_t);
-          lds_sync();
-          if (luma) filter_row(fw + kFwY + (li + 4) * FWY + 16, kin, t_in, ilevel, hev_t);
-          lds_sync();
-        }
-        if (y > 0) {  // top MB edge (VFilter16 / VFilter8)
-          if (luma) filter_col(fw + kFwY + 4 * FWY + 4 + li, FWY, kmb, t_mb, ilevel, hev_t);
-          if (chroma) filter_col(cwin + 4 * FWC + 4 + cli, FWC, kmb, t_mb, ilevel, hev_t);
-          lds_sync();
-        }
-        if (inner) {  // inner horizontal edges (VFilter16i / VFilter8i)
-          if (luma) filter_col(fw + kFwY + 8 * FWY + 4 + li, FWY, kin, t_in, ilevel, hev_t);
-          if (chroma) filter_col(cwin + 8 * FWC + 4 + cli, FWC, kin, t_in, ilevel, hev_t);
-          lds_sync();
-          if (luma) filter_col(fw + kFwY + 12 * FWY + 4 + li, FWY, kin, t_in, ilevel, hev_t);
-          lds_sync();
-          if (luma) filter_col(fw + kFwY + 16 * FWY + 4 + li, FWY, kin, t_in, ilevel, hev_t);
-          lds_sync();
-        }
-      }
-
-      // ---- deposit this row's bottom samples for the row below (fbot)
-      {
-        const bool last_x = (x == mb_w - 1);
-        if (lane < 16) {  // luma rows 12..15, dwords: cols -4..-1 -> col x-1, cols 0..11 / 12..15 -> col x
-          const int rr = lane >> 2, d = lane & 3;  // d=0: cols -4..-1, d=1..3: cols 0..11
-          if (d == 0) {
-            if (x > 0) st32(col - kColBytes + 32 + rr * 16 + 12, lds32(fw + kFwY + (rr + 16) * FWY + 0));
-          } else {
-            st32(col + 32 + rr * 16 + 4 * (d - 1), lds32(fw + kFwY + (rr + 16) * FWY + 4 * d));
-          }
-          if (last_x && d == 0) st32(col + 32 + rr * 16 + 12, lds32(fw + kFwY + (rr + 16) * FWY + 16));
-        } else if (lane < 32) {  // chroma rows 4..7
-          const int k = lane - 16, p = k >> 3, rr = (k >> 1) & 3, d = k & 1;
-          const uint8_t* cw = fw + (p ? kFwV : kFwU);
-          uint8_t* cb0 = col + 96 + 32 * p + 8 * rr;
-          if (d == 0) {
-            if (x > 0) st32(cb0 - kColBytes + 4, lds32(cw + (rr + 8) * FWC + 0));
-          } else {
-            st32(cb0, lds32(cw + (rr + 8) * FWC + 4));
-          }
-          if (last_x && d == 0) st32(cb0 + 4, lds32(cw + (rr + 8) * FWC + 8));
-        }
-      }
-
-      // ---- final pixels to HBM (each byte written once)
-      {
-        const bool last_x = (x == mb_w - 1);
-        // luma: rows 0..nrows_y-1, window cols -4..11 (dword d = cols 4d-4..4d-1)
+        // ---- filter window: MB body from the workspace, rows above from fbot
+        st32(fw + kFwY + (b0 + 4) * FWY + 4 + 4 * q, ld32(ws + Y_OFF + b0 * BPS + 4 * q));
+        st32(fw + kFwY + (b0 + 12) * FWY + 4 + 4 * q, ld32(ws + Y_OFF + (b0 + 8) * BPS + 4 * q));
         {
-          const int r = lane >> 2, d = lane & 3;
-          if (r < nrows_y && (d > 0 || x > 0))
-            *reinterpret_cast<uint32_t*>(Yp + (size_t)(16 * y + r) * ys + 16 * x - 4 + 4 * d) =
-                lds32(fw + kFwY + (r + 4) * FWY + 4 * d);
+          const int p = l >> 4, rr = (l >> 1) & 7, dd = l & 1;
+          st32(fw + (p ? kFwV : kFwU) + (rr + 4) * FWC + 4 + 4 * dd, ld32(ws + (p ? V_OFF : U_OFF) + rr * BPS + 4 * dd));
         }
-        // luma rows 13..15 of the last row: r = 16..15 handled above via nrows; extra lanes:
-        if (lane < 16) {
-          const int r = lane;  // rows -3..-1 (MB above) use lanes 0..11; last column cols 12..15
-          if (y > 0 && r < 12) {
-            const int rr = (r >> 2) - 3, d = r & 3;
-            *reinterpret_cast<uint32_t*>(Yp + (size_t)(16 * y + rr) * ys + 16 * x + 4 * d) =
-                lds32(fw + kFwY + (rr + 4) * FWY + 4 + 4 * d);
-          }
-          if (last_x && r < nrows_y)
-            *reinterpret_cast<uint32_t*>(Yp + (size_t)(16 * y + r) * ys + 16 * x + 12) =
-                lds32(fw + kFwY + (r + 4) * FWY + 16);
-        } else if (lane < 48) {  // chroma: rows 0..nrows_c-1 cols -4..3, both planes
-          const int k = lane - 16, p = k >> 4, r = (k >> 1) & 7, d = k & 1;
-          const uint8_t* cw = fw + (p ? kFwV : kFwU);
-          uint8_t* plane = p ? Vp : Up;
-          if (r < nrows_c && (d > 0 || x > 0))
-            *reinterpret_cast<uint32_t*>(plane + (size_t)(8 * y + r) * uvs + 8 * x - 4 + 4 * d) =
-                lds32(cw + (r + 4) * FWC + 4 * d);
-          if (last_x && d == 0 && r < nrows_c)
-            *reinterpret_cast<uint32_t*>(plane + (size_t)(8 * y + r) * uvs + 8 * x + 4) =
-                lds32(cw + (r + 4) * FWC + 8);
-        } else if (y > 0) {  // chroma rows -3..-1 of the MB above, cols 0..7
-          const int k = lane - 48;  // 0..15: p, row, d
-          const int p = k >> 3, rr = ((k >> 1) & 3), d = k & 1;
-          if (rr < 3) {
-            const uint8_t* cw = fw + (p ? kFwV : kFwU);
-            uint8_t* plane = p ? Vp : Up;
-            const int row = rr - 3;
-            *reinterpret_cast<uint32_t*>(plane + (size_t)(8 * y + row) * uvs + 8 * x + 4 * d) =
-                lds32(cw + (row + 4) * FWC + 4 + 4 * d);
+        if (y > 0) {
+          if (l < 16) {
+            st32(fw + kFwY + (l >> 2) * FWY + 4 + 4 * (l & 3), ld32(col + 32 + 4 * l));
+          } else {
+            const int kk = l - 16, p = kk >> 3, rr = (kk >> 1) & 3, dd = kk & 1;
+            st32(fw + (p ? kFwV : kFwU) + rr * FWC + 4 + 4 * dd, ld32(col + 96 + 32 * p + 8 * rr + 4 * dd));
           }
         }
       }
       lds_sync();
 
-      // ---- rotate for the next MB (frame_dec.c.go:106-114) + filter window
-      if (lane < 17) {  // Y rows -1..15: cols 12..15 -> -4..-1
-        const int r = lane - 1;
-        const uint32_t v = lds32(ws + Y_OFF + r * BPS + 12);
-        st32(ws + Y_OFF + r * BPS - 4, v);
-        if (r >= 0) left[r] = (uint8_t)(v >> 24);
-      } else if (lane < 35) {  // U/V rows -1..7: cols 4..7 -> -4..-1
-        const int k = lane - 17, p = k / 9, r = k % 9 - 1;
-        const int off = p ? V_OFF : U_OFF;
-        const uint32_t v = lds32(ws + off + r * BPS + 4);
-        st32(ws + off + r * BPS - 4, v);
-        if (r >= 0) left[16 + 8 * p + r] = (uint8_t)(v >> 24);
-      } else if (lane < 51) {  // window luma rows 0..15
-        const int r = lane - 35;
-        st32(fw + kFwY + (r + 4) * FWY, lds32(fw + kFwY + (r + 4) * FWY + 16));
-      } else if (lane < 64) {  // window chroma rows 0..7 (13 lanes: U 0..7, V 0..4)
-        const int k = lane - 51, p = k >> 3, r = k & 7;
-        uint8_t* cw = fw + (p ? kFwV : kFwU);
-        st32(cw + (r + 4) * FWC, lds32(cw + (r + 4) * FWC + 8));
+      // ---- loop filter on the window
+      {
+        const uint32_t fi = rc.finfo;
+        const int limit = fi & 0xff;
+        const bool on = act && limit > 0;
+        if (ftype > 0 && __any(on)) {
+          const int ilevel = (fi >> 8) & 0xff, inner = (fi >> 16) & 0xff, hev_t = (fi >> 24) & 0xff;
+          if (ftype == 2) filter_mb<true>(fw, l, on, x > 0, y > 0, inner != 0, limit, ilevel, hev_t);
+          else filter_mb<false>(fw, l, on, x > 0, y > 0, inner != 0, limit, ilevel, hev_t);
+        }
       }
-      if (lane < 3) {  // window V rows 5..7
-        uint8_t* cw = fw + kFwV;
-        const int r = 5 + lane;
-        st32(cw + (r + 4) * FWC, lds32(cw + (r + 4) * FWC + 8));
+
+      if (act) {
+        // ---- deposit final bottom rows of this MB column (and the left neighbour's
+        //      cols 12..15 / 4..7, final now) for the row below's top-edge filter
+        if (!last_row) {
+          if (l < 16) {
+            const int rr = l >> 2, d = l & 3;
+            const uint8_t* src = fw + kFwY + (rr + 16) * FWY;
+            if (d == 0) {
+              if (x > 0) st32(col - kColBytes + 32 + rr * 16 + 12, ld32(src));
+              if (last_x) st32(col + 32 + rr * 16 + 12, ld32(src + 16));
+            } else {
+              st32(col + 32 + rr * 16 + 4 * (d - 1), ld32(src + 4 * d));
+            }
+          } else {
+            const int kk = l - 16, p = kk >> 3, rr = (kk >> 1) & 3, d = kk & 1;
+            const uint8_t* src = fw + (p ? kFwV : kFwU) + (rr + 8) * FWC;
+            uint8_t* cb0 = col + 96 + 32 * p + 8 * rr;
+            if (d == 0) {
+              if (x > 0) st32(cb0 - kColBytes + 4, ld32(src));
+              if (last_x) st32(cb0 + 4, ld32(src + 8));
+            } else {
+              st32(cb0, ld32(src + 4));
+            }
+          }
+        }
+        // ---- final pixels to HBM (each byte written once)
+        {  // luma rows 0..nrows_y-1, window cols -4..11 (dword q = cols 4q-4..4q-1)
+          const int r0 = b0, r1 = b0 + 8;
+          if (q > 0 || x > 0) {
+            if (r0 < nrows_y)
+              *reinterpret_cast<gptr<uint32_t>>(Yp + (size_t)(16 * y + r0) * ys + 16 * x - 4 + 4 * q) =
+                  ld32(fw + kFwY + (r0 + 4) * FWY + 4 * q);
+            if (r1 < nrows_y)
+              *reinterpret_cast<gptr<uint32_t>>(Yp + (size_t)(16 * y + r1) * ys + 16 * x - 4 + 4 * q) =
+                  ld32(fw + kFwY + (r1 + 4) * FWY + 4 * q);
+          }
+        }
+        if (l < 16) {
+          if (y > 0 && l < 12) {  // luma rows -3..-1 of the MB above, cols 0..15
+            const int rr = (l >> 2) - 3, d = l & 3;
+            *reinterpret_cast<gptr<uint32_t>>(Yp + (size_t)(16 * y + rr) * ys + 16 * x + 4 * d) =
+                ld32(fw + kFwY + (rr + 4) * FWY + 4 + 4 * d);
+          }
+          if (last_x && l < nrows_y)  // last column: luma cols 12..15
+            *reinterpret_cast<gptr<uint32_t>>(Yp + (size_t)(16 * y + l) * ys + 16 * x + 12) =
+                ld32(fw + kFwY + (l + 4) * FWY + 16);
+        } else {
+          const int kk = l - 16, p = kk >> 3, r = kk & 7;
+          if (last_x && r < nrows_c)  // last column: chroma cols 4..7
+            *reinterpret_cast<gptr<uint32_t>>((p ? Vp : Up) + (size_t)(8 * y + r) * uvs + 8 * x + 4) =
+                ld32(fw + (p ? kFwV : kFwU) + (r + 4) * FWC + 8);
+        }
+        {  // chroma rows 0..nrows_c-1, cols -4..3
+          const int p = l >> 4, r = (l >> 1) & 7, d = l & 1;
+          if (r < nrows_c && (d > 0 || x > 0))
+            *reinterpret_cast<gptr<uint32_t>>((p ? Vp : Up) + (size_t)(8 * y + r) * uvs + 8 * x - 4 + 4 * d) =
+                ld32(fw + (p ? kFwV : kFwU) + (r + 4) * FWC + 4 * d);
+        }
+        if (y > 0 && l < 12) {  // chroma rows -3..-1 of the MB above, cols 0..7
+          const int p = l / 6, rem = l - 6 * p, rr = (rem >> 1) - 3, d = rem & 1;
+          *reinterpret_cast<gptr<uint32_t>>((p ? Vp : Up) + (size_t)(8 * y + rr) * uvs + 8 * x + 4 * d) =
+              ld32(fw + (p ? kFwV : kFwU) + (rr + 4) * FWC + 4 + 4 * d);
+        }
       }
       lds_sync();
-      if (lane == 0) progress[y & (kWaves - 1)] = (uint32_t)y * mb_w + x + 1;
+
+      // ---- rotate for the next MB (frame_dec.c.go:106-114) + the filter window
+      if (act) {
+#pragma unroll
+        for (int rep = 0; rep < 3; ++rep) {
+          const int task = l + 32 * rep;
+          if (task < 17) {  // Y rows -1..15: cols 12..15 -> -4..-1
+            const int r = task - 1;
+            const uint32_t v = ld32(ws + Y_OFF + r * BPS + 12);
+            st32(ws + Y_OFF + r * BPS - 4, v);
+            if (r >= 0) left[r] = (uint8_t)(v >> 24);
+          } else if (task < 35) {  // U/V rows -1..7: cols 4..7 -> -4..-1
+            const int kk = task - 17, p = kk >= 9, r = kk - 9 * p - 1;
+            const int off = p ? V_OFF : U_OFF;
+            const uint32_t v = ld32(ws + off + r * BPS + 4);
+            st32(ws + off + r * BPS - 4, v);
+            if (r >= 0) left[16 + 8 * p + r] = (uint8_t)(v >> 24);
+          } else if (task < 51) {  // window luma rows 0..15
+            const int r = task - 35;
+            st32(fw + kFwY + (r + 4) * FWY, ld32(fw + kFwY + (r + 4) * FWY + 16));
+          } else if (task < 67) {  // window chroma rows 0..7
+            const int kk = task - 51, p = kk >> 3, r = kk & 7;
+            uint8_t* cw = fw + (p ? kFwV : kFwU);
+            st32(cw + (r + 4) * FWC, ld32(cw + (r + 4) * FWC + 8));
+          }
+        }
+      }
+      lds_sync();
+      if (lane == 32 && has_odd && x >= 0)
+        __hip_atomic_store(progress + (k & (kWaves - 1)), ((uint32_t)k << 16) | (uint32_t)(x + 1), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WORKGROUP);
+      rc = rn;
+      rn = rnn;
+      cc = cn;
+      blk = blk_next;
     }
   }
 }
 
 size_t vp8_recon_lds_bytes(int mb_w) {
-  return (size_t)kProgBytes + (size_t)kWaves * kWaveBytes + (size_t)mb_w * kColBytes;
+  return (size_t)kHdrBytes + (size_t)2 * kWaves * kSlotBytes + (size_t)mb_w * kColBytes;
 }
 
-int vp8_recon_max_mb_w() { return (int)((163840 - kProgBytes - kWaves * kWaveBytes) / kColBytes); }
+int vp8_recon_max_mb_w() { return (int)((163840 - kHdrBytes - 2 * kWaves * kSlotBytes) / kColBytes); }
 
-hipError_t launch_vp8_recon_filter(const FrameDesc* d_frames, int n_frames, int max_mb_w, hipStream_t stream) {
+hipError_t launch_vp8_recon_filter(const FrameDesc* d_frames, int n_frames, int max_mb_w, int* d_err,
+                                   hipStream_t stream) {
   const size_t lds = vp8_recon_lds_bytes(max_mb_w);
   static size_t configured = 0;
   if (lds > 65536 && lds > configured) {
@@ -667,7 +650,7 @@ hipError_t launch_vp8_recon_filter(const FrameDesc* d_frames, int n_frames, int 
     if (e != hipSuccess) return e;
     configured = lds;
   }
-  hipLaunchKernelGGL(vp8_recon_filter_kernel, dim3(n_frames), dim3(1024), lds, stream, d_frames);
+  hipLaunchKernelGGL(vp8_recon_filter_kernel, dim3(n_frames), dim3(1024), lds, stream, d_frames, d_err);
   return hipGetLastError();
 }
 

@@ -27,14 +27,23 @@ namespace {
 constexpr int kTileX = 64;  // 8-pixel groups per workgroup row (512 px)
 constexpr int kTileY = 4;   // row pairs per workgroup
 
+// clamp(v, 0, 255) as an opaque v_med3_i32.  Written in asm on purpose: ROCm 7.2 fuses
+// two `clamp(x >> 6)` + byte-pack sequences into gfx950's v_ashr_pk_u8_i32 and then
+// assumes its upper 16 bits are zero, which corrupted the B byte whenever G saturated
+// low (caught by tests/test_gpu_parity.py).
+__device__ __forceinline__ uint32_t clamp_u8(int v) {
+  int r;
+  asm("v_med3_i32 %0, %1, 0, %2" : "=v"(r) : "v"(v), "s"(255));
+  return (uint32_t)r;
+}
+
 __device__ __forceinline__ uint32_t yuv_to_rgba(int y, int u, int v) {
   // MultHi(a, c) = (a*c) >> 8; Clip8(v) = clamp(v >> 6, 0, 255) (YUV_FIX2 = 6)
   const int y1 = __mul24(y, 19077) >> 8;
   const int r = (y1 + (__mul24(v, 26149) >> 8) - 14234) >> 6;
   const int g = (y1 - (__mul24(u, 6419) >> 8) - (__mul24(v, 13320) >> 8) + 8708) >> 6;
   const int b = (y1 + (__mul24(u, 33050) >> 8) - 17685) >> 6;
-  return (uint32_t)min(max(r, 0), 255) | ((uint32_t)min(max(g, 0), 255) << 8) |
-         ((uint32_t)min(max(b, 0), 255) << 16) | 0xff000000u;
+  return clamp_u8(r) | (clamp_u8(g) << 8) | (clamp_u8(b) << 16) | 0xff000000u;
 }
 
 __device__ __forceinline__ int bsel(uint32_t w, int i) { return (w >> (8 * i)) & 0xff; }

@@ -16,6 +16,19 @@
 
 namespace wg {
 
+#if defined(__HIPCC__)
+// Pointers read out of a FrameDesc are generic; re-qualified as global, loads/stores
+// become global_* (vmcnt only) instead of flat_* (vmcnt AND lgkmcnt, which every LDS
+// wait would then also drain).  Scalar element types only (copying structs across
+// address spaces is not allowed in C++).
+template <typename T>
+using gptr = __attribute__((address_space(1))) T*;
+template <typename T>
+__host__ __device__ __forceinline__ gptr<T> as_global(T* p) {
+  return (gptr<T>)p;
+}
+#endif
+
 // MbRec.flags bit fields
 constexpr uint32_t kNzMask = 0x00ffffffu;  // bit b set: 4x4 block b has coefficients
 constexpr int kI4Shift = 24;                // is_i4x4

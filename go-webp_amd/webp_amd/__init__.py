@@ -12,6 +12,7 @@ decode calls raise.
 """
 import ctypes as C
 import os
+import weakref
 
 import numpy as np
 
@@ -95,10 +96,26 @@ _SIGS = {
 EXPORTED = tuple(_SIGS)
 
 
+def _bind_torch_runtime():
+    """If torch (ROCm wheel) is installed, import it BEFORE loading our library.
+
+    The wheel bundles its own libamdhip64 (SONAME libamdhip64.so.7).  Loaded first, it
+    satisfies our library's DT_NEEDED, so the process has ONE HIP/HSA runtime and device
+    pointers / streams can be shared with torch.  Loaded after /opt/rocm's copy, torch
+    would bring up a second runtime (and fail to see the GPU)."""
+    try:
+        import importlib.util
+        if importlib.util.find_spec("torch") is not None:
+            import torch  # noqa: F401
+    except Exception:
+        pass
+
+
 def lib():
     """Load libgowebp_amd.so (raises if it has not been built)."""
     global _lib
     if _lib is None:
+        _bind_torch_runtime()
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"{LIB_PATH} not built: run `make -C go-webp_amd/csrc` or __graft_entry__.build()")
         L = C.CDLL(LIB_PATH)
@@ -175,6 +192,8 @@ class Batch:
     """Device-resident batch: host parse + H2D once, then run() the device path many times."""
 
     def __init__(self, ctx, datas, flags=0):
+        self._ctx = ctx  # keep the context alive while the batch exists
+        self._h = None
         self._bufs, ptrs, sizes = _ptr_arrays(datas)
         n = len(self._bufs)
         self.status = np.zeros(n, np.int32)
@@ -183,6 +202,7 @@ class Batch:
             raise WebPError(int(self.status.max() or Status.OUT_OF_MEMORY), "wg_batch_create")
         self.n = n
         self.flags = flags
+        ctx._batches.add(self)
 
     def run(self, stream=None):
         st = lib().wg_batch_run(self._h, stream)
@@ -234,6 +254,7 @@ class Batch:
         if self._h:
             lib().wg_batch_destroy(self._h)
             self._h = None
+            self._ctx._batches.discard(self)
 
     def __del__(self):
         try:
@@ -246,6 +267,7 @@ class Context:
     """One decode context per HIP device (wg_ctx)."""
 
     def __init__(self, device=0, host_threads=0):
+        self._batches = weakref.WeakSet()
         self._h = lib().wg_ctx_create(device, host_threads)
         if not self._h:
             raise WebPError(Status.UNSUPPORTED_FEATURE, f"wg_ctx_create(device={device}) (no GPU?)")
@@ -275,6 +297,8 @@ class Context:
         return [o if s == Status.OK else None for o, s in zip(outs, status)], status
 
     def close(self):
+        for b in list(self._batches):
+            b.close()
         if self._h:
             lib().wg_ctx_destroy(self._h)
             self._h = None

@@ -708,3 +708,7 @@ void oracle_transform_block(const int16_t* in, uint8_t* dst4x4_bps32, int code) 
   if (code < 0) TransformOne(in, dst4x4_bps32);
   else DoTransform((uint32_t)code << 30, in, dst4x4_bps32);
 }
+
+/* Isolated 4x4 luma predictor (mode = B_* enum) on a BPS=32 workspace whose block origin
+ * is `dst` (known-answer tests of the device's per-pixel predictor table). */
+void oracle_pred_luma4(int mode, uint8_t* dst) { kPredLuma4[mode](dst); }

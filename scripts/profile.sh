@@ -1,0 +1,23 @@
+#!/bin/bash
+# rocprofv3 passes for the bench workload: kernel-trace stats, then PMC passes (separate runs).
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+TAG=${TAG:-r01}
+WL=${WL:-c3}
+OUT=gpurun_out/prof_$TAG
+mkdir -p $OUT
+BENCH="python3 bench.py --workload $WL --steps ${STEPS:-3} --warmup 1 --no-cpu-baseline"
+run() {  # run <name> <timeout> <rocprofv3 args...>
+  local name=$1 to=$2; shift 2
+  echo "=== $name"
+  timeout -k 10 $to rocprofv3 "$@" -d $OUT/$name -o $name --output-format csv -- $BENCH > $OUT/$name.log 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc"; tail -n 3 $OUT/$name.log
+  if [ $rc -ne 0 ]; then exit $rc; fi
+}
+run trace 600 --kernel-trace --stats
+if [ -n "$PMC1" ]; then run pmc1 600 --pmc $PMC1; fi
+if [ -n "$PMC2" ]; then run pmc2 600 --pmc $PMC2; fi
+if [ -n "$PMC3" ]; then run pmc3 600 --pmc $PMC3; fi
+if [ -n "$PMC4" ]; then run pmc4 600 --pmc $PMC4; fi
+find $OUT -name "*.csv" | head -50

@@ -1,0 +1,88 @@
+"""CPU tests of the C ABI boundary: the library loads, exports every declared symbol,
+and its host-only entry points (features / entropy stage) behave like libwebp's."""
+import ctypes as C
+import glob
+import os
+import re
+
+import numpy as np
+import pytest
+
+import webp_amd
+from oracle_lib import GOLDEN, ROOT, load_lossy, lossy_cases, manifest
+
+
+def test_library_exports_every_declared_symbol():
+    hdr = open(os.path.join(ROOT, "include", "gowebp_amd.h")).read()
+    declared = set(re.findall(r"^\w+\s*\*?\s+(wg_[a-z0-9_]+)\s*\(", hdr, re.M))
+    L = C.CDLL(webp_amd.LIB_PATH)
+    missing = [s for s in sorted(declared) if not hasattr(L, s)]
+    assert not missing, missing
+    assert declared == set(webp_amd.EXPORTED), declared ^ set(webp_amd.EXPORTED)
+
+
+def test_version():
+    assert webp_amd.lib().wg_version() == 0x000100
+
+
+@pytest.mark.parametrize("kind", ["lossy", "lossless", "bench"])
+def test_features_match_manifest(kind):
+    m = manifest()[kind]
+    for fn, ent in m.items():
+        name = fn if fn.endswith(".webp") else fn + ".webp"
+        data = open(os.path.join(GOLDEN, kind, name), "rb").read()
+        w, h, has_alpha = webp_amd.decode_config(data)
+        assert (w, h) == (ent["width"], ent["height"]), fn
+        f = webp_amd.features(data)
+        assert f.format == (2 if kind == "lossless" or fn.startswith("c5") else 1)
+        if "alpha" in fn:
+            assert has_alpha
+
+
+def test_features_error_statuses():
+    data, _ = load_lossy("synth_80x96")
+    S = webp_amd.Status
+    for bad, want in [(b"", S.NOT_ENOUGH_DATA), (data[:11], S.NOT_ENOUGH_DATA),
+                      (b"RIFF\x00\x00\x00\x00WEBPVP8 ", S.BITSTREAM_ERROR),
+                      (b"RIFX" + data[4:], None), (data[:20], S.NOT_ENOUGH_DATA)]:
+        with pytest.raises(webp_amd.WebPError) as e:
+            webp_amd.features(bad)
+        if want is not None:
+            assert e.value.status == want, (bad[:16], e.value.status)
+
+
+def test_truncated_frames_fail_in_entropy_stage():
+    data, _ = load_lossy("noise_96x64_complex_s0")
+    for cut in (30, 200, len(data) // 2, len(data) - 10):
+        with pytest.raises(webp_amd.WebPError) as e:
+            webp_amd.vp8_parse(data[:cut])
+        assert e.value.status in (webp_amd.Status.NOT_ENOUGH_DATA, webp_amd.Status.BITSTREAM_ERROR)
+
+
+def test_parse_info_fields():
+    m = manifest()["lossy"]
+    for name in lossy_cases():
+        data, _ = load_lossy(name)
+        info, mbs = webp_amd.vp8_parse(data, with_mbs=True)
+        hdr = m[name]["header"]
+        assert info.mb_w == (info.width + 15) // 16 and info.mb_h == (info.height + 15) // 16
+        assert info.num_parts == hdr["partitions"]
+        want_ft = 0 if hdr["level"] == 0 else (1 if hdr["simple"] else 2)
+        assert info.filter_type == want_ft
+        assert info.use_segment == hdr["segments"]
+        assert mbs.shape == (info.mb_w * info.mb_h,)
+        # f_limit is only set when the frame is filtered (PrecomputeFilterStrengths)
+        if want_ft == 0:
+            assert (mbs["f_limit"] == 0).all()
+
+
+def test_no_cpu_fallback_without_gpu():
+    """The product decode path fails loudly instead of falling back to a CPU path."""
+    if webp_amd.device_count() > 0:
+        pytest.skip("GPU present")
+    data, _ = load_lossy("synth_17x9")
+    with pytest.raises(webp_amd.WebPError) as e:
+        webp_amd.decode(data)
+    assert e.value.status == webp_amd.Status.UNSUPPORTED_FEATURE
+    with pytest.raises(webp_amd.WebPError):
+        webp_amd.Context(0)

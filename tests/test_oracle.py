@@ -176,3 +176,50 @@ def test_bench_frames_sha256(prefix):
         assert hashlib.sha256(out["rgba"].tobytes()).hexdigest() == ent["rgba"]
         assert hashlib.sha256(out["y"].tobytes()).hexdigest() == ent["y"]
         assert hashlib.sha256(out["u"].tobytes()).hexdigest() == ent["u"]
+
+
+def _pred4_table():
+    import os, re
+    from oracle_lib import ROOT
+    src = open(os.path.join(ROOT, "go-webp_amd", "csrc", "device", "pred4_table.inc")).read()
+    body = src[src.index("{"):]
+    return [int(v, 16) for v in re.findall(r"0x([0-9a-f]+)u", body)]
+
+
+def test_pred4_table_matches_oracle_predictors():
+    """The device's per-pixel recipe table (kind + 3 edge offsets) reproduces every
+    libwebp 4x4 predictor (dec.c.go:261-410) exactly, on random edges."""
+    tab = _pred4_table()
+    assert len(tab) == 160
+    L = oracle()
+    L.oracle_pred_luma4.argtypes = [C.c_int, C.c_void_p]
+    L.oracle_pred_luma4.restype = None
+    rng = np.random.default_rng(3)
+    BPS = 32
+    for it in range(400):
+        ws = rng.integers(0, 256, (8, BPS), dtype=np.uint8)
+        if it % 4 == 0:
+            ws[:] = rng.integers(0, 2) * 255  # saturating edges
+        org = 2 * BPS + 8  # block origin (row 2, col 8)
+        flat = ws.reshape(-1)
+        for mode in range(10):
+            ref = flat.copy()
+            L.oracle_pred_luma4(mode, ref.ctypes.data + org)
+            for y in range(4):
+                for x in range(4):
+                    w = tab[mode * 16 + y * 4 + x]
+                    kind = w >> 24
+                    offs = [((w >> (8 * k)) & 0xff) for k in range(3)]
+                    offs = [o - 256 if o >= 128 else o for o in offs]
+                    a, b, c = (int(flat[org + o]) for o in offs)
+                    if kind == 0:
+                        v = (a + 2 * b + c + 2) >> 2
+                    elif kind == 1:
+                        v = (a + b + 1) >> 1
+                    elif kind == 2:
+                        v = min(max(a + b - c, 0), 255)
+                    else:
+                        top = sum(int(flat[org - BPS + k]) for k in range(4))
+                        left = sum(int(flat[org + k * BPS - 1]) for k in range(4))
+                        v = (top + left + 4) >> 3
+                    assert v == ref[org + y * BPS + x], (mode, x, y)
