@@ -415,9 +415,9 @@ int wg_decode_rgba_into(const uint8_t* data, size_t size, uint8_t* rgba, size_t 
 
 int wg_yuv420_to_rgba_device(const uint8_t* y, const uint8_t* u, const uint8_t* v, int y_stride, int uv_stride,
                              uint8_t* rgba, int rgba_stride, int width, int height, int fancy, void* stream) {
-  if (!y || !u || !v || !rgba || width <= 0 || height <= 0 || rgba_stride < 4 * width || y_stride < width ||
-      uv_stride < (width + 1) / 2 || (y_stride & 7) || (uv_stride & 3) ||
-      (reinterpret_cast<uintptr_t>(y) & 7) || (reinterpret_cast<uintptr_t>(u) & 3) ||
+  if (!y || !u || !v || !rgba || width <= 0 || height <= 0 || rgba_stride < 4 * width ||
+      y_stride < ((width + 15) & ~15) || uv_stride < ((((width + 1) >> 1) + 7) & ~7) || (y_stride & 15) ||
+      (uv_stride & 3) || (reinterpret_cast<uintptr_t>(y) & 15) || (reinterpret_cast<uintptr_t>(u) & 3) ||
       (reinterpret_cast<uintptr_t>(v) & 3))
     return WG_STATUS_INVALID_PARAM;
   FrameDesc d{};

@@ -6,14 +6,22 @@
 //   EmitSampledRGB         pkg/libwebp/decoder/io_dec.c.go:53-59, dsp/yuv.go:19-58
 //   VP8YuvToRgba           R,G,B = YUVToR/G/B (pkg/color/yuv/conversion.go:28-49), A=0xff
 //
-// The line-pair upsampler with its packed-u/v "diagonal" trick is exactly the
-// separable 9-3-3-1 filter (9a + 3b + 3c + d + 8) >> 4 with edge replication
-// (tests/test_oracle.py::test_upsampler_closed_form), where for output pixel
-// (x, y): near chroma = (y>>1, x>>1), far row/col = near -/+ 1 toward the pixel,
-// clamped to the plane.  So every output pixel is independent: one thread makes an
-// 8-pixel x 2-row block (output rows 2p-1 and 2p share chroma rows p-1 and p),
-// reading 2 x 8 luma bytes and 2 x 2 x 6 chroma bytes and writing 64 RGBA bytes
-// with 16-byte stores.  Algorithmic traffic: W*H + 2*ceil(W/2)*ceil(H/2) bytes in,
+// The line-pair upsampler with its packed-u/v "diagonal" trick is exactly the separable
+// 9-3-3-1 filter (9a + 3b + 3c + d + 8) >> 4 with edge replication
+// (tests/test_oracle.py::test_upsampler_closed_form): for output pixel (x, y) the near
+// chroma sample is (y>>1, x>>1), the far row/column is near -/+ 1 toward the pixel,
+// clamped to the plane.  Written separably: v = 3*near_row + far_row per chroma column,
+// then pixel = (3*v[near_col] + v[far_col] + 8) >> 4.
+//
+// Work split: output rows 2p-1 and 2p ("pair p") both read chroma rows p-1 and p.  A wave
+// covers a 1024-pixel-wide strip and walks kPairs pairs down it, carrying chroma row p
+// into pair p+1 (each chroma row is loaded once per strip).  Lane l owns the four
+// 4-pixel groups x = x0 + 256k + 4l (k = 0..3), so every load and every 16-byte RGBA
+// store instruction of the wave touches one contiguous run (256 B of luma, 128 B per
+// chroma plane, 1 KB of RGBA): full cache lines, no partial-line write amplification.
+// A group needs chroma columns cb-1 .. cb+2 (cb = x/2); the outer two come from the
+// neighbouring lanes as one packed U/V dword through ds_bpermute, and only the wave's
+// edge lanes load them.  Algorithmic traffic: W*H + 2*ceil(W/2)*ceil(H/2) bytes in,
 // 4*W*H bytes out.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -24,8 +32,12 @@
 namespace wg {
 namespace {
 
-constexpr int kTileX = 64;  // 8-pixel groups per workgroup row (512 px)
-constexpr int kTileY = 4;   // row pairs per workgroup
+constexpr int kGroups = 4;                   // 4-pixel groups per lane per row
+constexpr int kStripPx = 64 * 4 * kGroups;   // pixels per wave row (1024)
+constexpr int kPairs = 16;                   // row pairs per wave strip (32 output rows)
+constexpr int kWavesPerWG = 4;
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 // clamp(v, 0, 255) as an opaque v_med3_i32.  Written in asm on purpose: ROCm 7.2 fuses
 // two `clamp(x >> 6)` + byte-pack sequences into gfx950's v_ashr_pk_u8_i32 and then
@@ -46,106 +58,197 @@ __device__ __forceinline__ uint32_t yuv_to_rgba(int y, int u, int v) {
   return clamp_u8(r) | (clamp_u8(g) << 8) | (clamp_u8(b) << 16) | 0xff000000u;
 }
 
-__device__ __forceinline__ int bsel(uint32_t w, int i) { return (w >> (8 * i)) & 0xff; }
+__device__ __forceinline__ int byte_of(uint32_t w, int i) { return (w >> (8 * i)) & 0xff; }
 
-// Chroma samples c0-1 .. c0+4 of one row as an array s[0..5] (clamped at the edges).
-struct Row6 { int s[6]; };
+__device__ __forceinline__ uint32_t bperm(uint32_t v, int src_lane) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane << 2, (int)v);
+}
 
-__device__ __forceinline__ Row6 load_row6(const uint8_t* row, int c0, int uv_w) {
-  Row6 r;
-  const uint32_t w = *reinterpret_cast<const uint32_t*>(row + c0);
-  const int last = uv_w - 1;
-  r.s[0] = row[max(c0 - 1, 0)];
-  r.s[1] = bsel(w, 0);
-  r.s[2] = c0 + 1 <= last ? bsel(w, 1) : r.s[1];
-  r.s[3] = c0 + 2 <= last ? bsel(w, 2) : r.s[2];
-  r.s[4] = c0 + 3 <= last ? bsel(w, 3) : r.s[3];
-  r.s[5] = c0 + 4 <= last ? row[c0 + 4] : r.s[4];
+// One chroma row as loaded by a lane: per group k the packed dword
+// U[cb] | U[cb+1] << 8 | V[cb] << 16 | V[cb+1] << 24 (cb = group's first chroma column,
+// cb+1 already replicated at the right edge), plus the wave-edge bytes: lane 0 holds
+// the column left of its group 0, lane 63 the column right of its group 3 (same packing,
+// U in byte 0, V in byte 2).
+struct ChromaRaw {
+  uint32_t p[kGroups];
+  uint32_t edge;
+};
+
+// Per group, the 4 chroma columns cb-1 .. cb+2 with edge replication:
+// u = U[cb-1] | U[cb] << 8 | U[cb+1] << 16 | U[cb+2] << 24, v likewise.
+struct ChromaWin {
+  uint32_t u[kGroups], v[kGroups];
+};
+
+__device__ __forceinline__ ChromaRaw load_chroma(gptr<const uint8_t> ur, gptr<const uint8_t> vr, int cb0, int uv_w,
+                                                 int lane, bool row_ok) {
+  ChromaRaw r;
+#pragma unroll
+  for (int k = 0; k < kGroups; ++k) {
+    const int cb = cb0 + 128 * k;
+    uint32_t u = 0, v = 0;
+    if (row_ok && cb < uv_w) {
+      u = *reinterpret_cast<gptr<const uint16_t>>(ur + cb);
+      v = *reinterpret_cast<gptr<const uint16_t>>(vr + cb);
+      if (cb + 1 >= uv_w) {  // odd width: column cb+1 replicates cb
+        u = (u & 0xff) * 0x101u;
+        v = (v & 0xff) * 0x101u;
+      }
+    }
+    r.p[k] = u | (v << 16);
+  }
+  r.edge = 0;
+  if (row_ok) {
+    const int ce = lane == 0 ? cb0 - 1 : cb0 + 128 * (kGroups - 1) + 2;
+    if ((lane == 0 && ce >= 0) || (lane == 63 && ce < uv_w)) r.edge = ur[ce] | ((uint32_t)vr[ce] << 16);
+  }
   return r;
 }
 
-// Upsampled chroma for the 8 pixels x0..x0+7 (x0 = 2*c0) of one output row.
-__device__ __forceinline__ void upsample8(const Row6& n, const Row6& f, int out[8]) {
+__device__ __forceinline__ ChromaWin make_win(const ChromaRaw& r, int cb0, int uv_w, int lane) {
+  ChromaWin w;
+  const int from_l = (lane + 63) & 63, from_r = (lane + 1) & 63;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int nc = 1 + (i >> 1);
-    const int fc = (i & 1) ? nc + 1 : nc - 1;
-    out[i] = (9 * n.s[nc] + 3 * n.s[fc] + 3 * f.s[nc] + f.s[fc] + 8) >> 4;
+  for (int k = 0; k < kGroups; ++k) {
+    const int cb = cb0 + 128 * k;
+    // neighbour lanes' packed dwords; lane 63 / lane 0 forward the adjacent group's so the
+    // rotation across the wave boundary lands on the right column.
+    uint32_t lp = bperm(lane == 63 && k > 0 ? r.p[k - 1] : r.p[k], from_l) >> 8;  // U[cb-1] b0, V[cb-1] b2
+    uint32_t rp = bperm(lane == 0 && k + 1 < kGroups ? r.p[k + 1] : r.p[k], from_r);  // U[cb+2] b0, V b2
+    if (lane == 0 && k == 0) lp = r.edge;
+    if (lane == 63 && k == kGroups - 1) rp = r.edge;
+    const uint32_t s = r.p[k];
+    uint32_t ul = lp & 0xff, vl = (lp >> 16) & 0xff;
+    uint32_t ur = rp & 0xff, vr = (rp >> 16) & 0xff;
+    if (cb == 0) {
+      ul = s & 0xff;
+      vl = (s >> 16) & 0xff;
+    }
+    if (cb + 2 >= uv_w) {
+      ur = (s >> 8) & 0xff;
+      vr = s >> 24;
+    }
+    w.u[k] = ul | ((s & 0xffff) << 8) | (ur << 24);
+    w.v[k] = vl | ((s >> 16) << 8) | (vr << 24);
   }
+  return w;
 }
 
-__device__ __forceinline__ void store8(uint8_t* dst, const uint32_t px[8], int nvalid, bool aligned) {
-  if (aligned && nvalid == 8) {
-    reinterpret_cast<uint4*>(dst)[0] = make_uint4(px[0], px[1], px[2], px[3]);
-    reinterpret_cast<uint4*>(dst)[1] = make_uint4(px[4], px[5], px[6], px[7]);
+// 4 pixels of group k: near/far chroma windows (n, f), luma dword.
+__device__ __forceinline__ u32x4 convert_group(uint32_t nu, uint32_t fu, uint32_t nv, uint32_t fv, uint32_t yw) {
+  int a[4], b[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    a[j] = 3 * byte_of(nu, j) + byte_of(fu, j);
+    b[j] = 3 * byte_of(nv, j) + byte_of(fv, j);
+  }
+  // pixel 2c: near column c, far column c-1; pixel 2c+1: far column c+1
+  const int u0 = (3 * a[1] + a[0] + 8) >> 4, u1 = (3 * a[1] + a[2] + 8) >> 4;
+  const int u2 = (3 * a[2] + a[1] + 8) >> 4, u3 = (3 * a[2] + a[3] + 8) >> 4;
+  const int v0 = (3 * b[1] + b[0] + 8) >> 4, v1 = (3 * b[1] + b[2] + 8) >> 4;
+  const int v2 = (3 * b[2] + b[1] + 8) >> 4, v3 = (3 * b[2] + b[3] + 8) >> 4;
+  return u32x4{yuv_to_rgba(byte_of(yw, 0), u0, v0), yuv_to_rgba(byte_of(yw, 1), u1, v1),
+               yuv_to_rgba(byte_of(yw, 2), u2, v2), yuv_to_rgba(byte_of(yw, 3), u3, v3)};
+}
+
+__device__ __forceinline__ void store_group(gptr<uint8_t> dst, u32x4 px, int nvalid, bool aligned) {
+  if (aligned && nvalid >= 4) {
+    __builtin_nontemporal_store(px, reinterpret_cast<gptr<u32x4>>(dst));
   } else {
-    for (int i = 0; i < 8; ++i)
-      if (i < nvalid) reinterpret_cast<uint32_t*>(dst)[i] = px[i];
+    gptr<uint32_t> d = reinterpret_cast<gptr<uint32_t>>(dst);
+    if (nvalid > 0) d[0] = px.x;
+    if (nvalid > 1) d[1] = px.y;
+    if (nvalid > 2) d[2] = px.z;
+    if (nvalid > 3) d[3] = px.w;
   }
 }
 
 template <bool kFancy>
-__global__ void __launch_bounds__(256) yuv_to_rgba_kernel(const FrameDesc* __restrict__ frames, FrameDesc single,
-                                                          int use_single) {
+__global__ void __launch_bounds__(64 * kWavesPerWG) yuv_to_rgba_kernel(const FrameDesc* __restrict__ frames,
+                                                                       FrameDesc single, int use_single) {
   const FrameDesc& F = use_single ? single : frames[blockIdx.y];
   if (!F.valid) return;
   const int W = F.width, H = F.height;
   const int uv_w = (W + 1) >> 1, uv_h = (H + 1) >> 1;
-  const int groups = (W + 7) >> 3;
-  const int gx_tiles = (groups + kTileX - 1) / kTileX;
-  const int tile = blockIdx.x;
-  const int tx = tile % gx_tiles, ty = tile / gx_tiles;
-  const int g = tx * kTileX + (threadIdx.x & (kTileX - 1));
-  const int p = ty * kTileY + (threadIdx.x / kTileX);
-  const int npairs = kFancy ? (H >> 1) + 1 : (H + 1) >> 1;
-  if (g >= groups || p >= npairs) return;
-  const int x0 = 8 * g, c0 = 4 * g;
-  const int nvalid = min(8, W - x0);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int strips_x = (W + kStripPx - 1) / kStripPx;
+  const int tx = blockIdx.x % strips_x, ty = blockIdx.x / strips_x;
+  const int xl = tx * kStripPx + 4 * lane;  // group k pixel x = xl + 256k
+  const int cb0 = xl >> 1;
   const bool aligned = ((F.rgba_stride & 15) == 0) && ((reinterpret_cast<uintptr_t>(F.rgba) & 15) == 0);
-  const uint8_t* Y = F.y;
-  const uint8_t* U = F.u;
-  const uint8_t* V = F.v;
-  if (kFancy) {
-    // output rows ya = 2p-1 (odd) and yb = 2p (even); chroma rows r0 = p-1, r1 = p (clamped)
-    const int ya = 2 * p - 1, yb = 2 * p;
-    const int r0 = max(p - 1, 0), r1 = min(p, uv_h - 1);
-    const Row6 u0 = load_row6(U + (size_t)r0 * F.uv_stride, c0, uv_w);
-    const Row6 u1 = load_row6(U + (size_t)r1 * F.uv_stride, c0, uv_w);
-    const Row6 v0 = load_row6(V + (size_t)r0 * F.uv_stride, c0, uv_w);
-    const Row6 v1 = load_row6(V + (size_t)r1 * F.uv_stride, c0, uv_w);
-    if (ya >= 0) {  // near = r0, far = r1
-      const uint2 yy = *reinterpret_cast<const uint2*>(Y + (size_t)ya * F.y_stride + x0);
-      int uu[8], vv[8];
-      upsample8(u0, u1, uu);
-      upsample8(v0, v1, vv);
-      uint32_t px[8];
+  const gptr<const uint8_t> Y = as_global(static_cast<const uint8_t*>(F.y));
+  const gptr<const uint8_t> U = as_global(static_cast<const uint8_t*>(F.u));
+  const gptr<const uint8_t> V = as_global(static_cast<const uint8_t*>(F.v));
+  const gptr<uint8_t> out = as_global(F.rgba);
+  const int ys = F.y_stride, uvs = F.uv_stride, os = F.rgba_stride;
+
+  auto load_luma = [&](int row, uint32_t yw[kGroups]) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) px[i] = yuv_to_rgba(bsel(i < 4 ? yy.x : yy.y, i & 3), uu[i], vv[i]);
-      store8(F.rgba + (size_t)ya * F.rgba_stride + 4 * x0, px, nvalid, aligned);
+    for (int k = 0; k < kGroups; ++k) {
+      const int x = xl + 256 * k;
+      yw[k] = (row >= 0 && row < H && x < W) ? *reinterpret_cast<gptr<const uint32_t>>(Y + (size_t)row * ys + x) : 0u;
     }
-    if (yb < H) {  // near = r1, far = r0
-      const uint2 yy = *reinterpret_cast<const uint2*>(Y + (size_t)yb * F.y_stride + x0);
-      int uu[8], vv[8];
-      upsample8(u1, u0, uu);
-      upsample8(v1, v0, vv);
-      uint32_t px[8];
+  };
+
+  if (kFancy) {
+    const int npairs = (H >> 1) + 1;  // pair p: output rows 2p-1, 2p
+    const int p0 = (ty * kWavesPerWG + wave) * kPairs;
+    if (p0 >= npairs) return;
+    const int p1 = min(p0 + kPairs, npairs);
+    const int rp = max(p0 - 1, 0), rc = min(p0, uv_h - 1);
+    const ChromaRaw raw_prev = load_chroma(U + (size_t)rp * uvs, V + (size_t)rp * uvs, cb0, uv_w, lane, true);
+    ChromaRaw raw_cur = load_chroma(U + (size_t)rc * uvs, V + (size_t)rc * uvs, cb0, uv_w, lane, true);
+    ChromaWin wp = make_win(raw_prev, cb0, uv_w, lane);
+    for (int p = p0; p < p1; ++p) {
+      const int ya = 2 * p - 1, yb = 2 * p;
+      uint32_t yA[kGroups], yB[kGroups];
+      load_luma(ya, yA);
+      load_luma(yb, yB);
+      const int rn = min(p + 1, uv_h - 1);  // chroma row for the next pair
+      const ChromaRaw raw_next = load_chroma(U + (size_t)rn * uvs, V + (size_t)rn * uvs, cb0, uv_w, lane, p + 1 < p1);
+      const ChromaWin wc = make_win(raw_cur, cb0, uv_w, lane);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) px[i] = yuv_to_rgba(bsel(i < 4 ? yy.x : yy.y, i & 3), uu[i], vv[i]);
-      store8(F.rgba + (size_t)yb * F.rgba_stride + 4 * x0, px, nvalid, aligned);
+      for (int k = 0; k < kGroups; ++k) {
+        const int x = xl + 256 * k;
+        const int nvalid = W - x;
+        if (nvalid <= 0) continue;
+        if (ya >= 0)  // near = chroma row p-1, far = row p
+          store_group(out + (size_t)ya * os + 4 * x, convert_group(wp.u[k], wc.u[k], wp.v[k], wc.v[k], yA[k]), nvalid,
+                      aligned);
+        if (yb < H)  // near = chroma row p, far = row p-1
+          store_group(out + (size_t)yb * os + 4 * x, convert_group(wc.u[k], wp.u[k], wc.v[k], wp.v[k], yB[k]), nvalid,
+                      aligned);
+      }
+      wp = wc;
+      raw_cur = raw_next;
     }
   } else {
     // point sampling: rows 2p and 2p+1 both use chroma row p (WebPSamplerProcessPlane)
-    const uint32_t uw = *reinterpret_cast<const uint32_t*>(U + (size_t)p * F.uv_stride + c0);
-    const uint32_t vw = *reinterpret_cast<const uint32_t*>(V + (size_t)p * F.uv_stride + c0);
-    for (int k = 0; k < 2; ++k) {
-      const int yr = 2 * p + k;
-      if (yr >= H) break;
-      const uint2 yy = *reinterpret_cast<const uint2*>(Y + (size_t)yr * F.y_stride + x0);
-      uint32_t px[8];
+    const int npairs = (H + 1) >> 1;
+    const int p0 = (ty * kWavesPerWG + wave) * kPairs;
+    if (p0 >= npairs) return;
+    const int p1 = min(p0 + kPairs, npairs);
+    for (int p = p0; p < p1; ++p) {
+      uint32_t yA[kGroups], yB[kGroups];
+      load_luma(2 * p, yA);
+      load_luma(2 * p + 1, yB);
+      const ChromaRaw c = load_chroma(U + (size_t)p * uvs, V + (size_t)p * uvs, cb0, uv_w, lane, true);
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
-        px[i] = yuv_to_rgba(bsel(i < 4 ? yy.x : yy.y, i & 3), bsel(uw, i >> 1), bsel(vw, i >> 1));
-      store8(F.rgba + (size_t)yr * F.rgba_stride + 4 * x0, px, nvalid, aligned);
+      for (int k = 0; k < kGroups; ++k) {
+        const int x = xl + 256 * k;
+        const int nvalid = W - x;
+        if (nvalid <= 0) continue;
+        const int u0 = byte_of(c.p[k], 0), u1 = byte_of(c.p[k], 1), v0 = byte_of(c.p[k], 2), v1 = byte_of(c.p[k], 3);
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+          const int yr = 2 * p + r;
+          if (yr >= H) break;
+          const uint32_t yw = r ? yB[k] : yA[k];
+          const u32x4 px{yuv_to_rgba(byte_of(yw, 0), u0, v0), yuv_to_rgba(byte_of(yw, 1), u0, v0),
+                         yuv_to_rgba(byte_of(yw, 2), u1, v1), yuv_to_rgba(byte_of(yw, 3), u1, v1)};
+          store_group(out + (size_t)yr * os + 4 * x, px, nvalid, aligned);
+        }
+      }
     }
   }
 }
@@ -154,17 +257,18 @@ __global__ void __launch_bounds__(256) yuv_to_rgba_kernel(const FrameDesc* __res
 
 hipError_t launch_yuv_to_rgba(const FrameDesc* d_frames, const FrameDesc* single, int n_frames, int max_w,
                               int max_h, int fancy, hipStream_t stream) {
-  const int groups = (max_w + 7) >> 3;
-  const int gx = (groups + kTileX - 1) / kTileX;
+  const int strips_x = (max_w + kStripPx - 1) / kStripPx;
   const int npairs = (max_h >> 1) + 1;
-  const int gy = (npairs + kTileY - 1) / kTileY;
-  const dim3 grid(gx * gy, single ? 1 : n_frames);
+  const int strips_y = (npairs + kPairs * kWavesPerWG - 1) / (kPairs * kWavesPerWG);
+  const dim3 grid(strips_x * strips_y, single ? 1 : n_frames);
   FrameDesc s{};
   if (single) s = *single;
   if (fancy)
-    hipLaunchKernelGGL(yuv_to_rgba_kernel<true>, grid, dim3(256), 0, stream, d_frames, s, single ? 1 : 0);
+    hipLaunchKernelGGL(yuv_to_rgba_kernel<true>, grid, dim3(64 * kWavesPerWG), 0, stream, d_frames, s,
+                       single ? 1 : 0);
   else
-    hipLaunchKernelGGL(yuv_to_rgba_kernel<false>, grid, dim3(256), 0, stream, d_frames, s, single ? 1 : 0);
+    hipLaunchKernelGGL(yuv_to_rgba_kernel<false>, grid, dim3(64 * kWavesPerWG), 0, stream, d_frames, s,
+                       single ? 1 : 0);
   return hipGetLastError();
 }
 

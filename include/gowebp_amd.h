@@ -120,7 +120,11 @@ int wg_batch_download_yuv(wg_batch* b, int i, uint8_t* y, uint8_t* u, uint8_t* v
 /* ---- stage entry point: YUV420 -> RGBA on device pointers ---------------------------- */
 /* Fancy (fancy!=0, UpsampleRgbaLinePair, upsampling.c.go:43-107) or point-sampled
  * (EmitSampledRGB, io_dec.c.go:53-59) conversion of one frame; all pointers are device
- * pointers.  Asynchronous on `stream`. */
+ * pointers.  Asynchronous on `stream`.  The kernel reads planes in 16-byte (luma) and
+ * 8-byte (chroma) groups, so: y and y_stride 16-byte aligned with
+ * y_stride >= round_up(width, 16); u, v and uv_stride 4-byte aligned with
+ * uv_stride >= round_up((width+1)/2, 8) (the batch's MB-padded planes satisfy this).
+ * Anything else -> WG_STATUS_INVALID_PARAM. */
 int wg_yuv420_to_rgba_device(const uint8_t* y, const uint8_t* u, const uint8_t* v,
                              int y_stride, int uv_stride, uint8_t* rgba, int rgba_stride,
                              int width, int height, int fancy, void* stream);

@@ -129,9 +129,9 @@ def test_yuv_to_rgba_device_stage_vs_oracle():
     """Stage entry point on torch device tensors, random planes incl. odd sizes."""
     import torch
     rng = np.random.default_rng(5)
-    for (h, w) in [(1, 1), (3, 5), (17, 33), (64, 64), (270, 481), (1080, 1920)]:
+    for (h, w) in [(1, 1), (3, 5), (17, 33), (64, 64), (129, 1041), (270, 481), (1080, 1920)]:
         uw, uh = (w + 1) // 2, (h + 1) // 2
-        ys, uvs = (w + 7) // 8 * 8 + 8, (uw + 3) // 4 * 4 + 4
+        ys, uvs = (w + 15) // 16 * 16 + 16, (uw + 7) // 8 * 8 + 4
         Y = rng.integers(0, 256, (h, ys), dtype=np.uint8)
         U = rng.integers(0, 256, (uh, uvs), dtype=np.uint8)
         V = rng.integers(0, 256, (uh, uvs), dtype=np.uint8)
