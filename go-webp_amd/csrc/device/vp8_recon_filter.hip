@@ -27,7 +27,8 @@
 // (tests/test_oracle.py::test_transform_shortcuts_exact).
 //
 // Loop filter (per MB, libwebp edge order): lanes 0..15 luma lines, 16..31 chroma
-// lines; branch-free FilterLoop26/24 / simple-filter math in a per-MB LDS window.
+// lines, one pass of FilterLoop26/24 / simple-filter math per edge step in a per-MB LDS
+// window (8 passes per MB).
 //
 // Memory.  Cross-MB state lives in LDS only: the unfiltered top samples `ytop`
 // (VP8TopSamples), the final bottom rows `fbot` of each MB column for the next row's
@@ -159,11 +160,18 @@ __device__ __forceinline__ int sclip2(int v) { return min(max(v, -16), 15); }
 // KIND 1: complex MB edge (FilterLoop26: hev ? DoFilter2 : DoFilter6, :592-606);
 // KIND 2: complex inner edge (FilterLoop24: hev ? DoFilter2 : DoFilter4, :608-622).
 // Branch-free: every variant is computed and selected.  t2 = 2*thresh + 1.
+// |a - b| (+ c) for byte values in one v_sad_u32 (sub/neg/max otherwise).
+__device__ __forceinline__ int absd(int a, int b, int c = 0) {
+  int r;
+  asm("v_sad_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
 template <int KIND>
 __device__ __forceinline__ void filter_line(Line& l, int t2, int it, int hev_t) {
   const int d0 = l.q0 - l.p0;
   const int sp = sclip1(l.p1 - l.q1);
-  const bool edge_ok = 4 * abs(d0) + abs(l.p1 - l.q1) <= t2;
+  const bool edge_ok = absd(l.p1, l.q1, 4 * absd(l.p0, l.q0)) <= t2;
   // DoFilter2
   const int a = 3 * d0 + sp;
   const int f2p0 = clamp255(l.p0 + sclip2((a + 3) >> 3));
@@ -173,10 +181,11 @@ __device__ __forceinline__ void filter_line(Line& l, int t2, int it, int hev_t) 
     l.q0 = edge_ok ? f2q0 : l.q0;
     return;
   }
-  const int in_p = max(max(abs(l.p3 - l.p2), abs(l.p2 - l.p1)), abs(l.p1 - l.p0));
-  const int in_q = max(max(abs(l.q3 - l.q2), abs(l.q2 - l.q1)), abs(l.q1 - l.q0));
+  const int dp = absd(l.p1, l.p0), dq = absd(l.q1, l.q0);
+  const int in_p = max(max(absd(l.p3, l.p2), absd(l.p2, l.p1)), dp);
+  const int in_q = max(max(absd(l.q3, l.q2), absd(l.q2, l.q1)), dq);
   const bool on = edge_ok && max(in_p, in_q) <= it;
-  const bool hv = max(abs(l.p1 - l.p0), abs(l.q1 - l.q0)) > hev_t;
+  const bool hv = max(dp, dq) > hev_t;
   const bool f2 = on && hv, fx = on && !hv;
   if (KIND == 1) {  // DoFilter6
     const int w = sclip1(a);
@@ -229,38 +238,39 @@ __device__ __forceinline__ void filter_col(uint8_t* p, int s, int t2, int it, in
 }
 
 // The eight edge steps of DoFilter (frame_dec.c.go:204-251) for one MB per half-wave.
-// Lanes 0..15: luma line l; 16..31: chroma line (plane (l>>3)&1, index l&7), complex only.
+// Lane l < 16 filters luma line l; lanes 16..31 chroma line l&7 of plane U (16..23) or
+// V (24..31), complex filter only.  Each lane addresses its own plane window (base and
+// stride), so a step that covers luma and chroma is ONE pass of the filter code.  Window
+// offsets coincide: MB edge at window column/row 4, the chroma inner edge and the first
+// luma inner edge at 8; luma inner edges 12 and 16 are luma-only steps.
 template <bool kComplex>
 __device__ __forceinline__ void filter_mb(uint8_t* fw, int l, bool on, bool fx, bool fy, bool fin, int limit,
                                           int ilevel, int hev_t) {
   constexpr int KMB = kComplex ? 1 : 0, KIN = kComplex ? 2 : 0;
   const int t_mb = 2 * (limit + 4) + 1, t_in = 2 * limit + 1;
   const bool luma = l < 16;
-  const bool chroma = kComplex && !luma;
-  const int li = l & 15, cl = l & 7;
-  uint8_t* cwin = fw + ((l >> 3) & 1 ? kFwV : kFwU);
-  uint8_t* yrow = fw + kFwY + (li + 4) * FWY;
-  uint8_t* crow = cwin + (cl + 4) * FWC;
-  const bool lx = on && fx, lin = on && fin, ly = on && fy;
-  if (lx && luma) filter_row<KMB>(yrow + 4, t_mb, ilevel, hev_t);  // HFilter16 / SimpleHFilter16
-  if (lx && chroma) filter_row<KMB>(crow + 4, t_mb, ilevel, hev_t);  // HFilter8
+  const bool lane_on = on && (luma || kComplex);
+  const int li = luma ? l : (l & 7);
+  const int st = luma ? FWY : FWC;
+  uint8_t* win = fw + (luma ? kFwY : ((l >> 3) & 1 ? kFwV : kFwU));
+  uint8_t* row = win + (li + 4) * st;  // line li, for vertical edges
+  uint8_t* col = win + 4 + li;         // column li, for horizontal edges
+  const bool lx = lane_on && fx, lin = lane_on && fin, ly = lane_on && fy;
+  if (lx) filter_row<KMB>(row + 4, t_mb, ilevel, hev_t);  // HFilter16 / HFilter8 / SimpleHFilter16
   lds_sync();
-  if (lin && luma) filter_row<KIN>(yrow + 8, t_in, ilevel, hev_t);  // HFilter16i
-  if (lin && chroma) filter_row<KIN>(crow + 8, t_in, ilevel, hev_t);  // HFilter8i
+  if (lin) filter_row<KIN>(row + 8, t_in, ilevel, hev_t);  // HFilter16i (first) / HFilter8i
   lds_sync();
-  if (lin && luma) filter_row<KIN>(yrow + 12, t_in, ilevel, hev_t);
+  if (lin && luma) filter_row<KIN>(row + 12, t_in, ilevel, hev_t);
   lds_sync();
-  if (lin && luma) filter_row<KIN>(yrow + 16, t_in, ilevel, hev_t);
+  if (lin && luma) filter_row<KIN>(row + 16, t_in, ilevel, hev_t);
   lds_sync();
-  if (ly && luma) filter_col<KMB>(fw + kFwY + 4 * FWY + 4 + li, FWY, t_mb, ilevel, hev_t);  // VFilter16
-  if (ly && chroma) filter_col<KMB>(cwin + 4 * FWC + 4 + cl, FWC, t_mb, ilevel, hev_t);   // VFilter8
+  if (ly) filter_col<KMB>(col + 4 * st, st, t_mb, ilevel, hev_t);  // VFilter16 / VFilter8
   lds_sync();
-  if (lin && luma) filter_col<KIN>(fw + kFwY + 8 * FWY + 4 + li, FWY, t_in, ilevel, hev_t);  // VFilter16i
-  if (lin && chroma) filter_col<KIN>(cwin + 8 * FWC + 4 + cl, FWC, t_in, ilevel, hev_t);   // VFilter8i
+  if (lin) filter_col<KIN>(col + 8 * st, st, t_in, ilevel, hev_t);  // VFilter16i (first) / VFilter8i
   lds_sync();
-  if (lin && luma) filter_col<KIN>(fw + kFwY + 12 * FWY + 4 + li, FWY, t_in, ilevel, hev_t);
+  if (lin && luma) filter_col<KIN>(col + 12 * FWY, FWY, t_in, ilevel, hev_t);
   lds_sync();
-  if (lin && luma) filter_col<KIN>(fw + kFwY + 16 * FWY + 4 + li, FWY, t_in, ilevel, hev_t);
+  if (lin && luma) filter_col<KIN>(col + 16 * FWY, FWY, t_in, ilevel, hev_t);
   lds_sync();
 }
 

@@ -1,0 +1,69 @@
+#!/usr/bin/env python3
+"""Static instruction mix per section of the K1 loop body.
+
+Copies vp8_recon_filter.hip with `asm volatile(";MARK name")` inserted before the section
+comments listed below, compiles it for gfx950 and counts VALU/SALU/LDS/VMEM instructions
+between markers.  Static counts (loops and both filter variants counted once), useful for
+before/after comparisons of a change.
+"""
+import collections
+import glob
+import os
+import re
+import subprocess
+import sys
+import tempfile
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SRC = os.path.join(HERE, "..", "go-webp_amd", "csrc", "device", "vp8_recon_filter.hip")
+MARKS = [("// ---- software pipeline", "prefetch"), ("// ---- wait for the previous pair", "wait"),
+         ("// ---- ReconstructRow prologue", "prologue"), ("// ---- top samples", "top"),
+         ("// ---- residuals of all blocks", "idct"), ("// ---- luma prediction + residual", "lumapred"),
+         ("if (__any(act && i4))", "i4"), ("// ---- chroma prediction + residual", "chroma"),
+         ("// ---- stash unfiltered bottom", "window"), ("// ---- loop filter on the window", "filter"),
+         ("// ---- deposit final bottom rows", "deposit"), ("// ---- final pixels to HBM", "hbm"),
+         ("// ---- rotate for the next MB", "rotate"), ("rc = rn;", "end")]
+
+
+def main():
+    src = sys.argv[1] if len(sys.argv) > 1 else SRC
+    d = os.path.dirname(os.path.abspath(src))
+    s = open(src).read()
+    for m, name in MARKS:
+        if m in s:
+            s = s.replace(m, 'asm volatile(";MARK %s");\n      ' % name + m, 1)
+    for inc in re.findall(r'#include "([^"]+)"', s):
+        s = s.replace(f'#include "{inc}"', f'#include "{os.path.normpath(os.path.join(d, inc))}"')
+    with tempfile.TemporaryDirectory() as t:
+        f = os.path.join(t, "k.hip")
+        open(f, "w").write(s)
+        subprocess.check_call(["/opt/rocm/lib/llvm/bin/clang++", "--offload-arch=gfx950", "-O3", "-std=c++17", "-x",
+                               "hip", "-c", f, "--cuda-device-only", "-save-temps=obj", "-o",
+                               os.path.join(t, "k.o")], cwd=t)
+        asm = glob.glob(os.path.join(t, "*gfx950*.s"))[0]
+        cur, cnt = "pre", collections.OrderedDict()
+        meta = {}
+        for line in open(asm):
+            m = re.search(r";MARK (\w+)", line)
+            if m:
+                cur = m.group(1)
+                continue
+            m = re.match(r"\s+\.(vgpr_count|sgpr_count|private_segment_fixed_size):\s+(\d+)", line)
+            if m:
+                meta[m.group(1)] = m.group(2)
+            tok = line.strip().split()
+            if not tok or tok[0].startswith((".", ";")) or tok[0].endswith(":"):
+                continue
+            op = tok[0]
+            cls = ("valu" if op.startswith("v_") else "salu" if op.startswith("s_") else "lds" if op.startswith("ds_")
+                   else "vmem" if op.startswith(("global_", "buffer_", "flat_")) else "other")
+            cnt.setdefault(cur, collections.Counter())[cls] += 1
+    tot = collections.Counter()
+    for k, v in cnt.items():
+        print(f"{k:10s} " + " ".join(f"{c}={v[c]}" for c in ("valu", "salu", "lds", "vmem")))
+        tot += v
+    print("total      " + " ".join(f"{c}={tot[c]}" for c in ("valu", "salu", "lds", "vmem")), meta)
+
+
+if __name__ == "__main__":
+    main()
