@@ -63,6 +63,7 @@ constexpr int kProgBytes = 64;  // reserved (progress lives in a static __shared
 constexpr int kTabBytes = 640;
 constexpr int kHdrBytes = kProgBytes + kTabBytes;
 constexpr int kColBytes = 32 + 128;  // ytop (y16 u8 v8) + fbot (Y 4x16, U 4x8, V 4x8)
+constexpr uint32_t kDrop = 0x80000000u;  // buffer offset beyond any frame: store dropped
 
 __device__ __forceinline__ void lds_sync() {
   // LDS ops of one wave complete in order; this makes every lane's earlier LDS write
@@ -124,6 +125,20 @@ __device__ __forceinline__ void idct_quad(int q, uint2 cv, int r[4]) {
   r[1] = (b + c) >> 3;
   r[2] = (b - c) >> 3;
   r[3] = (a - d) >> 3;
+}
+
+// Residuals of one IDCT pass (3 per MB: luma blocks b0, b0+8, chroma).  When every block
+// in the pass (both half-waves) is zero or DC-only, TransformOne reduces to
+// (in[0] + 4) >> 3 on every pixel (TransformDC, dec.c.go:112-118): broadcast the DC from
+// the quad's column-0 lane instead of running both butterfly passes.
+__device__ __forceinline__ void idct_pass(int q, uint2 cv, int r[4]) {
+  const uint32_t ac = (q == 0 ? (cv.x & 0xffff0000u) : cv.x) | cv.y;
+  if (__all(ac == 0)) {
+    const int dc = __builtin_amdgcn_mov_dpp((int)(int16_t)(cv.x & 0xffff), 0x00, 0xF, 0xF, true);
+    r[0] = r[1] = r[2] = r[3] = (dc + 4) >> 3;
+  } else {
+    idct_quad(q, cv, r);
+  }
 }
 
 __device__ __forceinline__ uint32_t add_res(uint32_t pred, const int r[4]) {
@@ -313,9 +328,11 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
   const gptr<const uint32_t> mbs = as_global(reinterpret_cast<const uint32_t*>(F->mbs));
   const gptr<const uint32_t> row_block0 = as_global(F->row_block0);
   const gptr<const uint32_t> blocks = as_global(reinterpret_cast<const uint32_t*>(F->blocks));
-  const gptr<uint8_t> Yp = as_global(F->y);
-  const gptr<uint8_t> Up = as_global(F->u);
-  const gptr<uint8_t> Vp = as_global(F->v);
+  // One buffer descriptor over the frame's planes: the batch allocates Y, U, V of a frame
+  // back to back (capi.cpp), so U and V are 32-bit offsets from Y.
+  const uint32_t uoff = (uint32_t)(F->u - F->y), voff = (uint32_t)(F->v - F->y);
+  const __amdgpu_buffer_rsrc_t planes =
+      __builtin_amdgcn_make_buffer_rsrc(F->y, 0, (int)(voff + (uint32_t)(8 * mb_h * uvs)), 0x00020000);
 
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
@@ -419,9 +436,9 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
 
       // ---- residuals of all blocks (prediction-independent)
       int ry0[4], ry1[4], rcr[4];
-      idct_quad(q, cc.y0, ry0);
-      idct_quad(q, cc.y1, ry1);
-      idct_quad(q, cc.c, rcr);
+      idct_pass(q, cc.y0, ry0);
+      idct_pass(q, cc.y1, ry1);
+      idct_pass(q, cc.c, rcr);
 
       // ---- luma prediction + residual
       const int row_a = 4 * lby + q, row_b = row_a + 8;
@@ -565,44 +582,49 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
             }
           }
         }
-        // ---- final pixels to HBM (each byte written once)
-        {  // luma rows 0..nrows_y-1, window cols -4..11 (dword q = cols 4q-4..4q-1)
-          const int r0 = b0, r1 = b0 + 8;
-          if (q > 0 || x > 0) {
-            if (r0 < nrows_y)
-              *reinterpret_cast<gptr<uint32_t>>(Yp + (size_t)(16 * y + r0) * ys + 16 * x - 4 + 4 * q) =
-                  ld32(fw + kFwY + (r0 + 4) * FWY + 4 * q);
-            if (r1 < nrows_y)
-              *reinterpret_cast<gptr<uint32_t>>(Yp + (size_t)(16 * y + r1) * ys + 16 * x - 4 + 4 * q) =
-                  ld32(fw + kFwY + (r1 + 4) * FWY + 4 * q);
-          }
-        }
-        if (l < 16) {
-          if (y > 0 && l < 12) {  // luma rows -3..-1 of the MB above, cols 0..15
-            const int rr = (l >> 2) - 3, d = l & 3;
-            *reinterpret_cast<gptr<uint32_t>>(Yp + (size_t)(16 * y + rr) * ys + 16 * x + 4 * d) =
-                ld32(fw + kFwY + (rr + 4) * FWY + 4 + 4 * d);
-          }
-          if (last_x && l < nrows_y)  // last column: luma cols 12..15
-            *reinterpret_cast<gptr<uint32_t>>(Yp + (size_t)(16 * y + l) * ys + 16 * x + 12) =
-                ld32(fw + kFwY + (l + 4) * FWY + 16);
-        } else {
-          const int kk = l - 16, p = kk >> 3, r = kk & 7;
-          if (last_x && r < nrows_c)  // last column: chroma cols 4..7
-            *reinterpret_cast<gptr<uint32_t>>((p ? Vp : Up) + (size_t)(8 * y + r) * uvs + 8 * x + 4) =
-                ld32(fw + (p ? kFwV : kFwU) + (r + 4) * FWC + 8);
-        }
-        {  // chroma rows 0..nrows_c-1, cols -4..3
-          const int p = l >> 4, r = (l >> 1) & 7, d = l & 1;
-          if (r < nrows_c && (d > 0 || x > 0))
-            *reinterpret_cast<gptr<uint32_t>>((p ? Vp : Up) + (size_t)(8 * y + r) * uvs + 8 * x - 4 + 4 * d) =
-                ld32(fw + (p ? kFwV : kFwU) + (r + 4) * FWC + 4 * d);
-        }
-        if (y > 0 && l < 12) {  // chroma rows -3..-1 of the MB above, cols 0..7
-          const int p = l / 6, rem = l - 6 * p, rr = (rem >> 1) - 3, d = rem & 1;
-          *reinterpret_cast<gptr<uint32_t>>((p ? Vp : Up) + (size_t)(8 * y + rr) * uvs + 8 * x + 4 * d) =
-              ld32(fw + (p ? kFwV : kFwU) + (rr + 4) * FWC + 4 + 4 * d);
-        }
+      }
+      // ---- final pixels to HBM (each byte written once).  Five dword slots per lane, all
+      //      buffer stores against one descriptor spanning the frame's Y|U|V planes; an idle
+      //      slot gets an out-of-range offset and the hardware bounds check drops it, so the
+      //      section is branch-free and its LDS reads issue back to back.
+      {
+        const bool cl = l >= 16;  // chroma lane (slots C, E by plane)
+        const int pl = (l >> 3) & 1;
+        const uint32_t cpoff = pl ? voff : uoff;                    // slot C chroma plane
+        const uint8_t* cwin = fw + (pl ? kFwV : kFwU);
+        const int ep = l >> 4, er = (l >> 1) & 7, ed = l & 1;      // slot E
+        const uint32_t epoff = ep ? voff : uoff;
+        const uint8_t* ewin = fw + (ep ? kFwV : kFwU);
+        // slot B: lanes 0..11 luma rows -3..-1 of the MB above (cols 0..15),
+        //         lanes 12..23 chroma rows -3..-1 (cols 0..7), U then V
+        const int bk = l - 12, bp = bk >= 6, brem = bk - 6 * bp;
+        const int brr = l < 12 ? (l >> 2) - 3 : (brem >> 1) - 3;
+        const int bd = l < 12 ? (l & 3) : (brem & 1);
+        const uint8_t* bsrc = l < 12 ? fw + kFwY + (brr + 4) * FWY + 4 + 4 * bd
+                                     : fw + (bp ? kFwV : kFwU) + (brr + 4) * FWC + 4 + 4 * bd;
+        const uint32_t vA0 = ld32(fw + kFwY + (b0 + 4) * FWY + 4 * q);
+        const uint32_t vA1 = ld32(fw + kFwY + (b0 + 12) * FWY + 4 * q);
+        const uint32_t vB = ld32(bsrc);
+        const uint32_t vC = cl ? ld32(cwin + ((l & 7) + 4) * FWC + 8) : ld32(fw + kFwY + (l + 4) * FWY + 16);
+        const uint32_t vE = ld32(ewin + (er + 4) * FWC + 4 * ed);
+        const bool aok = act && (q > 0 || x > 0);
+        const uint32_t oA = (uint32_t)(16 * x - 4 + 4 * q);
+        const uint32_t oA0 = aok && b0 < nrows_y ? (uint32_t)__mul24(16 * y + b0, ys) + oA : kDrop;
+        const uint32_t oA1 = aok && b0 + 8 < nrows_y ? (uint32_t)__mul24(16 * y + b0 + 8, ys) + oA : kDrop;
+        const uint32_t oB = !(act && y > 0 && l < 24) ? kDrop
+                            : l < 12 ? (uint32_t)__mul24(16 * y + brr, ys) + 16 * x + 4 * bd
+                                     : (bp ? voff : uoff) + (uint32_t)__mul24(8 * y + brr, uvs) + 8 * x + 4 * bd;
+        const uint32_t oC = !(act && last_x) ? kDrop
+                            : cl ? ((l & 7) < nrows_c ? cpoff + (uint32_t)__mul24(8 * y + (l & 7), uvs) + 8 * x + 4 : kDrop)
+                                 : (l < nrows_y ? (uint32_t)__mul24(16 * y + l, ys) + 16 * x + 12 : kDrop);
+        const uint32_t oE = act && er < nrows_c && (ed > 0 || x > 0)
+                                ? epoff + (uint32_t)__mul24(8 * y + er, uvs) + 8 * x - 4 + 4 * ed
+                                : kDrop;
+        __builtin_amdgcn_raw_buffer_store_b32(vA0, planes, (int)oA0, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(vA1, planes, (int)oA1, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(vB, planes, (int)oB, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(vC, planes, (int)oC, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(vE, planes, (int)oE, 0, 0);
       }
       lds_sync();
 
