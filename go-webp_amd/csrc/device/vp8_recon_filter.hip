@@ -27,8 +27,8 @@
 // (tests/test_oracle.py::test_transform_shortcuts_exact).
 //
 // Loop filter (per MB, libwebp edge order): lanes 0..15 luma lines, 16..31 chroma
-// lines, one pass of FilterLoop26/24 / simple-filter math per edge step in a per-MB LDS
-// window (8 passes per MB).
+// lines of a per-MB LDS window; each lane runs all vertical edges on its row in
+// registers, then all horizontal edges on its column (two LDS round trips per MB).
 //
 // Memory.  Cross-MB state lives in LDS only: the unfiltered top samples `ytop`
 // (VP8TopSamples), the final bottom rows `fbot` of each MB column for the next row's
@@ -37,6 +37,7 @@
 // record x+2 and coefficients x+1 are in flight while MB x is processed.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../device_format.h"
 #include "kernels.h"
@@ -65,10 +66,41 @@ constexpr int kHdrBytes = kProgBytes + kTabBytes;
 constexpr int kColBytes = 32 + 128;  // ytop (y16 u8 v8) + fbot (Y 4x16, U 4x8, V 4x8)
 constexpr uint32_t kDrop = 0x80000000u;  // buffer offset beyond any frame: store dropped
 
+// Opt-in per-section cycle accounting (make VARIANT=timing -> libgowebp_amd_timing.so,
+// read back by scripts/k1_sections.py): s_memtime deltas summed per loop section in
+// SGPRs, added to a device array once per wave.  Compiled out of the product library.
+#ifdef WG_K1_SECTION_TIMING
+constexpr int kSections = 14;
+__device__ unsigned long long g_k1_sections[kSections];
+#define K1_SECT_DECL() uint64_t sect_acc[kSections] = {}, sect_t = 0
+#define K1_SECT_START() (sect_t = __builtin_amdgcn_s_memtime())
+#define K1_SECT(id)                                       \
+  do {                                                    \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime();     \
+    sect_acc[id] += t_ - sect_t;                          \
+    sect_t = t_;                                          \
+  } while (0)
+#define K1_SECT_FLUSH()                                                        \
+  do {                                                                         \
+    if (lane == 0)                                                             \
+      for (int s_ = 0; s_ < kSections; ++s_) atomicAdd(&g_k1_sections[s_], sect_acc[s_]); \
+  } while (0)
+#else
+#define K1_SECT_DECL() (void)0
+#define K1_SECT_START() (void)0
+#define K1_SECT(id) (void)0
+#define K1_SECT_FLUSH() (void)0
+#endif
+
 __device__ __forceinline__ void lds_sync() {
-  // LDS ops of one wave complete in order; this makes every lane's earlier LDS write
-  // visible to every lane's later LDS read and stops compiler reordering.
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  // Intra-wave LDS exchange.  A wave's DS instructions execute in order, so a later read
+  // sees an earlier write of any lane (and a later write cannot overtake an earlier read)
+  // with no s_waitcnt; only compiler reordering has to be stopped.  Wavefront-scope fences
+  // emit no instruction.  Cross-wave hand-off goes through the release/acquire progress
+  // counters instead.
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 __device__ __forceinline__ int clamp255(int v) { return min(max(v, 0), 255); }
@@ -225,39 +257,26 @@ __device__ __forceinline__ void filter_line(Line& l, int t2, int it, int hev_t) 
   }
 }
 
-// Across a vertical edge at window byte `row_at_e` (horizontal step): two dwords.
+// One edge on eight consecutive samples v[0..7] = p3..q3 held in registers.
 template <int KIND>
-__device__ __forceinline__ void filter_row(uint8_t* row_at_e, int t2, int it, int ht) {
-  const uint32_t lo = ld32(row_at_e - 4), hi = ld32(row_at_e);
-  Line l{byte_of(lo, 0), byte_of(lo, 1), byte_of(lo, 2), byte_of(lo, 3),
-         byte_of(hi, 0), byte_of(hi, 1), byte_of(hi, 2), byte_of(hi, 3)};
+__device__ __forceinline__ void filter_at(int* v, int t2, int it, int ht) {
+  Line l{v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]};
   filter_line<KIND>(l, t2, it, ht);
-  st32(row_at_e - 4, pack4(l.p3, l.p2, l.p1, l.p0));
-  st32(row_at_e, pack4(l.q0, l.q1, l.q2, l.q3));
-}
-// Across a horizontal edge (vertical step `s` = window stride): eight bytes.
-template <int KIND>
-__device__ __forceinline__ void filter_col(uint8_t* p, int s, int t2, int it, int ht) {
-  Line l{p[-4 * s], p[-3 * s], p[-2 * s], p[-s], p[0], p[s], p[2 * s], p[3 * s]};
-  filter_line<KIND>(l, t2, it, ht);
-  if (KIND == 1) {
-    p[-3 * s] = (uint8_t)l.p2;
-    p[2 * s] = (uint8_t)l.q2;
-  }
-  if (KIND != 0) {
-    p[-2 * s] = (uint8_t)l.p1;
-    p[s] = (uint8_t)l.q1;
-  }
-  p[-s] = (uint8_t)l.p0;
-  p[0] = (uint8_t)l.q0;
+  v[1] = l.p2;
+  v[2] = l.p1;
+  v[3] = l.p0;
+  v[4] = l.q0;
+  v[5] = l.q1;
+  v[6] = l.q2;
 }
 
-// The eight edge steps of DoFilter (frame_dec.c.go:204-251) for one MB per half-wave.
-// Lane l < 16 filters luma line l; lanes 16..31 chroma line l&7 of plane U (16..23) or
-// V (24..31), complex filter only.  Each lane addresses its own plane window (base and
-// stride), so a step that covers luma and chroma is ONE pass of the filter code.  Window
-// offsets coincide: MB edge at window column/row 4, the chroma inner edge and the first
-// luma inner edge at 8; luma inner edges 12 and 16 are luma-only steps.
+// DoFilter (frame_dec.c.go:204-251) for one MB per half-wave, libwebp edge order
+// (left MB edge, inner vertical edges, top MB edge, inner horizontal edges).
+// Lane l < 16 owns luma line l; lanes 16..31 chroma line l&7 of U (16..23) / V (24..31),
+// complex filter only.  Vertical edges: the lane loads its whole window row (luma cols
+// -4..15, chroma -4..7) and runs every vertical edge in registers; one LDS round trip
+// later it loads its window column and runs every horizontal edge the same way.  Two LDS
+// round trips per MB instead of one per edge step.
 template <bool kComplex>
 __device__ __forceinline__ void filter_mb(uint8_t* fw, int l, bool on, bool fx, bool fy, bool fin, int limit,
                                           int ilevel, int hev_t) {
@@ -268,24 +287,43 @@ __device__ __forceinline__ void filter_mb(uint8_t* fw, int l, bool on, bool fx, 
   const int li = luma ? l : (l & 7);
   const int st = luma ? FWY : FWC;
   uint8_t* win = fw + (luma ? kFwY : ((l >> 3) & 1 ? kFwV : kFwU));
-  uint8_t* row = win + (li + 4) * st;  // line li, for vertical edges
-  uint8_t* col = win + 4 + li;         // column li, for horizontal edges
-  const bool lx = lane_on && fx, lin = lane_on && fin, ly = lane_on && fy;
-  if (lx) filter_row<KMB>(row + 4, t_mb, ilevel, hev_t);  // HFilter16 / HFilter8 / SimpleHFilter16
+  int v[20];
+  if (lane_on) {  // vertical edges on window row li+4
+    uint32_t* row = reinterpret_cast<uint32_t*>(win + (li + 4) * st);
+    uint32_t w[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) w[k] = (k < 3 || luma) ? row[k] : 0u;
+#pragma unroll
+    for (int k = 0; k < 20; ++k) v[k] = byte_of(w[k >> 2], k & 3);
+    if (fx) filter_at<KMB>(v + 0, t_mb, ilevel, hev_t);  // HFilter16 / HFilter8 / SimpleHFilter16
+    if (fin) {
+      filter_at<KIN>(v + 4, t_in, ilevel, hev_t);  // HFilter16i / HFilter8i
+      if (luma) {
+        filter_at<KIN>(v + 8, t_in, ilevel, hev_t);
+        filter_at<KIN>(v + 12, t_in, ilevel, hev_t);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+      if (k < 3 || luma) row[k] = pack4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
+  }
   lds_sync();
-  if (lin) filter_row<KIN>(row + 8, t_in, ilevel, hev_t);  // HFilter16i (first) / HFilter8i
-  lds_sync();
-  if (lin && luma) filter_row<KIN>(row + 12, t_in, ilevel, hev_t);
-  lds_sync();
-  if (lin && luma) filter_row<KIN>(row + 16, t_in, ilevel, hev_t);
-  lds_sync();
-  if (ly) filter_col<KMB>(col + 4 * st, st, t_mb, ilevel, hev_t);  // VFilter16 / VFilter8
-  lds_sync();
-  if (lin) filter_col<KIN>(col + 8 * st, st, t_in, ilevel, hev_t);  // VFilter16i (first) / VFilter8i
-  lds_sync();
-  if (lin && luma) filter_col<KIN>(col + 12 * FWY, FWY, t_in, ilevel, hev_t);
-  lds_sync();
-  if (lin && luma) filter_col<KIN>(col + 16 * FWY, FWY, t_in, ilevel, hev_t);
+  if (lane_on) {  // horizontal edges on window column li+4
+    uint8_t* col = win + 4 + li;
+#pragma unroll
+    for (int k = 0; k < 20; ++k) v[k] = (k < 12 || luma) ? col[k * st] : 0;
+    if (fy) filter_at<KMB>(v + 0, t_mb, ilevel, hev_t);  // VFilter16 / VFilter8 / SimpleVFilter16
+    if (fin) {
+      filter_at<KIN>(v + 4, t_in, ilevel, hev_t);  // VFilter16i / VFilter8i
+      if (luma) {
+        filter_at<KIN>(v + 8, t_in, ilevel, hev_t);
+        filter_at<KIN>(v + 12, t_in, ilevel, hev_t);
+      }
+    }
+#pragma unroll
+    for (int k = 1; k < 19; ++k)
+      if (k < 11 || luma) col[k * st] = (uint8_t)v[k];
+  }
   lds_sync();
 }
 
@@ -314,7 +352,8 @@ __device__ __forceinline__ Coefs load_coefs(gptr<const uint32_t> blocks, uint32_
 
 }  // namespace
 
-__global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc* __restrict__ frames, int* err) {
+__global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc* __restrict__ frames, int* err,
+                                                                int lead_arg) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   // Progress counters as a typed __shared__ array + relaxed workgroup atomics, so the spin
   // is a ds_read (lgkmcnt) -- a volatile generic pointer became a flat load whose
@@ -336,6 +375,12 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
 
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
+  K1_SECT_DECL();
+  // Required lead of the previous row pair, in MB columns: 2 (top-right samples and the
+  // left-edge filter of MB (x+1, y-1) reach one MB up-right).  Larger leads were measured
+  // slower (c3: lead 2 9.7 ms, 8 10.2 ms, 16 11.6 ms): waves held back at start-up idle
+  // while the running ones gain nothing, so the pairs are packed as tightly as allowed.
+  const int lead = max(2, lead_arg);
   const int h = lane >> 5;  // half-wave: 0 = row 2k, 1 = row 2k+1
   const int l = lane & 31;
   uint32_t* tab = reinterpret_cast<uint32_t*>(lds + kProgBytes);
@@ -360,6 +405,7 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
     // loop header has no pending loads on cc/rc/rn and the in-loop uses of cc do not
     // conservatively drain the NEXT MB's prefetch with a vmcnt(0).
     __builtin_amdgcn_s_waitcnt(0x0F70);
+    K1_SECT_START();
 
     for (int i = 0; i < mb_w + 2; ++i) {
       // Lane roles, recomputed every iteration from an opaque lane id: hoisted out of the
@@ -383,18 +429,20 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
       const int x = i - 2 * h;
       const bool act = row_ok && x >= 0 && x < mb_w;
       const bool last_x = x == mb_w - 1;
+      K1_SECT(13);
       // ---- software pipeline: record x+2 and coefficients x+1 in flight during MB x
       const MbRec rnn = load_rec(mbs, mb_w, y, row_ok, x + 2);
       const uint32_t blk_next = blk + __builtin_popcount(rc.flags & kNzMask);
       const Coefs cn = load_coefs(blocks, rn.flags & kNzMask, blk_next, b0, cb, q);
 
+      K1_SECT(0);
       // ---- wait for the previous pair's odd row (t = x + 2y wavefront)
       if (k > 0 && i < mb_w) {
-        const uint32_t need = ((uint32_t)(k - 1) << 16) | (uint32_t)min(i + 2, mb_w);
+        const uint32_t need = ((uint32_t)(k - 1) << 16) | (uint32_t)min(i + lead, mb_w);
         uint32_t* pr = progress + ((k - 1) & (kWaves - 1));
-        if (__hip_atomic_load(pr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
+        if (__hip_atomic_load(pr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
           const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-          while (__hip_atomic_load(pr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
+          while (__hip_atomic_load(pr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
             __builtin_amdgcn_s_sleep(2);
             if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s: give up, flag
               if (lane == 0) atomicOr(err, 1);
@@ -407,6 +455,7 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
       const bool i4 = (fl >> kI4Shift) & 1;
       uint8_t* col = cols + x * kColBytes;
 
+      K1_SECT(1);
       // ---- ReconstructRow prologue at the row's first MB (frame_dec.c.go:79-98)
       if (act && x == 0) {
         if (l < 16) ws[Y_OFF + l * BPS - 1] = 129;
@@ -423,6 +472,7 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
         }
       }
       lds_sync();
+      K1_SECT(2);
       // ---- top samples (frame_dec.c.go:122-142)
       if (act && y > 0) {
         if (l < 4) st32(ws + Y_OFF - BPS + 4 * l, ld32(col + 4 * l));
@@ -434,12 +484,14 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
       lds_sync();
       if (act && i4 && l < 3) st32(ws + Y_OFF + (3 + 4 * l) * BPS + 16, ld32(ws + Y_OFF - BPS + 16));
 
+      K1_SECT(3);
       // ---- residuals of all blocks (prediction-independent)
       int ry0[4], ry1[4], rcr[4];
       idct_pass(q, cc.y0, ry0);
       idct_pass(q, cc.y1, ry1);
       idct_pass(q, cc.c, rcr);
 
+      K1_SECT(4);
       // ---- luma prediction + residual
       const int row_a = 4 * lby + q, row_b = row_a + 8;
       uint8_t* dst_a = ws + Y_OFF + row_a * BPS + 4 * lbx;
@@ -470,6 +522,7 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
             make_uint2((ry1[0] & 0xffff) | (ry1[1] << 16), (ry1[2] & 0xffff) | (ry1[3] << 16));
       }
       lds_sync();
+      K1_SECT(5);
       if (__any(act && i4)) {
         const uint32_t im_lo = rc.imodes_lo, im_hi = rc.imodes_hi;
         for (int t = 0; t < 10; ++t) {
@@ -500,6 +553,7 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
         }
       }
 
+      K1_SECT(6);
       // ---- chroma prediction + residual (lane = one pixel row of one 4x4 chroma block)
       if (act) {
         const int mode = check_mode(x, y, (fl >> kUVModeShift) & 3);
@@ -520,6 +574,7 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
       }
       lds_sync();
 
+      K1_SECT(7);
       if (act) {
         // ---- stash unfiltered bottom samples for the row below (frame_dec.c.go:175-179)
         if (!last_row) {
@@ -545,6 +600,7 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
       }
       lds_sync();
 
+      K1_SECT(8);
       // ---- loop filter on the window
       {
         const uint32_t fi = rc.finfo;
@@ -557,6 +613,7 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
         }
       }
 
+      K1_SECT(9);
       if (act) {
         // ---- deposit final bottom rows of this MB column (and the left neighbour's
         //      cols 12..15 / 4..7, final now) for the row below's top-edge filter
@@ -583,6 +640,7 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
           }
         }
       }
+      K1_SECT(10);
       // ---- final pixels to HBM (each byte written once).  Five dword slots per lane, all
       //      buffer stores against one descriptor spanning the frame's Y|U|V planes; an idle
       //      slot gets an out-of-range offset and the hardware bounds check drops it, so the
@@ -628,6 +686,7 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
       }
       lds_sync();
 
+      K1_SECT(11);
       // ---- rotate for the next MB (frame_dec.c.go:106-114) + the filter window
       if (act) {
 #pragma unroll
@@ -656,15 +715,29 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
       }
       lds_sync();
       if (lane == 32 && has_odd && x >= 0)
-        __hip_atomic_store(progress + (k & (kWaves - 1)), ((uint32_t)k << 16) | (uint32_t)(x + 1), __ATOMIC_RELAXED,
+        __hip_atomic_store(progress + (k & (kWaves - 1)), ((uint32_t)k << 16) | (uint32_t)(x + 1), __ATOMIC_RELEASE,
                            __HIP_MEMORY_SCOPE_WORKGROUP);
+      K1_SECT(12);
       rc = rn;
       rn = rnn;
       cc = cn;
       blk = blk_next;
     }
   }
+  K1_SECT_FLUSH();
 }
+
+#ifdef WG_K1_SECTION_TIMING
+extern "C" int wg_debug_k1_sections(unsigned long long* out, int n, int reset) {
+  if (n > kSections) n = kSections;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_k1_sections), n * sizeof(unsigned long long)) != hipSuccess) return -1;
+  if (reset) {
+    unsigned long long z[kSections] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_k1_sections), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return n;
+}
+#endif
 
 size_t vp8_recon_lds_bytes(int mb_w) {
   return (size_t)kHdrBytes + (size_t)2 * kWaves * kSlotBytes + (size_t)mb_w * kColBytes;
@@ -674,6 +747,11 @@ int vp8_recon_max_mb_w() { return (int)((163840 - kHdrBytes - 2 * kWaves * kSlot
 
 hipError_t launch_vp8_recon_filter(const FrameDesc* d_frames, int n_frames, int max_mb_w, int* d_err,
                                    hipStream_t stream) {
+  // WG_K1_LEAD overrides the inter-pair lead (tuning experiments only).
+  static const int lead = [] {
+    const char* e = getenv("WG_K1_LEAD");
+    return e ? atoi(e) : 0;
+  }();
   const size_t lds = vp8_recon_lds_bytes(max_mb_w);
   static size_t configured = 0;
   if (lds > 65536 && lds > configured) {
@@ -682,7 +760,7 @@ hipError_t launch_vp8_recon_filter(const FrameDesc* d_frames, int n_frames, int 
     if (e != hipSuccess) return e;
     configured = lds;
   }
-  hipLaunchKernelGGL(vp8_recon_filter_kernel, dim3(n_frames), dim3(1024), lds, stream, d_frames, d_err);
+  hipLaunchKernelGGL(vp8_recon_filter_kernel, dim3(n_frames), dim3(1024), lds, stream, d_frames, d_err, lead);
   return hipGetLastError();
 }
 

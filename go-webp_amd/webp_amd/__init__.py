@@ -23,7 +23,9 @@ __all__ = [
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libgowebp_amd.so")
+# WG_LIB_VARIANT=timing selects the K1 section-timing build (scripts/k1_sections.py).
+LIB_PATH = os.path.join(_HERE, "libgowebp_amd%s.so" % (
+    "_" + os.environ["WG_LIB_VARIANT"] if os.environ.get("WG_LIB_VARIANT") else ""))
 
 FLAG_BYPASS_FILTERING = 1
 FLAG_NO_FANCY_UPSAMPLING = 2
