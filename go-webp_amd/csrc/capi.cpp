@@ -246,6 +246,7 @@ wg_batch* wg_batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t*
     d.mbs = reinterpret_cast<const MbRec*>(b->d_in + f.off_recs);
     d.row_block0 = reinterpret_cast<const uint32_t*>(b->d_in + f.off_rows);
     d.blocks = reinterpret_cast<const int16_t*>(b->d_in + f.off_blocks);
+    d.blocks_bytes = (int32_t)(f.sf.blocks.size() * 2);
     d.y = b->d_planes + f.off_y;
     d.u = b->d_planes + f.off_u;
     d.v = b->d_planes + f.off_v;

@@ -187,14 +187,28 @@ __device__ __forceinline__ int check_mode(int mb_x, int mb_y, int mode) {  // fr
 }
 
 // One pixel row of the 16x16 luma / 8x8 chroma predictors (DC*, TM, VE, HE;
-// dec.c.go:178-249, 422-474); `dc` is the DC value computed by the caller.
-__device__ __forceinline__ uint32_t pred_row(int mode, uint32_t top, int left, int tl, int dc) {
-  if (mode == 2) return top;                                 // VE
-  if (mode == 3) return (uint32_t)left * 0x01010101u;        // HE
-  if (mode == 1)                                             // TM
-    return pack4(clamp255(byte_of(top, 0) + left - tl), clamp255(byte_of(top, 1) + left - tl),
-                 clamp255(byte_of(top, 2) + left - tl), clamp255(byte_of(top, 3) + left - tl));
-  return (uint32_t)dc * 0x01010101u;                         // DC variants
+// dec.c.go:178-249, 422-474) selected by bits of a one-hot mode mask (oh = 1 << mode): a
+// chain of `mode == k` tests becomes a switch lowered to a branch tree, bit tests stay
+// v_cndmask.  TrueMotion is only computed when some lane of the wave needs it.
+__device__ __forceinline__ uint32_t pred_row(uint32_t oh, uint32_t top, int left, int tl, int dc) {
+  uint32_t tm = 0;
+  if (__any(oh & 0x2))
+    tm = pack4(clamp255(byte_of(top, 0) + left - tl), clamp255(byte_of(top, 1) + left - tl),
+               clamp255(byte_of(top, 2) + left - tl), clamp255(byte_of(top, 3) + left - tl));
+  const uint32_t v = (oh & 0x4) ? top : (uint32_t)dc * 0x01010101u;  // VE : DC variants
+  const uint32_t w = (oh & 0x8) ? (uint32_t)left * 0x01010101u : tm;  // HE : TM
+  return (oh & 0xA) ? w : v;
+}
+
+// DC value by one-hot mode: DC (0) both edges, DC_NOTOP (4) left only, DC_NOLEFT (5) top
+// only, DC_NOTOPLEFT (6) 0x80.  `shift` = log2(edge length).
+__device__ __forceinline__ int dc_value(uint32_t oh, uint32_t st, uint32_t sl, int shift) {
+  const int both = (int)(st + sl + (1u << shift)) >> (shift + 1);
+  const int lonly = (int)(sl + (1u << (shift - 1))) >> shift;
+  const int tonly = (int)(st + (1u << (shift - 1))) >> shift;
+  const int a = (oh & 0x10) ? lonly : tonly;
+  const int b = (oh & 0x1) ? both : 0x80;
+  return (oh & 0x30) ? a : b;
 }
 
 // ---------------------------------------------------------------- loop filter
@@ -231,9 +245,9 @@ __device__ __forceinline__ void filter_line(Line& l, int t2, int it, int hev_t) 
   const int dp = absd(l.p1, l.p0), dq = absd(l.q1, l.q0);
   const int in_p = max(max(absd(l.p3, l.p2), absd(l.p2, l.p1)), dp);
   const int in_q = max(max(absd(l.q3, l.q2), absd(l.q2, l.q1)), dq);
-  const bool on = edge_ok && max(in_p, in_q) <= it;
+  const bool on = edge_ok & (max(in_p, in_q) <= it);  // & not &&: no short-circuit branch
   const bool hv = max(dp, dq) > hev_t;
-  const bool f2 = on && hv, fx = on && !hv;
+  const bool f2 = on & hv, fx = on & !hv;
   if (KIND == 1) {  // DoFilter6
     const int w = sclip1(a);
     const int a1 = (27 * w + 63) >> 7, a2 = (18 * w + 63) >> 7, a3 = (9 * w + 63) >> 7;
@@ -245,15 +259,16 @@ __device__ __forceinline__ void filter_line(Line& l, int t2, int it, int hev_t) 
     l.q2 = fx ? nq2 : l.q2;
     l.p0 = fx ? np0 : (f2 ? f2p0 : l.p0);
     l.q0 = fx ? nq0 : (f2 ? f2q0 : l.q0);
-  } else {  // DoFilter4
-    const int a4 = 3 * d0;
-    const int a1 = sclip2((a4 + 4) >> 3), a2 = sclip2((a4 + 3) >> 3), a3 = (a1 + 1) >> 1;
-    const int np1 = clamp255(l.p1 + a3), np0 = clamp255(l.p0 + a2);
-    const int nq0 = clamp255(l.q0 - a1), nq1 = clamp255(l.q1 - a3);
+  } else {  // DoFilter4, or DoFilter2 on hev lines: both are p0 += sclip2((a+3)>>3),
+            // q0 -= sclip2((a+4)>>3) with a = 3*(q0-p0) [+ sclip1(p1-q1) when hev]
+    const int a = 3 * d0 + (hv ? sp : 0);
+    const int a1 = sclip2((a + 4) >> 3), a2 = sclip2((a + 3) >> 3), a3 = (a1 + 1) >> 1;
+    const int np0 = clamp255(l.p0 + a2), nq0 = clamp255(l.q0 - a1);
+    const int np1 = clamp255(l.p1 + a3), nq1 = clamp255(l.q1 - a3);
     l.p1 = fx ? np1 : l.p1;
     l.q1 = fx ? nq1 : l.q1;
-    l.p0 = fx ? np0 : (f2 ? f2p0 : l.p0);
-    l.q0 = fx ? nq0 : (f2 ? f2q0 : l.q0);
+    l.p0 = on ? np0 : l.p0;
+    l.q0 = on ? nq0 : l.q0;
   }
 }
 
@@ -327,26 +342,32 @@ __device__ __forceinline__ void filter_mb(uint8_t* fw, int l, bool on, bool fx, 
   lds_sync();
 }
 
-__device__ __forceinline__ MbRec load_rec(gptr<const uint32_t> mbs, int mb_w, int y, bool row_ok, int x) {
-  if (row_ok && x >= 0 && x < mb_w) {
-    const gptr<const uint32_t> p = mbs + 4 * ((size_t)y * mb_w + x);
-    return MbRec{p[0], p[1], p[2], p[3]};
-  }
-  return MbRec{0, 0, 0, 0};
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// MB record of (x, y); out-of-frame positions read as all-zero through the buffer range
+// check (no branch, 32-bit offsets instead of 64-bit address arithmetic).
+__device__ __forceinline__ MbRec load_rec(__amdgpu_buffer_rsrc_t recs, int mb_w, int y, bool row_ok, int x) {
+  const bool ok = row_ok && x >= 0 && x < mb_w;
+  const u32x4 r = __builtin_amdgcn_raw_buffer_load_b128(recs, ok ? (y * mb_w + x) * 16 : (int)kDrop, 0, 0);
+  return MbRec{r.x, r.y, r.z, r.w};
 }
 
 struct Coefs { uint2 y0, y1, c; };
 
-__device__ __forceinline__ uint2 ld_blockcol(gptr<const uint32_t> blocks, uint32_t bi, int q) {
-  const gptr<const uint32_t> p = blocks + (size_t)bi * 8 + 2 * q;  // 16 int16 = 8 dwords per block
-  return make_uint2(p[0], p[1]);
+// Column q of non-zero block `bi` (16 int16 = 32 B per block, column-major); a zero block
+// reads as zeros through the range check.
+__device__ __forceinline__ uint2 ld_blockcol(__amdgpu_buffer_rsrc_t blks, bool nz, uint32_t bi, int q) {
+  const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(blks, nz ? (int)(bi * 32 + 8 * q) : (int)kDrop, 0, 0);
+  return make_uint2(v.x, v.y);
 }
 
-__device__ __forceinline__ Coefs load_coefs(gptr<const uint32_t> blocks, uint32_t nz, uint32_t blk, int b0, int cb, int q) {
-  Coefs c{{0, 0}, {0, 0}, {0, 0}};
-  if ((nz >> b0) & 1) c.y0 = ld_blockcol(blocks, blk + __builtin_popcount(nz & ((1u << b0) - 1)), q);
-  if ((nz >> (b0 + 8)) & 1) c.y1 = ld_blockcol(blocks, blk + __builtin_popcount(nz & ((1u << (b0 + 8)) - 1)), q);
-  if ((nz >> cb) & 1) c.c = ld_blockcol(blocks, blk + __builtin_popcount(nz & ((1u << cb) - 1)), q);
+__device__ __forceinline__ Coefs load_coefs(__amdgpu_buffer_rsrc_t blks, uint32_t nz, uint32_t blk, int b0, int cb,
+                                            int q) {
+  Coefs c;
+  c.y0 = ld_blockcol(blks, (nz >> b0) & 1, blk + __builtin_popcount(nz & ((1u << b0) - 1)), q);
+  c.y1 = ld_blockcol(blks, (nz >> (b0 + 8)) & 1, blk + __builtin_popcount(nz & ((1u << (b0 + 8)) - 1)), q);
+  c.c = ld_blockcol(blks, (nz >> cb) & 1, blk + __builtin_popcount(nz & ((1u << cb) - 1)), q);
   return c;
 }
 
@@ -364,9 +385,12 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
   const int mb_w = F->mb_w, mb_h = F->mb_h;
   const int ftype = F->filter_type;
   const int ys = F->y_stride, uvs = F->uv_stride;
-  const gptr<const uint32_t> mbs = as_global(reinterpret_cast<const uint32_t*>(F->mbs));
   const gptr<const uint32_t> row_block0 = as_global(F->row_block0);
-  const gptr<const uint32_t> blocks = as_global(reinterpret_cast<const uint32_t*>(F->blocks));
+  // Buffer descriptors: out-of-range loads return 0 and out-of-range stores are dropped.
+  const __amdgpu_buffer_rsrc_t recs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<MbRec*>(F->mbs), 0, mb_w * mb_h * 16, 0x00020000);
+  const __amdgpu_buffer_rsrc_t blks =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<int16_t*>(F->blocks), 0, F->blocks_bytes, 0x00020000);
   // One buffer descriptor over the frame's planes: the batch allocates Y, U, V of a frame
   // back to back (capi.cpp), so U and V are 32-bit offsets from Y.
   const uint32_t uoff = (uint32_t)(F->u - F->y), voff = (uint32_t)(F->v - F->y);
@@ -398,9 +422,9 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
     const int nrows_y = last_row ? 16 : 13;  // luma rows of this MB row final after its pass
     const int nrows_c = last_row ? 8 : 5;
     uint32_t blk = row_ok ? row_block0[y] : 0u;
-    MbRec rc = load_rec(mbs, mb_w, y, row_ok, -2 * h);
-    MbRec rn = load_rec(mbs, mb_w, y, row_ok, -2 * h + 1);
-    Coefs cc = load_coefs(blocks, rc.flags & kNzMask, blk, (l >> 2), 16 + (l >> 2), l & 3);
+    MbRec rc = load_rec(recs, mb_w, y, row_ok, -2 * h);
+    MbRec rn = load_rec(recs, mb_w, y, row_ok, -2 * h + 1);
+    Coefs cc = load_coefs(blks, rc.flags & kNzMask, blk, (l >> 2), 16 + (l >> 2), l & 3);
     // Retire the prologue loads here (visible to the waitcnt pass: 0x0F70 = vmcnt(0)), so the
     // loop header has no pending loads on cc/rc/rn and the in-loop uses of cc do not
     // conservatively drain the NEXT MB's prefetch with a vmcnt(0).
@@ -431,9 +455,9 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
       const bool last_x = x == mb_w - 1;
       K1_SECT(13);
       // ---- software pipeline: record x+2 and coefficients x+1 in flight during MB x
-      const MbRec rnn = load_rec(mbs, mb_w, y, row_ok, x + 2);
+      const MbRec rnn = load_rec(recs, mb_w, y, row_ok, x + 2);
       const uint32_t blk_next = blk + __builtin_popcount(rc.flags & kNzMask);
-      const Coefs cn = load_coefs(blocks, rn.flags & kNzMask, blk_next, b0, cb, q);
+      const Coefs cn = load_coefs(blks, rn.flags & kNzMask, blk_next, b0, cb, q);
 
       K1_SECT(0);
       // ---- wait for the previous pair's odd row (t = x + 2y wavefront)
@@ -497,21 +521,20 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
       uint8_t* dst_a = ws + Y_OFF + row_a * BPS + 4 * lbx;
       uint8_t* dst_b = ws + Y_OFF + row_b * BPS + 4 * lbx;
       if (act && !i4) {
-        const int mode = check_mode(x, y, (fl >> kYModeShift) & 3);
+        const uint32_t oh = 1u << check_mode(x, y, (fl >> kYModeShift) & 3);
         const uint32_t top = ld32(ws + Y_OFF - BPS + 4 * lbx);
         const int tl = ws[Y_OFF - BPS - 1];
-        int dc = 0x80;
-        if (mode == 0 || mode == 4 || mode == 5) {
-          uint32_t st = 0, sl = 0;
+        uint32_t st = 0, sl = 0;
+        if (__any(oh & 0x31)) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             st = __builtin_amdgcn_sad_u8(ld32(ws + Y_OFF - BPS + 4 * j), 0, st);
             sl = __builtin_amdgcn_sad_u8(ld32(left + 4 * j), 0, sl);
           }
-          dc = mode == 0 ? (int)(st + sl + 16) >> 5 : mode == 4 ? (int)(sl + 8) >> 4 : (int)(st + 8) >> 4;
         }
-        const uint32_t pa = pred_row(mode, top, left[row_a], tl, dc);
-        const uint32_t pb = pred_row(mode, top, left[row_b], tl, dc);
+        const int dc = dc_value(oh, st, sl, 4);
+        const uint32_t pa = pred_row(oh, top, left[row_a], tl, dc);
+        const uint32_t pb = pred_row(oh, top, left[row_b], tl, dc);
         st32(dst_a, add_res(pa, ry0));
         st32(dst_b, add_res(pb, ry1));
       }
@@ -556,20 +579,18 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
       K1_SECT(6);
       // ---- chroma prediction + residual (lane = one pixel row of one 4x4 chroma block)
       if (act) {
-        const int mode = check_mode(x, y, (fl >> kUVModeShift) & 3);
+        const uint32_t oh = 1u << check_mode(x, y, (fl >> kUVModeShift) & 3);
         const uint8_t* base = ws + coff;
+        const uint8_t* cleft = left + 16 + 8 * cpl;
         const int row = 4 * cby + q;
-        const uint32_t top = ld32(base - BPS + 4 * cbx);
-        const int tl = base[-BPS - 1];
-        int dc = 0x80;
-        if (mode == 0 || mode == 4 || mode == 5) {
-          uint32_t st = __builtin_amdgcn_sad_u8(ld32(base - BPS), 0, 0);
+        uint32_t st = 0, sl = 0;
+        if (__any(oh & 0x31)) {
+          st = __builtin_amdgcn_sad_u8(ld32(base - BPS), 0, 0);
           st = __builtin_amdgcn_sad_u8(ld32(base - BPS + 4), 0, st);
-          uint32_t sl = __builtin_amdgcn_sad_u8(ld32(left + 16 + 8 * cpl), 0, 0);
-          sl = __builtin_amdgcn_sad_u8(ld32(left + 16 + 8 * cpl + 4), 0, sl);
-          dc = mode == 0 ? (int)(st + sl + 8) >> 4 : mode == 4 ? (int)(sl + 4) >> 3 : (int)(st + 4) >> 3;
+          sl = __builtin_amdgcn_sad_u8(ld32(cleft), 0, 0);
+          sl = __builtin_amdgcn_sad_u8(ld32(cleft + 4), 0, sl);
         }
-        const uint32_t pred = pred_row(mode, top, left[16 + 8 * cpl + row], tl, dc);
+        const uint32_t pred = pred_row(oh, ld32(base - BPS + 4 * cbx), cleft[row], base[-BPS - 1], dc_value(oh, st, sl, 3));
         st32(ws + coff + row * BPS + 4 * cbx, add_res(pred, rcr));
       }
       lds_sync();

@@ -54,7 +54,7 @@ struct FrameDesc {
   uint64_t pad0;
   int32_t width, height, mb_w, mb_h;
   int32_t y_stride, uv_stride, rgba_stride, filter_type;
-  int32_t flags, valid, pad1, pad2;
+  int32_t flags, valid, blocks_bytes, pad2;  // blocks_bytes: size of `blocks` (K1 bounds)
   int32_t pad3[4];
 };
 static_assert(sizeof(FrameDesc) == 128, "FrameDesc must be 128 bytes");
