@@ -429,6 +429,7 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
     // loop header has no pending loads on cc/rc/rn and the in-loop uses of cc do not
     // conservatively drain the NEXT MB's prefetch with a vmcnt(0).
     __builtin_amdgcn_s_waitcnt(0x0F70);
+    uint32_t top_carry = 0;  // see "top samples"
     K1_SECT_START();
 
     for (int i = 0; i < mb_w + 2; ++i) {
@@ -497,13 +498,19 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
       }
       lds_sync();
       K1_SECT(2);
-      // ---- top samples (frame_dec.c.go:122-142)
+      // ---- top samples (frame_dec.c.go:122-142).  The top-left sample (row -1, col -1) is
+      //      the previous column's top byte 15 (chroma: 7), which the current row has already
+      //      overwritten in `cols`: lanes 3, 5, 7 carry it over from their previous load.
       if (act && y > 0) {
-        if (l < 4) st32(ws + Y_OFF - BPS + 4 * l, ld32(col + 4 * l));
-        else if (l < 6) st32(ws + U_OFF - BPS + 4 * (l - 4), ld32(col + 16 + 4 * (l - 4)));
-        else if (l < 8) st32(ws + V_OFF - BPS + 4 * (l - 6), ld32(col + 24 + 4 * (l - 6)));
-        else if (l == 8 && i4)
+        if (l < 8) {
+          const uint32_t tv = ld32(col + 4 * l);
+          st32(ws + (l < 4 ? Y_OFF - BPS + 4 * l : l < 6 ? U_OFF - BPS + 4 * (l - 4) : V_OFF - BPS + 4 * (l - 6)), tv);
+          if (x > 0 && (l == 3 || l == 5 || l == 7))
+            ws[(l == 3 ? Y_OFF : l == 5 ? U_OFF : V_OFF) - BPS - 1] = (uint8_t)(top_carry >> 24);
+          top_carry = tv;
+        } else if (l == 8 && i4) {
           st32(ws + Y_OFF - BPS + 16, last_x ? (uint32_t)col[15] * 0x01010101u : ld32(col + kColBytes));
+        }
       }
       lds_sync();
       if (act && i4 && l < 3) st32(ws + Y_OFF + (3 + 4 * l) * BPS + 16, ld32(ws + Y_OFF - BPS + 16));
@@ -547,19 +554,30 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
       lds_sync();
       K1_SECT(5);
       if (__any(act && i4)) {
+        // recipe words and residuals of all ten steps fetched up front (independent loads)
         const uint32_t im_lo = rc.imodes_lo, im_hi = rc.imodes_hi;
+        uint32_t e[10];
+        int rs[10];
+#pragma unroll
+        for (int t = 0; t < 10; ++t) {
+          const int by = min(max(0, (t - 2) >> 1) + ps, 3);
+          const int bx = min(max(t - 2 * by, 0), 3);
+          const int bi = by * 4 + bx;
+          const int mode = (bi < 8 ? im_lo >> (4 * bi) : im_hi >> (4 * (bi - 8))) & 0xf;
+          e[t] = tab[mode * 16 + pp];
+          rs[t] = res[bi * 16 + pp];
+        }
+#pragma unroll
         for (int t = 0; t < 10; ++t) {
           const int by = max(0, (t - 2) >> 1) + ps;
           const int bx = t - 2 * by;
           if (act && i4 && by <= min(3, t >> 1) && bx >= 0) {
-            const int bi = by * 4 + bx;
-            const int mode = (bi < 8 ? im_lo >> (4 * bi) : im_hi >> (4 * (bi - 8))) & 0xf;
-            const uint32_t e = tab[mode * 16 + pp];
             uint8_t* org = ws + Y_OFF + 4 * by * BPS + 4 * bx;
-            const int kind = e >> 24;
-            const int a = org[(int8_t)(e & 0xff)];
-            const int b = org[(int8_t)((e >> 8) & 0xff)];
-            const int c = org[(int8_t)((e >> 16) & 0xff)];
+            const uint32_t ew = e[t];
+            const int kind = ew >> 24;
+            const int a = org[(int8_t)(ew & 0xff)];
+            const int b = org[(int8_t)((ew >> 8) & 0xff)];
+            const int c = org[(int8_t)((ew >> 16) & 0xff)];
             int v;
             if (kind == 3) {  // DC4
               const uint32_t s = __builtin_amdgcn_sad_u8(ld32(org - BPS), 0, 0);
@@ -568,9 +586,9 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
               const int avg3 = (a + 2 * b + c + 2) >> 2;
               const int avg2 = (a + b + 1) >> 1;
               const int tm = clamp255(a + b - c);
-              v = kind == 0 ? avg3 : kind == 1 ? avg2 : tm;
+              v = (kind & 2) ? tm : (kind & 1) ? avg2 : avg3;
             }
-            org[ppy * BPS + ppx] = (uint8_t)clamp255(v + res[bi * 16 + pp]);
+            org[ppy * BPS + ppx] = (uint8_t)clamp255(v + rs[t]);
           }
           lds_sync();
         }
@@ -708,30 +726,22 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
       lds_sync();
 
       K1_SECT(11);
-      // ---- rotate for the next MB (frame_dec.c.go:106-114) + the filter window
+      // ---- rotate for the next MB (frame_dec.c.go:106-114) + the filter window: cols 12..15
+      //      (chroma 4..7) become cols -4..-1 for rows 0..15 (0..7); row -1 is not needed
+      //      (its col -1 comes from the top-left carry).  Pass 0: workspace + left[],
+      //      pass 1: filter window; lanes 0..15 luma rows, 16..31 chroma rows.
       if (act) {
-#pragma unroll
-        for (int rep = 0; rep < 3; ++rep) {
-          const int task = l + 32 * rep;
-          if (task < 17) {  // Y rows -1..15: cols 12..15 -> -4..-1
-            const int r = task - 1;
-            const uint32_t v = ld32(ws + Y_OFF + r * BPS + 12);
-            st32(ws + Y_OFF + r * BPS - 4, v);
-            if (r >= 0) left[r] = (uint8_t)(v >> 24);
-          } else if (task < 35) {  // U/V rows -1..7: cols 4..7 -> -4..-1
-            const int kk = task - 17, p = kk >= 9, r = kk - 9 * p - 1;
-            const int off = p ? V_OFF : U_OFF;
-            const uint32_t v = ld32(ws + off + r * BPS + 4);
-            st32(ws + off + r * BPS - 4, v);
-            if (r >= 0) left[16 + 8 * p + r] = (uint8_t)(v >> 24);
-          } else if (task < 51) {  // window luma rows 0..15
-            const int r = task - 35;
-            st32(fw + kFwY + (r + 4) * FWY, ld32(fw + kFwY + (r + 4) * FWY + 16));
-          } else if (task < 67) {  // window chroma rows 0..7
-            const int kk = task - 51, p = kk >> 3, r = kk & 7;
-            uint8_t* cw = fw + (p ? kFwV : kFwU);
-            st32(cw + (r + 4) * FWC, ld32(cw + (r + 4) * FWC + 8));
-          }
+        const bool ly = l < 16;
+        const int cp = (l >> 3) & 1, cr = l & 7;
+        {
+          uint8_t* src = ly ? ws + Y_OFF + l * BPS + 12 : ws + (cp ? V_OFF : U_OFF) + cr * BPS + 4;
+          const uint32_t v = ld32(src);
+          st32(src - (ly ? 16 : 8), v);
+          left[l] = (uint8_t)(v >> 24);
+        }
+        {
+          uint8_t* src = ly ? fw + kFwY + (l + 4) * FWY + 16 : fw + (cp ? kFwV : kFwU) + (cr + 4) * FWC + 8;
+          st32(src - (ly ? 16 : 8), ld32(src));
         }
       }
       lds_sync();
