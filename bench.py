@@ -19,6 +19,8 @@ import os
 import sys
 import time
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "go-webp_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -52,6 +54,26 @@ def _traffic(workload):
         return None
 
 
+def shard_frames(datas, rank, batch):
+    """Frames of one rank: `batch` frames cycling the distinct bitstreams, offset by rank
+    (independent frames, no exchange between ranks -- SURVEY §8(e))."""
+    return [datas[(rank + i) % len(datas)] for i in range(batch)]
+
+
+def reduce_job(dist, device, dt, pixels):
+    """Whole-job figures over all ranks: (max elapsed seconds, total pixels).  `dist` None =
+    single process; otherwise any initialised torch.distributed backend (nccl on the GPU
+    box, gloo in tests/test_multi_rank.py)."""
+    if dist is None:
+        return dt, pixels
+    import torch
+    t = torch.tensor([dt], dtype=torch.float64, device=device)
+    p = torch.tensor([float(pixels)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dist.all_reduce(p, op=dist.ReduceOp.SUM)
+    return float(t.item()), int(p.item())
+
+
 def cpu_baseline(datas, seconds):
     """CPU oracle (C restatement, 1 thread): host entropy stage + reconstruct + filter +
     fancy RGBA, frames decoded serially until `seconds` elapse."""
@@ -72,6 +94,39 @@ def cpu_baseline(datas, seconds):
                        f"(host entropy stage + oracle/vp8_dsp_oracle.c recon+filter+fancy RGBA), {el:.1f}s")
 
 
+def cpu_baseline_parallel(datas, seconds, threads):
+    """The same CPU path on `threads` host threads, frames decoded concurrently (ctypes
+    releases the GIL inside the entropy stage and the oracle)."""
+    import threading
+    import webp_amd
+    from oracle_lib import oracle, oracle_decode
+    oracle()
+    webp_amd.lib()
+    pix = [0] * threads
+    cnt = [0] * threads
+    t0 = time.perf_counter()
+    stop = t0 + seconds
+
+    def work(t):
+        n = t
+        while time.perf_counter() < stop:
+            info, mbs = webp_amd.vp8_parse(datas[n % len(datas)])
+            oracle_decode(info, mbs)
+            pix[t] += info.width * info.height
+            cnt[t] += 1
+            n += threads
+
+    ths = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    el = time.perf_counter() - t0
+    return dict(value=sum(pix) / el / 1e6, unit="MPix/s", cores=threads, kind="port",
+                sample=f"{sum(cnt)} frames of the same workload on {threads} host threads "
+                       f"(entropy stage + oracle/vp8_dsp_oracle.c), {el:.1f}s")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -81,6 +136,7 @@ def main():
     ap.add_argument("--batch", type=int, default=256, help="frames per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (host in, host out) leg")
     ap.add_argument("--host-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
     args = ap.parse_args()
 
@@ -102,8 +158,9 @@ def main():
 
     wl = WORKLOADS[args.workload]
     datas, bpp = _load_frames(wl["prefix"])
-    frames = [datas[(rank + i) % len(datas)] for i in range(args.batch)]
-    ctx = webp_amd.Context(local, host_threads=max(1, min(args.host_threads, 64)))
+    frames = shard_frames(datas, rank, args.batch)
+    ctx_threads = max(1, min(args.host_threads, 64))
+    ctx = webp_amd.Context(local, host_threads=ctx_threads)
     t_prep = time.perf_counter()
     b = ctx.batch(frames)
     t_prep = time.perf_counter() - t_prep
@@ -124,14 +181,10 @@ def main():
     torch.cuda.synchronize()
     barrier()
     dt = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
     ms_k1, ms_k2 = b.kernel_ms()  # per-launch averages over the timed steps (HIP events)
     by_k1, by_k2 = b.kernel_bytes()
     px_rank = b.pixels
-    total_px = px_rank * world * args.steps
+    dt, total_px = reduce_job(dist, "cuda", dt, px_rank * args.steps)
     value = total_px / dt / 1e6
 
     if rank == 0:
@@ -140,7 +193,7 @@ def main():
             tr = _traffic(wl["name"])
             return {"kernel": kernel, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-                    "traffic": (tr or {}).get(kernel), "algorithmic_bytes": int(bytes_),
+                    "traffic": ((tr or {}).get(kernel) or {}).get("bytes"), "algorithmic_bytes": int(bytes_),
                     "avg_launch_ms": round(ms, 4)}
         r1 = roof(by_k1, ms_k1, "vp8_recon_filter_kernel")
         r2 = roof(by_k2, ms_k2, "yuv_to_rgba_kernel")
@@ -167,10 +220,27 @@ def main():
             "kernel_ms": {"vp8_recon_filter_kernel": round(ms_k1, 4), "yuv_to_rgba_kernel": round(ms_k2, 4)},
             "host_prepare_s": round(t_prep, 3),
         }
+        if not args.no_e2e:
+            # secondary figure: host bitstreams in, host RGBA out (entropy stage on host threads
+            # + H2D + K1 + K2 + D2H into pageable numpy buffers allocated outside the timing)
+            outs = [np.empty((b.dims(i)[1], b.dims(i)[0], 4), np.uint8) for i in range(b.n)]
+            ctx.decode_batch(frames[:2], out=outs[:2])
+            t_e = time.perf_counter()
+            ctx.decode_batch(frames, out=outs)
+            t_e = time.perf_counter() - t_e
+            out["end_to_end"] = {"value": round(px_rank / t_e / 1e6, 1), "unit": "MPix/s", "n_gpus": 1,
+                                 "seconds": round(t_e, 3), "host_threads": ctx_threads,
+                                 "note": "one batch: host entropy stage + H2D + kernels + D2H (pageable), "
+                                         "host-bound; not the headline value"}
+            del outs
         if world == 1 and not args.no_cpu_baseline:
             cb = cpu_baseline(datas, args.cpu_seconds)
             out["cpu_baseline"] = cb
             out["speedup_vs_cpu_baseline"] = round(value / cb["value"], 1)
+            threads = max(1, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)))
+            cba = cpu_baseline_parallel(datas, max(2.0, args.cpu_seconds / 2), threads)
+            out["cpu_baseline_all_cores"] = cba
+            out["speedup_vs_cpu_all_cores"] = round(value / cba["value"], 1)
         print(json.dumps(out), flush=True)
     b.close()
     ctx.close()

@@ -278,17 +278,23 @@ class Context:
     def batch(self, datas, flags=0):
         return Batch(self, datas, flags)
 
-    def decode_batch(self, datas, flags=0):
-        """Decode a list of WebP files; returns (list of RGBA arrays or None, status array)."""
+    def decode_batch(self, datas, flags=0, out=None):
+        """Decode a list of WebP files; returns (list of RGBA arrays or None, status array).
+        `out`: optional preallocated (H, W, 4) uint8 arrays, one per input."""
         bufs, ptrs, sizes = _ptr_arrays(datas)
         n = len(bufs)
         outs, optr, strides = [], (C.c_void_p * n)(), (C.c_int32 * n)()
         for i, b in enumerate(bufs):
-            try:
-                f = features(b)
-                a = np.empty((f.height, f.width, 4), np.uint8)
-            except WebPError:
-                a = np.empty((1, 1, 4), np.uint8)
+            if out is not None:
+                a = out[i]
+                if a.dtype != np.uint8 or a.ndim != 3 or a.shape[2] != 4 or not a.flags.c_contiguous:
+                    raise ValueError("out arrays must be C-contiguous (H, W, 4) uint8")
+            else:
+                try:
+                    f = features(b)
+                    a = np.empty((f.height, f.width, 4), np.uint8)
+                except WebPError:
+                    a = np.empty((1, 1, 4), np.uint8)
             outs.append(a)
             optr[i] = a.ctypes.data
             strides[i] = a.shape[1] * 4

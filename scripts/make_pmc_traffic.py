@@ -1,0 +1,55 @@
+#!/usr/bin/env python3
+"""HBM traffic per launch from rocprofv3 PMC passes -> profiles/pmc_traffic.json.
+
+Usage: make_pmc_traffic.py <workload name> <prof dir> [<workload name> <prof dir> ...]
+Each prof dir holds the passes written by scripts/profile.sh with PMC2=FETCH_SIZE and
+PMC3=WRITE_SIZE (one counter block each: FETCH_SIZE and WRITE_SIZE cannot share a pass).
+Per MI355X_MICROARCH.md (HBM section): FETCH_SIZE/WRITE_SIZE are KiB; FETCH_SIZE reports
+half the bytes of a coalesced streaming read on gfx950, so it is doubled; WRITE_SIZE is
+exact for 16-byte-per-lane streaming stores.  Averages over all launches of a kernel.
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KERNELS = {"vp8_recon_filter_kernel": "vp8_recon_filter_kernel", "yuv_to_rgba_kernel": "yuv_to_rgba_kernel"}
+
+
+def per_kernel(d):
+    acc = collections.defaultdict(list)
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            for key in KERNELS:
+                if key in r["Kernel_Name"]:
+                    acc[(key, r["Counter_Name"])].append(float(r["Counter_Value"]))
+    out = {}
+    for key in KERNELS:
+        fetch = acc.get((key, "FETCH_SIZE"))
+        write = acc.get((key, "WRITE_SIZE"))
+        if not fetch or not write:
+            continue
+        fb = 2.0 * 1024 * sum(fetch) / len(fetch)
+        wb = 1024.0 * sum(write) / len(write)
+        out[key] = {"bytes": int(fb + wb), "read_bytes": int(fb), "write_bytes": int(wb),
+                    "launches": len(fetch), "source": os.path.relpath(d, ROOT)}
+    return out
+
+
+def main():
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    data = json.load(open(path)) if os.path.exists(path) else {}
+    args = sys.argv[1:]
+    for name, d in zip(args[0::2], args[1::2]):
+        data[name] = per_kernel(d)
+    data["_note"] = ("HBM bytes per launch: 2*FETCH_SIZE + WRITE_SIZE (KiB->B), rocprofv3 --pmc in separate "
+                     "passes (scripts/profile.sh); FETCH_SIZE doubling per MI355X_MICROARCH.md gfx950 note")
+    json.dump(data, open(path, "w"), indent=1, sort_keys=True)
+    print(json.dumps(data, indent=1, sort_keys=True))
+
+
+if __name__ == "__main__":
+    main()
