@@ -132,6 +132,35 @@ int wg_vp8_parse(const uint8_t* data, size_t size, int flags, wg_vp8_info* info,
   return wg::vp8_parse(data, size, flags, info, mbs, nullptr);
 }
 
+int wg_vp8l_parse(const uint8_t* data, size_t size, wg_vp8l_info* info, uint32_t* argb,
+                  uint32_t* const* transform_data) {
+  if (data == nullptr || info == nullptr) return WG_STATUS_INVALID_PARAM;
+  wg::Container c;
+  wg_features feat{};
+  int st = wg::parse_container(data, size, &c, &feat);
+  if (st != WG_STATUS_OK) return st;
+  if (!c.is_lossless) return WG_STATUS_UNSUPPORTED_FEATURE;
+  wg::VP8LFrame f;
+  st = wg::vp8l_parse(data + c.payload_off, c.payload_size, &f);
+  if (st != WG_STATUS_OK) return st;
+  std::memset(info, 0, sizeof(*info));
+  info->width = f.width;
+  info->height = f.height;
+  info->has_alpha = f.has_alpha;
+  info->coded_width = f.coded_width;
+  info->num_transforms = (int32_t)f.transforms.size();
+  for (size_t i = 0; i < f.transforms.size(); ++i) {
+    info->transform_type[i] = f.transforms[i].type;
+    info->transform_bits[i] = f.transforms[i].bits;
+    info->transform_xsize[i] = f.transforms[i].xsize;
+    info->transform_size[i] = (int32_t)f.transforms[i].data.size();
+    if (transform_data && transform_data[i] && !f.transforms[i].data.empty())
+      std::memcpy(transform_data[i], f.transforms[i].data.data(), f.transforms[i].data.size() * 4);
+  }
+  if (argb) std::memcpy(argb, f.argb.data(), f.argb.size() * 4);
+  return WG_STATUS_OK;
+}
+
 wg_ctx* wg_ctx_create(int device, int host_threads) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return nullptr;

@@ -36,4 +36,25 @@ struct SparseFrame {
 int vp8_parse(const uint8_t* data, size_t size, int flags, wg_vp8_info* info,
               wg_vp8_mb* dense, SparseFrame* sparse);
 
+// VP8L (lossless) after the host entropy stage: the entropy-coded ARGB image and the
+// transforms in bitstream (read) order; the device applies them in reverse.
+enum : int { kVP8LPredictor = 0, kVP8LCrossColor = 1, kVP8LSubtractGreen = 2, kVP8LColorIndexing = 3 };
+
+struct VP8LTransform {
+  int type = 0;
+  int bits = 0;               // tile bits (predictor / cross-color) or pixel-packing bits (color indexing)
+  int xsize = 0, ysize = 0;   // image size the transform's output has
+  std::vector<uint32_t> data; // tile image, or the expanded palette (1 << (8 >> bits) entries)
+};
+
+struct VP8LFrame {
+  int width = 0, height = 0, has_alpha = 0;
+  int coded_width = 0;                    // width of `argb` (reduced by color-index packing)
+  std::vector<VP8LTransform> transforms;  // read order
+  std::vector<uint32_t> argb;             // coded_width * height
+};
+
+// Entropy-decode a VP8L bitstream (the VP8L chunk payload).
+int vp8l_parse(const uint8_t* data, size_t size, VP8LFrame* out);
+
 }  // namespace wg

@@ -18,8 +18,8 @@ import numpy as np
 
 __all__ = [
     "Status", "WebPError", "FLAG_BYPASS_FILTERING", "FLAG_NO_FANCY_UPSAMPLING", "Features",
-    "lib", "features", "decode_config", "decode", "Context", "Batch", "vp8_parse", "MB_DTYPE",
-    "VP8Info", "device_count", "yuv420_to_rgba_device",
+    "lib", "features", "decode_config", "decode", "Context", "Batch", "vp8_parse", "vp8l_parse", "MB_DTYPE",
+    "VP8Info", "VP8LInfo", "device_count", "yuv420_to_rgba_device",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -63,6 +63,14 @@ class VP8Info(C.Structure):
                 ("frame_offset", C.c_int32)]
 
 
+class VP8LInfo(C.Structure):
+    """wg_vp8l_info: a lossless frame after the host entropy stage."""
+    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("has_alpha", C.c_int32),
+                ("coded_width", C.c_int32), ("num_transforms", C.c_int32),
+                ("transform_type", C.c_int32 * 4), ("transform_bits", C.c_int32 * 4),
+                ("transform_xsize", C.c_int32 * 4), ("transform_size", C.c_int32 * 4)]
+
+
 # wg_vp8_mb: VP8MBData + VP8FInfo (pkg/vp8/models.go:66-107)
 MB_DTYPE = np.dtype([("coeffs", "<i2", (384,)), ("non_zero_y", "<u4"), ("non_zero_uv", "<u4"),
                      ("is_i4x4", "u1"), ("uvmode", "u1"), ("segment", "u1"), ("skip", "u1"),
@@ -94,6 +102,7 @@ _SIGS = {
     "wg_yuv420_to_rgba_device": (C.c_int, [_P, _P, _P, C.c_int, C.c_int, _P, C.c_int, C.c_int, C.c_int,
                                            C.c_int, _P]),
     "wg_vp8_parse": (C.c_int, [_P, C.c_size_t, C.c_int, C.POINTER(VP8Info), _P]),
+    "wg_vp8l_parse": (C.c_int, [_P, C.c_size_t, C.POINTER(VP8LInfo), _P, _P]),
 }
 EXPORTED = tuple(_SIGS)
 
@@ -180,6 +189,24 @@ def vp8_parse(data, flags=0, with_mbs=True):
     if st != Status.OK:
         raise WebPError(st, "wg_vp8_parse")
     return info, mbs
+
+
+def vp8l_parse(data):
+    """Host entropy stage of a lossless file: (VP8LInfo, coded ARGB image as uint32
+    (height, coded_width), [transform data arrays in read order])."""
+    b = _buf(data)
+    info = VP8LInfo()
+    L = lib()
+    st = L.wg_vp8l_parse(b, len(b), C.byref(info), None, None)
+    if st != Status.OK:
+        raise WebPError(st, "wg_vp8l_parse")
+    argb = np.zeros((info.height, info.coded_width), np.uint32)
+    tdata = [np.zeros(max(1, info.transform_size[i]), np.uint32) for i in range(info.num_transforms)]
+    ptrs = (C.c_void_p * 4)(*([t.ctypes.data for t in tdata] + [None] * (4 - len(tdata))))
+    st = L.wg_vp8l_parse(b, len(b), C.byref(info), argb.ctypes.data, ptrs)
+    if st != Status.OK:
+        raise WebPError(st, "wg_vp8l_parse")
+    return info, argb, tdata
 
 
 def _ptr_arrays(datas):

@@ -157,6 +157,26 @@ typedef struct {
  * `mbs` (mb_w*mb_h entries, raster order) may be NULL to only fill `info`. */
 int wg_vp8_parse(const uint8_t* data, size_t size, int flags, wg_vp8_info* info, wg_vp8_mb* mbs);
 
+/* ---- host entropy stage of VP8L (lossless) --------------------------------------------- */
+/* A lossless frame after prefix-code / LZ77 / color-cache decoding (libwebp DecodeImageStream,
+ * reference pkg/vp8/vp8l_dec.c.go), before its inverse transforms.  Transforms are listed in
+ * bitstream (read) order; they are undone in reverse.  Types: 0 predictor, 1 cross-color,
+ * 2 subtract-green, 3 color indexing. */
+typedef struct {
+  int32_t width, height, has_alpha;
+  int32_t coded_width;          /* width of the entropy-coded image (< width with pixel packing) */
+  int32_t num_transforms;
+  int32_t transform_type[4];
+  int32_t transform_bits[4];    /* tile bits, or packing bits for color indexing              */
+  int32_t transform_xsize[4];   /* output width of the transform                              */
+  int32_t transform_size[4];    /* uint32 words of its data (tile image / expanded palette)    */
+} wg_vp8l_info;
+
+/* `argb` (coded_width*height words) and `transform_data[i]` (transform_size[i] words) may be
+ * NULL to only fill `info`. */
+int wg_vp8l_parse(const uint8_t* data, size_t size, wg_vp8l_info* info, uint32_t* argb,
+                  uint32_t* const* transform_data);
+
 #ifdef __cplusplus
 }  /* extern "C" */
 #endif

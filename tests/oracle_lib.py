@@ -31,6 +31,7 @@ def oracle():
         L.oracle_yuv_to_rgba_point.argtypes = [P, C.c_int, P, P, C.c_int, P, C.c_int, C.c_int, C.c_int]
         L.oracle_transform_block.argtypes = [P, P, C.c_int]
         L.oracle_transform_block.restype = None
+        L.oracle_vp8l_decode.argtypes = [P, P, P, P]
         _lib = L
     return _lib
 
@@ -47,6 +48,24 @@ def oracle_decode(info, mbs, fancy=True):
                                     v.ctypes.data, rgba.ctypes.data, 1 if fancy else 0)
     assert st == 0
     return dict(y=y, u=u, v=v, rgba=rgba)
+
+
+def oracle_vp8l_decode(info, argb, tdata):
+    """CPU inverse transforms + BGRA->RGBA of a lossless frame from webp_amd.vp8l_parse."""
+    rgba = np.empty((info.height, info.width, 4), np.uint8)
+    ptrs = (C.c_void_p * 4)(*([t.ctypes.data for t in tdata] + [None] * (4 - len(tdata))))
+    assert oracle().oracle_vp8l_decode(C.addressof(info), argb.ctypes.data, ptrs, rgba.ctypes.data) == 0
+    return rgba
+
+
+def load_lossless(name):
+    with open(os.path.join(GOLDEN, "lossless", name + ".webp"), "rb") as f:
+        data = f.read()
+    return data, dict(np.load(os.path.join(GOLDEN, "lossless", name + ".npz")))
+
+
+def lossless_names():
+    return sorted(os.path.basename(p)[:-5] for p in glob.glob(os.path.join(GOLDEN, "lossless", "*.webp")))
 
 
 def oracle_yuv_to_rgba(y, u, v, fancy=True):
