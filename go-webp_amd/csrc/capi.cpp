@@ -21,6 +21,7 @@
 #include "host/host.h"
 
 using wg::FrameDesc;
+using wg::LLDesc;
 using wg::MbRec;
 
 struct wg_ctx {
@@ -37,26 +38,47 @@ inline size_t align_up(size_t v) { return (v + kAlign - 1) & ~(kAlign - 1); }
 
 struct FrameParse {
   int status = WG_STATUS_OK;
-  wg::SparseFrame sf;
-  size_t off_recs = 0, off_rows = 0, off_blocks = 0;  // within the input buffer
+  bool lossless = false;
+  wg::SparseFrame sf;  // lossy
+  wg::VP8LFrame lf;    // lossless
+  size_t off_recs = 0, off_rows = 0, off_blocks = 0;  // within the input buffer (lossy)
+  size_t off_coded = 0, off_tdata[4] = {0, 0, 0, 0};  // within the input buffer (lossless)
   size_t off_y = 0, off_u = 0, off_v = 0;            // within the plane buffer
+  size_t off_scratch = 0;                             // lossless two-pass scratch (plane buffer)
   size_t off_rgba = 0;                                // within the RGBA buffer
+  int width = 0, height = 0;
 };
 
 struct Timing {
-  hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
 };
+
+// Does the lossless frame need a second pass (predictor and color indexing both present)?
+bool ll_two_pass(const wg::VP8LFrame& f) {
+  int cores = 0;
+  for (const auto& t : f.transforms) cores += (t.type == wg::kVP8LPredictor || t.type == wg::kVP8LColorIndexing);
+  return cores > 1;
+}
 
 int parse_one(const uint8_t* data, size_t size, int flags, FrameParse* fp) {
   wg::Container c;
   wg_features feat{};
   int st = wg::parse_container(data, size, &c, &feat);
   if (st != WG_STATUS_OK) return st;
-  if (c.is_lossless) return WG_STATUS_UNSUPPORTED_FEATURE;  // VP8L: next row of SURVEY §8(f)
+  if (c.is_lossless) {  // VP8L: host entropy stage, K3 on device
+    fp->lossless = true;
+    st = wg::vp8l_parse(data + c.payload_off, c.payload_size, &fp->lf);
+    if (st != WG_STATUS_OK) return st;
+    fp->width = fp->lf.width;
+    fp->height = fp->lf.height;
+    return WG_STATUS_OK;
+  }
   if (c.alpha_size > 0) return WG_STATUS_UNSUPPORTED_FEATURE;  // ALPH: next row (f2)
   st = wg::vp8_parse(data, size, flags, nullptr, nullptr, &fp->sf);
   if (st != WG_STATUS_OK) return st;
   if (fp->sf.info.mb_w > wg::vp8_recon_max_mb_w()) return WG_STATUS_UNSUPPORTED_FEATURE;
+  fp->width = fp->sf.info.width;
+  fp->height = fp->sf.info.height;
   return WG_STATUS_OK;
 }
 
@@ -93,7 +115,10 @@ struct wg_batch {
   int flags = 0;
   std::vector<FrameParse> fp;
   std::vector<FrameDesc> desc;
+  std::vector<LLDesc> lldesc;
   FrameDesc* d_desc = nullptr;
+  LLDesc* d_lldesc = nullptr;
+  int n_lossy = 0, n_lossless = 0;
   int* d_err = nullptr;
   uint8_t* d_in = nullptr;
   uint8_t* d_planes = nullptr;
@@ -102,7 +127,7 @@ struct wg_batch {
   int max_mb_w = 1, max_w = 1, max_h = 1;
   int n_valid = 0;
   int64_t pixels = 0;
-  double kbytes[2] = {0, 0};
+  double kbytes[3] = {0, 0, 0};
   std::vector<Timing> timings;  // one per run since the last query
   size_t n_runs_pending = 0;
 };
@@ -190,6 +215,7 @@ void wg_batch_destroy(wg_batch* b) {
     for (auto& e : t.ev)
       if (e) hipEventDestroy(e);
   if (b->d_desc) hipFree(b->d_desc);
+  if (b->d_lldesc) hipFree(b->d_lldesc);
   if (b->d_err) hipFree(b->d_err);
   if (b->d_in) hipFree(b->d_in);
   if (b->d_planes) hipFree(b->d_planes);
@@ -210,10 +236,38 @@ wg_batch* wg_batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t*
   // layout
   size_t in_b = 0, pl_b = 0, rg_b = 0;
   double k1 = 0, k2 = 0;
+  double k3 = 0;
   for (int i = 0; i < n; ++i) {
     FrameParse& f = b->fp[i];
     if (status) status[i] = f.status;
     if (f.status != WG_STATUS_OK) continue;
+    f.off_rgba = rg_b;
+    rg_b = align_up(rg_b + (size_t)f.width * f.height * 4);
+    b->max_w = std::max(b->max_w, f.width);
+    b->max_h = std::max(b->max_h, f.height);
+    b->n_valid++;
+    b->pixels += (int64_t)f.width * f.height;
+    const double px = (double)f.width * f.height;
+    if (f.lossless) {
+      // K3 reads the coded image + transform data, writes RGBA (and a scratch image when
+      // two passes are needed).
+      b->n_lossless++;
+      f.off_coded = in_b;
+      in_b = align_up(in_b + f.lf.argb.size() * 4);
+      k3 += f.lf.argb.size() * 4.0 + 4.0 * px;
+      for (size_t t = 0; t < f.lf.transforms.size(); ++t) {
+        f.off_tdata[t] = in_b;
+        in_b = align_up(in_b + std::max<size_t>(f.lf.transforms[t].data.size(), 1) * 4);
+        k3 += f.lf.transforms[t].data.size() * 4.0;
+      }
+      if (ll_two_pass(f.lf)) {
+        f.off_scratch = pl_b;
+        pl_b = align_up(pl_b + (size_t)f.width * f.height * 4);
+        k3 += 8.0 * px;
+      }
+      continue;
+    }
+    b->n_lossy++;
     const wg_vp8_info& inf = f.sf.info;
     const size_t nmb = (size_t)inf.mb_w * inf.mb_h;
     f.off_recs = in_b;
@@ -228,20 +282,14 @@ wg_batch* wg_batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t*
     pl_b = align_up(pl_b + nmb * 64);
     f.off_v = pl_b;
     pl_b = align_up(pl_b + nmb * 64);
-    f.off_rgba = rg_b;
-    rg_b = align_up(rg_b + (size_t)inf.width * inf.height * 4);
     b->max_mb_w = std::max(b->max_mb_w, inf.mb_w);
-    b->max_w = std::max(b->max_w, inf.width);
-    b->max_h = std::max(b->max_h, inf.height);
-    b->n_valid++;
-    b->pixels += (int64_t)inf.width * inf.height;
     // algorithmic bytes: K1 reads records + coefficients, writes MB-padded
     // planes; K2 reads cropped planes, writes RGBA.
-    const double px = (double)inf.width * inf.height;
     const double uvpx = 2.0 * ((inf.width + 1) / 2) * (double)((inf.height + 1) / 2);
     k1 += (double)nmb * sizeof(MbRec) + inf.mb_h * 4.0 + f.sf.blocks.size() * 2.0 + nmb * 384.0;
     k2 += px + uvpx + 4.0 * px;
   }
+  b->kbytes[2] = k3;
   b->kbytes[0] = k1;
   b->kbytes[1] = k2;
   b->in_bytes = std::max<size_t>(in_b, kAlign);
@@ -257,6 +305,7 @@ wg_batch* wg_batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t*
   if (hipMalloc(&b->d_in, b->in_bytes) != hipSuccess || hipMalloc(&b->d_planes, b->plane_bytes) != hipSuccess ||
       hipMalloc(&b->d_rgba, b->rgba_bytes) != hipSuccess ||
       hipMalloc(&b->d_desc, sizeof(FrameDesc) * (size_t)n) != hipSuccess ||
+      hipMalloc(&b->d_lldesc, sizeof(LLDesc) * (size_t)std::max(b->n_lossless, 1)) != hipSuccess ||
       hipMalloc(&b->d_err, sizeof(int)) != hipSuccess || hipMemset(b->d_err, 0, sizeof(int)) != hipSuccess)
     return fail(WG_STATUS_OUT_OF_MEMORY);
   // stage inputs in pinned memory, one H2D copy
@@ -268,6 +317,41 @@ wg_batch* wg_batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t*
     FrameParse& f = b->fp[i];
     FrameDesc& d = b->desc[i];
     if (f.status != WG_STATUS_OK) continue;
+    d.rgba = b->d_rgba + f.off_rgba;
+    d.width = f.width;
+    d.height = f.height;
+    d.rgba_stride = 4 * f.width;
+    if (f.lossless) {  // K1/K2 skip it (valid = 0); K3 gets an LLDesc
+      LLDesc l{};
+      std::memcpy(h_in + f.off_coded, f.lf.argb.data(), f.lf.argb.size() * 4);
+      l.coded = reinterpret_cast<const uint32_t*>(b->d_in + f.off_coded);
+      l.coded_bytes = (int32_t)(f.lf.argb.size() * 4);
+      l.scratch = ll_two_pass(f.lf) ? reinterpret_cast<uint32_t*>(b->d_planes + f.off_scratch) : nullptr;
+      l.scratch_bytes = l.scratch ? f.width * f.height * 4 : 0;
+      l.rgba = d.rgba;
+      l.rgba_stride = d.rgba_stride;
+      l.width = f.width;
+      l.height = f.height;
+      l.coded_width = f.lf.coded_width;
+      l.n_stages = (int32_t)f.lf.transforms.size();
+      for (int t = 0; t < l.n_stages; ++t) {  // application order = reverse of read order
+        const wg::VP8LTransform& tr = f.lf.transforms[(size_t)(l.n_stages - 1 - t)];
+        const size_t off = f.off_tdata[l.n_stages - 1 - t];
+        if (!tr.data.empty()) std::memcpy(h_in + off, tr.data.data(), tr.data.size() * 4);
+        l.stages[t].type = tr.type;
+        l.stages[t].bits = tr.bits;
+        l.stages[t].xsize = tr.xsize;
+        l.stages[t].tiles_per_row = (tr.type == wg::kVP8LPredictor || tr.type == wg::kVP8LCrossColor)
+                                        ? (tr.xsize + (1 << tr.bits) - 1) >> tr.bits
+                                        : 0;
+        l.stages[t].data = reinterpret_cast<const uint32_t*>(b->d_in + off);
+      }
+      l.valid = 1;
+      b->lldesc.push_back(l);
+      wg::VP8LFrame().transforms.swap(f.lf.transforms);
+      std::vector<uint32_t>().swap(f.lf.argb);
+      continue;
+    }
     const wg_vp8_info& inf = f.sf.info;
     std::memcpy(h_in + f.off_recs, f.sf.mbs.data(), f.sf.mbs.size() * sizeof(MbRec));
     std::memcpy(h_in + f.off_rows, f.sf.row_block0.data(), f.sf.row_block0.size() * 4);
@@ -279,14 +363,10 @@ wg_batch* wg_batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t*
     d.y = b->d_planes + f.off_y;
     d.u = b->d_planes + f.off_u;
     d.v = b->d_planes + f.off_v;
-    d.rgba = b->d_rgba + f.off_rgba;
-    d.width = inf.width;
-    d.height = inf.height;
     d.mb_w = inf.mb_w;
     d.mb_h = inf.mb_h;
     d.y_stride = 16 * inf.mb_w;
     d.uv_stride = 8 * inf.mb_w;
-    d.rgba_stride = 4 * inf.width;
     d.filter_type = inf.filter_type;
     d.flags = flags;
     d.valid = 1;
@@ -298,6 +378,9 @@ wg_batch* wg_batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t*
   hipError_t e = hipMemcpyAsync(b->d_in, h_in, b->in_bytes, hipMemcpyHostToDevice, ctx->stream);
   if (e == hipSuccess)
     e = hipMemcpyAsync(b->d_desc, b->desc.data(), sizeof(FrameDesc) * (size_t)n, hipMemcpyHostToDevice,
+                       ctx->stream);
+  if (e == hipSuccess && !b->lldesc.empty())
+    e = hipMemcpyAsync(b->d_lldesc, b->lldesc.data(), sizeof(LLDesc) * b->lldesc.size(), hipMemcpyHostToDevice,
                        ctx->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
   hipHostFree(h_in);
@@ -318,43 +401,51 @@ int wg_batch_run(wg_batch* b, void* stream) {
   }
   Timing& t = b->timings[b->n_runs_pending++];
   hipEventRecord(t.ev[0], s);
-  hipError_t e = wg::launch_vp8_recon_filter(b->d_desc, b->n, b->max_mb_w, b->d_err, s);
-  if (e != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
+  if (b->n_lossy > 0) {
+    hipError_t e = wg::launch_vp8_recon_filter(b->d_desc, b->n, b->max_mb_w, b->d_err, s);
+    if (e != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
+  }
   hipEventRecord(t.ev[1], s);
-  e = wg::launch_yuv_to_rgba(b->d_desc, nullptr, b->n, b->max_w, b->max_h,
-                             (b->flags & WG_FLAG_NO_FANCY_UPSAMPLING) ? 0 : 1, s);
-  if (e != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
+  if (b->n_lossy > 0) {
+    hipError_t e = wg::launch_yuv_to_rgba(b->d_desc, nullptr, b->n, b->max_w, b->max_h,
+                                          (b->flags & WG_FLAG_NO_FANCY_UPSAMPLING) ? 0 : 1, s);
+    if (e != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
+  }
   hipEventRecord(t.ev[2], s);
+  if (b->n_lossless > 0) {
+    hipError_t e = wg::launch_vp8l_transforms(b->d_lldesc, b->n_lossless, b->d_err, s);
+    if (e != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
+  }
+  hipEventRecord(t.ev[3], s);
   return WG_STATUS_OK;
 }
 
 int wg_batch_kernel_ms(const wg_batch* bc, float* ms, int n_ms) {
   wg_batch* b = const_cast<wg_batch*>(bc);
-  if (!b || !ms || n_ms < 2) return WG_STATUS_INVALID_PARAM;
-  ms[0] = ms[1] = 0.f;
+  if (!b || !ms || n_ms < 1) return WG_STATUS_INVALID_PARAM;
+  for (int k = 0; k < n_ms; ++k) ms[k] = 0.f;
   if (b->n_runs_pending == 0) return WG_STATUS_OK;
-  double s0 = 0, s1 = 0;
+  double acc[3] = {0, 0, 0};
   for (size_t i = 0; i < b->n_runs_pending; ++i) {
     Timing& t = b->timings[i];
-    if (hipEventSynchronize(t.ev[2]) != hipSuccess) return WG_STATUS_USER_ABORT;
-    float a = 0, c = 0;
-    hipEventElapsedTime(&a, t.ev[0], t.ev[1]);
-    hipEventElapsedTime(&c, t.ev[1], t.ev[2]);
-    s0 += a;
-    s1 += c;
+    if (hipEventSynchronize(t.ev[3]) != hipSuccess) return WG_STATUS_USER_ABORT;
+    for (int k = 0; k < 3; ++k) {
+      float a = 0;
+      hipEventElapsedTime(&a, t.ev[k], t.ev[k + 1]);
+      acc[k] += a;
+    }
   }
   int err = 0;
   if (hipMemcpy(&err, b->d_err, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess || err) return WG_STATUS_USER_ABORT;
-  ms[0] = (float)(s0 / b->n_runs_pending);
-  ms[1] = (float)(s1 / b->n_runs_pending);
+  const bool ran[3] = {b->n_lossy > 0, b->n_lossy > 0, b->n_lossless > 0};
+  for (int k = 0; k < std::min(n_ms, 3); ++k) ms[k] = ran[k] ? (float)(acc[k] / b->n_runs_pending) : 0.f;
   b->n_runs_pending = 0;
   return WG_STATUS_OK;
 }
 
 int wg_batch_kernel_bytes(const wg_batch* b, double* bytes, int n_bytes) {
-  if (!b || !bytes || n_bytes < 2) return WG_STATUS_INVALID_PARAM;
-  bytes[0] = b->kbytes[0];
-  bytes[1] = b->kbytes[1];
+  if (!b || !bytes || n_bytes < 1) return WG_STATUS_INVALID_PARAM;
+  for (int k = 0; k < n_bytes; ++k) bytes[k] = k < 3 ? b->kbytes[k] : 0.0;
   return WG_STATUS_OK;
 }
 
@@ -389,6 +480,7 @@ int wg_batch_download_rgba(wg_batch* b, int i, uint8_t* rgba, int stride) {
 int wg_batch_download_yuv(wg_batch* b, int i, uint8_t* y, uint8_t* u, uint8_t* v) {
   if (!b || i < 0 || i >= b->n) return WG_STATUS_INVALID_PARAM;
   if (b->fp[i].status != WG_STATUS_OK) return b->fp[i].status;
+  if (b->fp[i].lossless) return WG_STATUS_UNSUPPORTED_FEATURE;  // VP8L has no YUV planes
   const FrameDesc& d = b->desc[i];
   hipSetDevice(b->ctx->device);
   hipError_t e = hipDeviceSynchronize();

@@ -19,4 +19,9 @@ hipError_t launch_vp8_recon_filter(const FrameDesc* d_frames, int n_frames, int 
 hipError_t launch_yuv_to_rgba(const FrameDesc* d_frames, const FrameDesc* single, int n_frames,
                               int max_w, int max_h, int fancy, hipStream_t stream);
 
+// K3: VP8L inverse transforms + BGRA->RGBA, one 1024-thread workgroup per lossless frame.
+size_t vp8l_lds_bytes();
+// d_err: OR-ed with 2 if a wave gave up waiting (bounded spin).
+hipError_t launch_vp8l_transforms(const LLDesc* d_frames, int n_frames, int* d_err, hipStream_t stream);
+
 }  // namespace wg

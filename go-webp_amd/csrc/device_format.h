@@ -59,4 +59,26 @@ struct FrameDesc {
 };
 static_assert(sizeof(FrameDesc) == 128, "FrameDesc must be 128 bytes");
 
+// One lossless (VP8L) frame for K3.  `coded` is the entropy-coded ARGB image from the host
+// stage; `stages` are its transforms in APPLICATION order (the reverse of bitstream order).
+// Transform types: 0 predictor, 1 cross-color, 2 add-green (subtract-green undone),
+// 3 color indexing.
+struct LLStage {
+  int32_t type, bits, xsize, tiles_per_row;
+  const uint32_t* data;  // tile image (predictor / cross-color) or expanded palette
+};
+static_assert(sizeof(LLStage) == 24, "LLStage must be 24 bytes");
+
+struct LLDesc {
+  const uint32_t* coded;
+  uint32_t* scratch;  // width*height words, used when the transforms need two passes
+  uint8_t* rgba;
+  uint64_t pad0;
+  int32_t width, height, coded_width, n_stages;
+  int32_t valid, rgba_stride, coded_bytes, scratch_bytes;
+  LLStage stages[4];
+  uint64_t pad1[4];
+};
+static_assert(sizeof(LLDesc) == 192, "LLDesc must be 192 bytes");
+
 }  // namespace wg

@@ -239,16 +239,18 @@ class Batch:
             raise WebPError(st, "wg_batch_run")
 
     def kernel_ms(self):
-        ms = (C.c_float * 2)()
-        st = lib().wg_batch_kernel_ms(self._h, ms, 2)
+        """(K1, K2, K3) per-launch ms averaged over the runs since the last call."""
+        ms = (C.c_float * 3)()
+        st = lib().wg_batch_kernel_ms(self._h, ms, 3)
         if st != Status.OK:
             raise WebPError(st, "wg_batch_kernel_ms")
-        return float(ms[0]), float(ms[1])
+        return float(ms[0]), float(ms[1]), float(ms[2])
 
     def kernel_bytes(self):
-        b = (C.c_double * 2)()
-        lib().wg_batch_kernel_bytes(self._h, b, 2)
-        return float(b[0]), float(b[1])
+        """Algorithmic HBM bytes per launch of (K1, K2, K3)."""
+        b = (C.c_double * 3)()
+        lib().wg_batch_kernel_bytes(self._h, b, 3)
+        return float(b[0]), float(b[1]), float(b[2])
 
     @property
     def pixels(self):

@@ -98,14 +98,17 @@ wg_batch* wg_batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t*
 void wg_batch_destroy(wg_batch* b);
 
 /* Run the device DSP path for the whole batch on `stream` (NULL = ctx stream):
- * K1 reconstruct+deblock wavefront, K2 YUV420->RGBA.  Kernel durations of the last run
+ * lossy frames: K1 reconstruct+deblock wavefront, K2 YUV420->RGBA; lossless frames:
+ * K3 inverse transforms + RGBA.  Kernel durations of the last run
  * (HIP events on that stream) are available from wg_batch_kernel_ms(). */
 int wg_batch_run(wg_batch* b, void* stream);
 
-/* ms[0] = reconstruct+filter kernel, ms[1] = yuv->rgba kernel (last run). */
+/* Per-launch kernel durations averaged over the runs since the last query:
+ * ms[0] = VP8 reconstruct+filter (K1), ms[1] = YUV->RGBA (K2), ms[2] = VP8L inverse
+ * transforms (K3); a kernel with no frames in the batch reports 0.  n_ms >= 1. */
 int wg_batch_kernel_ms(const wg_batch* b, float* ms, int n_ms);
 
-/* Algorithmic HBM bytes per launch of each kernel. */
+/* Algorithmic HBM bytes per launch of K1, K2, K3. */
 int wg_batch_kernel_bytes(const wg_batch* b, double* bytes, int n_bytes);
 
 int wg_batch_size(const wg_batch* b);
@@ -115,7 +118,7 @@ int64_t wg_batch_pixels(const wg_batch* b);
 /* Copy results of frame i back to host: RGBA (stride >= 4*width) and/or the cropped
  * Y/U/V planes (strides width, (width+1)/2). */
 int wg_batch_download_rgba(wg_batch* b, int i, uint8_t* rgba, int stride);
-int wg_batch_download_yuv(wg_batch* b, int i, uint8_t* y, uint8_t* u, uint8_t* v);
+int wg_batch_download_yuv(wg_batch* b, int i, uint8_t* y, uint8_t* u, uint8_t* v); /* lossy only */
 
 /* ---- stage entry point: YUV420 -> RGBA on device pointers ---------------------------- */
 /* Fancy (fancy!=0, UpsampleRgbaLinePair, upsampling.c.go:43-107) or point-sampled
