@@ -119,6 +119,7 @@ struct wg_batch {
   FrameDesc* d_desc = nullptr;
   LLDesc* d_lldesc = nullptr;
   int n_lossy = 0, n_lossless = 0;
+  int ll_groups[wg::kVP8LVariants] = {0, 0, 0, 0, 0};  // K3 frames per kernel variant
   int* d_err = nullptr;
   uint8_t* d_in = nullptr;
   uint8_t* d_planes = nullptr;
@@ -347,6 +348,16 @@ wg_batch* wg_batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t*
         l.stages[t].data = reinterpret_cast<const uint32_t*>(b->d_in + off);
       }
       l.valid = 1;
+      {
+        int types[4], bits[4], tiles[4];
+        for (int t = 0; t < l.n_stages; ++t) {
+          const wg::LLStage& st = l.stages[t];
+          types[t] = st.type;
+          bits[t] = st.bits;
+          tiles[t] = st.tiles_per_row ? st.tiles_per_row * ((f.height + (1 << st.bits) - 1) >> st.bits) : 0;
+        }
+        l.pad1[0] = (uint64_t)wg::vp8l_variant(types, bits, tiles, l.n_stages);  // sort key
+      }
       b->lldesc.push_back(l);
       wg::VP8LFrame().transforms.swap(f.lf.transforms);
       std::vector<uint32_t>().swap(f.lf.argb);
@@ -379,6 +390,10 @@ wg_batch* wg_batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t*
   if (e == hipSuccess)
     e = hipMemcpyAsync(b->d_desc, b->desc.data(), sizeof(FrameDesc) * (size_t)n, hipMemcpyHostToDevice,
                        ctx->stream);
+  // K3 launches one kernel per variant over a contiguous group of descriptors
+  std::stable_sort(b->lldesc.begin(), b->lldesc.end(),
+                   [](const LLDesc& a, const LLDesc& c) { return a.pad1[0] < c.pad1[0]; });
+  for (const LLDesc& l : b->lldesc) b->ll_groups[l.pad1[0]]++;
   if (e == hipSuccess && !b->lldesc.empty())
     e = hipMemcpyAsync(b->d_lldesc, b->lldesc.data(), sizeof(LLDesc) * b->lldesc.size(), hipMemcpyHostToDevice,
                        ctx->stream);
@@ -413,7 +428,7 @@ int wg_batch_run(wg_batch* b, void* stream) {
   }
   hipEventRecord(t.ev[2], s);
   if (b->n_lossless > 0) {
-    hipError_t e = wg::launch_vp8l_transforms(b->d_lldesc, b->n_lossless, b->d_err, s);
+    hipError_t e = wg::launch_vp8l_transforms(b->d_lldesc, b->ll_groups, b->d_err, s);
     if (e != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
   }
   hipEventRecord(t.ev[3], s);

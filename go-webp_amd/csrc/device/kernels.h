@@ -21,7 +21,11 @@ hipError_t launch_yuv_to_rgba(const FrameDesc* d_frames, const FrameDesc* single
 
 // K3: VP8L inverse transforms + BGRA->RGBA, one 1024-thread workgroup per lossless frame.
 size_t vp8l_lds_bytes();
+// Frames are grouped by variant (vp8l_variant(): 0 generic, 1..4 compile-time predictor
+// passes); d_frames holds group 0 first, then 1..4; group_count[v] frames each.
 // d_err: OR-ed with 2 if a wave gave up waiting (bounded spin).
-hipError_t launch_vp8l_transforms(const LLDesc* d_frames, int n_frames, int* d_err, hipStream_t stream);
+constexpr int kVP8LVariants = 5;
+int vp8l_variant(const int* types, const int* bits, const int* tiles, int n_stages);  // stages in application order
+hipError_t launch_vp8l_transforms(const LLDesc* d_frames, const int* group_count, int* d_err, hipStream_t stream);
 
 }  // namespace wg

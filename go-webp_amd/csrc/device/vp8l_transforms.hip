@@ -94,6 +94,38 @@ __device__ __forceinline__ uint32_t predict(int mode, uint32_t L, uint32_t T, ui
   }
 }
 
+// All fourteen predictors by per-lane mode without a divergent switch: the cheap ones
+// (copies, Average2 family, Select) computed for every lane, ClampedAddSubtract{Full,Half}
+// only when some lane of the wave uses them, then a 4-level v_cndmask tree on the mode
+// bits.  Modes 0, 14, 15 -> ARGB black.
+__device__ __forceinline__ uint32_t predict_tree(int mode, uint32_t L, uint32_t T, uint32_t TL, uint32_t TR) {
+  const uint32_t a6 = avg2(L, TL), a9 = avg2(T, TR);
+  uint32_t v[16];
+  v[0] = 0xff000000u;
+  v[1] = L;
+  v[2] = T;
+  v[3] = TR;
+  v[4] = TL;
+  v[5] = avg2(avg2(L, TR), T);
+  v[6] = a6;
+  v[7] = avg2(L, T);
+  v[8] = avg2(TL, T);
+  v[9] = a9;
+  v[10] = avg2(a6, a9);
+  v[11] = select_px(T, L, TL);
+  v[12] = v[13] = 0;
+  if (__any(mode == 12)) v[12] = add_sub_full(L, T, TL);
+  if (__any(mode == 13)) v[13] = add_sub_half(L, T, TL);
+  v[14] = v[15] = 0xff000000u;
+#pragma unroll
+  for (int lvl = 0, w = 16; lvl < 4; ++lvl, w >>= 1) {
+    const bool bit = (mode >> lvl) & 1;
+#pragma unroll
+    for (int k = 0; k < w / 2; ++k) v[k] = bit ? v[2 * k + 1] : v[2 * k];
+  }
+  return v[0];
+}
+
 __device__ __forceinline__ int cdelta(int t, int c) {  // ColorTransformDelta on int8 values
   return ((int)(int8_t)t * (int)(int8_t)c) >> 5;
 }
@@ -112,33 +144,8 @@ __device__ __forceinline__ uint32_t bgra_to_rgba(uint32_t c) {
   return __builtin_amdgcn_perm(c, c, 0x07040506u);  // bytes B,G,R,A -> R,G,B,A
 }
 
-// A per-pixel op (cross-color or add-green) with its tile table.
-struct PixOp {
-  int type, bits, tpr, idx;  // idx: stage index in the frame's list
-  const uint32_t* cc;        // LDS or global multipliers (cross-color)
-};
-
-__device__ __forceinline__ uint32_t apply_ops(const PixOp* ops, int n, uint32_t v, int x, int y) {
-  for (int k = 0; k < n; ++k) {
-    if (ops[k].type == T_AG) {
-      v = add_green(v);
-    } else {
-      v = cross_color_inv(v, ops[k].cc[(y >> ops[k].bits) * ops[k].tpr + (x >> ops[k].bits)]);
-    }
-  }
-  return v;
-}
-
 __device__ __forceinline__ uint32_t shr1(uint32_t old, uint32_t v) {  // lane i <- lane i-1; lane 0 <- old
   return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x138, 0xF, 0xF, false);
-}
-
-// Stage a cross-color table into LDS when it fits; returns the table to use.
-__device__ const uint32_t* stage_cc(const LLStage& st, uint32_t* lds_cc, int ysize) {
-  const int n = st.tiles_per_row * ((ysize + (1 << st.bits) - 1) >> st.bits);
-  if (n > kCCTabMax) return st.data;
-  for (int t = threadIdx.x; t < n; t += blockDim.x) lds_cc[t] = st.data[t];
-  return lds_cc;
 }
 
 // Bounded spin on a progress counter: gives up after 2 s (s_memrealtime is 100 MHz),
@@ -156,6 +163,151 @@ __device__ __forceinline__ bool wait_progress(uint32_t* pr, uint32_t need, int* 
   return true;
 }
 
+// Per-pass context, all wave-uniform.  Per-pixel ops: up to two (cross-color, add-green;
+// each type occurs once per frame) before and after the core.  The cross-color table and
+// the predictor modes live in LDS when they fit, else they are read from HBM.
+struct Pass {
+  int npre, pre0, pre1;    // op types, application order
+  int npost, post0, post1;
+  int cc_bits, cc_tpr, cc_in_lds;
+  gptr<const uint32_t> cc_g;
+  int m_bits, m_tpr, m_in_lds;
+  gptr<const uint32_t> m_g;
+};
+
+__device__ __forceinline__ uint32_t cc_word(const Pass& P, const uint32_t* cc_lds, int x, int y) {
+  const int t = (y >> P.cc_bits) * P.cc_tpr + (x >> P.cc_bits);
+  return P.cc_in_lds ? cc_lds[t] : P.cc_g[t];
+}
+__device__ __forceinline__ uint32_t op(int type, const Pass& P, const uint32_t* cc_lds, uint32_t v, int x, int y) {
+  return type == T_AG ? add_green(v) : cross_color_inv(v, cc_word(P, cc_lds, x, y));
+}
+__device__ __forceinline__ uint32_t pre_ops(const Pass& P, const uint32_t* cc_lds, uint32_t v, int x, int y) {
+  if (P.npre > 0) v = op(P.pre0, P, cc_lds, v, x, y);
+  if (P.npre > 1) v = op(P.pre1, P, cc_lds, v, x, y);
+  return v;
+}
+__device__ __forceinline__ uint32_t post_ops(const Pass& P, const uint32_t* cc_lds, uint32_t v, int x, int y) {
+  if (P.npost > 0) v = op(P.post0, P, cc_lds, v, x, y);
+  if (P.npost > 1) v = op(P.post1, P, cc_lds, v, x, y);
+  return v;
+}
+
+// Compile-time per-pixel op sequences: 0 none, 1 cross-color, 2 add-green,
+// 3 cross-color then add-green, 4 add-green then cross-color.
+template <int OPS>
+__device__ __forceinline__ uint32_t ops_ct(const Pass& P, const uint32_t* cc_lds, uint32_t v, int x, int y) {
+  auto cc = [&](uint32_t a) {
+    return cross_color_inv(a, cc_lds[(y >> P.cc_bits) * P.cc_tpr + (x >> P.cc_bits)]);
+  };
+  if (OPS == 1) return cc(v);
+  if (OPS == 2) return add_green(v);
+  if (OPS == 3) return add_green(cc(v));
+  if (OPS == 4) return cc(add_green(v));
+  return v;
+}
+
+// The predictor wavefront of one pass (see the file comment).  GENERIC: ops and tables
+// at run time (tables may be in HBM); otherwise PRE/POST ops are compile-time and both
+// tables are in LDS.  Returns false if a wave gave up waiting.
+template <int PRE, int POST, bool GENERIC>
+__device__ __forceinline__ bool pred_wavefront(const Pass& P, int W, int H, int w_in, bool last, __amdgpu_buffer_rsrc_t in_rs,
+                               __amdgpu_buffer_rsrc_t out_rs, int dst_stride, uint32_t* ring, const uint8_t* mode_tab,
+                               const uint32_t* cc_tab, uint32_t* prog, int* err) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int nbands = (H + kBand - 1) / kBand;
+  const int steps = W + 2 * (kBand - 1);
+  const int nchunks = (steps + kChunk - 1) / kChunk;
+  for (int b = wave; b < nbands; b += kWaves) {
+    const int y = b * kBand + lane;
+    const bool row_ok = y < H;
+    const uint32_t* ring_prev = ring + ((b - 1) & (kWaves - 1)) * kRing;  // band b-1's last row
+    uint32_t* ring_mine = ring + (b & (kWaves - 1)) * kRing;
+    // ring slot b&15 was last written by band b-16 and read by band b-15: that reader
+    // must be done before this band overwrites it
+    if (b >= kWaves && !wait_progress(prog + ((b - kWaves + 1) & (kWaves - 1)),
+                                      ((uint32_t)(b - kWaves + 1) << 16) | (uint32_t)steps, err))
+      return false;
+    const int mrow = (y >> P.m_bits) * P.m_tpr;
+    uint32_t h1 = 0, h2 = 0, h3 = 0, first = 0;
+    uint32_t cin[kChunk], cnext[kChunk];
+    auto load_chunk = [&](int c, uint32_t* dstv) {
+#pragma unroll
+      for (int k = 0; k < kChunk; k += 2) {
+        const int x = c * kChunk + k - 2 * lane;
+        const bool ok = row_ok && x >= 0 && x < W;
+        const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(in_rs, ok ? (y * w_in + x) * 4 : (int)kDrop, 0, 0);
+        dstv[k] = v.x;
+        dstv[k + 1] = v.y;
+      }
+    };
+    load_chunk(0, cin);
+    for (int c = 0; c < nchunks; ++c) {
+      if (c + 1 < nchunks) load_chunk(c + 1, cnext);
+      // band b-1 must be 135 steps ahead of this chunk's end (its last row, lane 63, then
+      // covers column x+1 of lane 0); band b+1 must have consumed the ring columns this
+      // chunk overwrites
+      if (b > 0) {
+        const uint32_t need = ((uint32_t)(b - 1) << 16) | (uint32_t)min(c * kChunk + kChunk + 127, steps);
+        if (!wait_progress(prog + ((b - 1) & (kWaves - 1)), need, err)) return false;
+      }
+      if (b + 1 < nbands) {
+        const int lag = c * kChunk + kChunk - 2 * (kBand - 1) - kRing + 16;  // oldest column still needed
+        if (lag > 0 &&
+            !wait_progress(prog + ((b + 1) & (kWaves - 1)), ((uint32_t)(b + 1) << 16) | (uint32_t)lag, err))
+          return false;
+      }
+      uint32_t cout[kChunk];
+#pragma unroll
+      for (int k = 0; k < kChunk; ++k) {
+        const int s = c * kChunk + k;
+        const int x = s - 2 * lane;
+        const bool ok = row_ok && x >= 0 && x < W;
+        // row above: lane i-1's outputs at steps s-1 (x+1), s-2 (x), s-3 (x-1); lane 0
+        // reads the previous band's last row from the ring
+        const uint32_t rTR = ring_prev[(x + 1) & (kRing - 1)];
+        const uint32_t rT = ring_prev[x & (kRing - 1)];
+        const uint32_t rTL = ring_prev[(x - 1) & (kRing - 1)];
+        uint32_t TR = shr1(rTR, h1);
+        const uint32_t T = shr1(rT, h2), TL = shr1(rTL, h3);
+        const uint32_t v = GENERIC ? pre_ops(P, cc_tab, cin[k], x, y) : ops_ct<PRE>(P, cc_tab, cin[k], x, y);
+        if (x == W - 1) TR = first;  // rightmost top-right: this row's first pixel
+        const int tile = mrow + (max(x, 0) >> P.m_bits);
+        int mode;
+        if (GENERIC)
+          mode = P.m_in_lds ? (int)mode_tab[tile] : (int)((P.m_g[tile] >> 8) & 0xf);
+        else
+          mode = mode_tab[tile];
+        // row 0: black then L; column 0: T
+        mode = y == 0 ? (x == 0 ? 0 : 1) : (x == 0 ? 2 : mode);
+        const uint32_t o = add_pixels(v, predict(mode, h1, T, TL, TR));
+        if (x == 0) first = o;
+        if (lane == kBand - 1 && ok) ring_mine[x & (kRing - 1)] = o;
+        h3 = h2;
+        h2 = h1;
+        h1 = o;
+        const uint32_t f = GENERIC ? post_ops(P, cc_tab, o, x, y) : ops_ct<POST>(P, cc_tab, o, x, y);
+        cout[k] = last ? bgra_to_rgba(f) : f;
+      }
+#pragma unroll
+      for (int k = 0; k < kChunk; ++k) {
+        const int x = c * kChunk + k - 2 * lane;
+        const bool ok = row_ok && x >= 0 && x < W;
+        __builtin_amdgcn_raw_buffer_store_b32(cout[k], out_rs, ok ? y * dst_stride + 4 * x : (int)kDrop, 0, 0);
+      }
+      if (lane == 0)
+        __hip_atomic_store(prog + (b & (kWaves - 1)), ((uint32_t)b << 16) | (uint32_t)min(c * kChunk + kChunk, steps),
+                           __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+#pragma unroll
+      for (int k = 0; k < kChunk; ++k) cin[k] = cnext[k];
+    }
+  }
+  return true;
+}
+
+// VARIANT (chosen per frame on the host, vp8l_variant()): 1..4 = the predictor pass with
+// compile-time ops (CC|PRED|AG, PRED|AG, CC|PRED, PRED) and LDS tables, 0 = generic.
+template <int VARIANT>
 __global__ void __launch_bounds__(1024) vp8l_transforms_kernel(const LLDesc* __restrict__ frames, int* err) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   __shared__ uint32_t prog[kWaves];
@@ -165,7 +317,6 @@ __global__ void __launch_bounds__(1024) vp8l_transforms_kernel(const LLDesc* __r
   uint8_t* mode_tab = lds + kRingBytes;
   uint32_t* cc_tab = reinterpret_cast<uint32_t*>(lds + kRingBytes + kModeTabMax);
   const int W = F.width, H = F.height, n = F.n_stages;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
 
   int i = 0, w_in = F.coded_width;
   const uint32_t* src = F.coded;
@@ -174,146 +325,75 @@ __global__ void __launch_bounds__(1024) vp8l_transforms_kernel(const LLDesc* __r
   while (first_pass || i < n) {
     first_pass = false;
     // ---- plan one pass: [ops] core [ops]
-    PixOp pre[2], post[2];
-    int npre = 0, npost = 0, core = -1;
+    Pass P{};
+    int cc_stage = -1;
     while (i < n && (F.stages[i].type == T_CC || F.stages[i].type == T_AG)) {
-      pre[npre] = PixOp{F.stages[i].type, F.stages[i].bits, F.stages[i].tiles_per_row, i, F.stages[i].data};
-      ++npre;
+      if (F.stages[i].type == T_CC) cc_stage = i;
+      if (P.npre == 0) P.pre0 = F.stages[i].type; else P.pre1 = F.stages[i].type;
+      ++P.npre;
       ++i;
     }
-    if (i < n) core = i++;
+    const int core = i < n ? i++ : -1;
     while (i < n && (F.stages[i].type == T_CC || F.stages[i].type == T_AG)) {
-      post[npost] = PixOp{F.stages[i].type, F.stages[i].bits, F.stages[i].tiles_per_row, i, F.stages[i].data};
-      ++npost;
+      if (F.stages[i].type == T_CC) cc_stage = i;
+      if (P.npost == 0) P.post0 = F.stages[i].type; else P.post1 = F.stages[i].type;
+      ++P.npost;
       ++i;
     }
     const bool last = i >= n;
     const int w_out = core >= 0 ? F.stages[core].xsize : W;
-    // ---- stage tables (one cross-color table at most: the type occurs once)
-    __syncthreads();
-    for (int k = 0; k < npre; ++k)
-      if (pre[k].type == T_CC) pre[k].cc = stage_cc(F.stages[pre[k].idx], cc_tab, H);
-    for (int k = 0; k < npost; ++k)
-      if (post[k].type == T_CC) post[k].cc = stage_cc(F.stages[post[k].idx], cc_tab, H);
     const bool pred = core >= 0 && F.stages[core].type == T_PRED;
-    const uint8_t* modes = nullptr;
-    int mbits = 0, mtpr = 0;
-    const uint32_t* gmodes = nullptr;
+    // ---- stage the cross-color and predictor-mode tables
+    __syncthreads();
+    if (cc_stage >= 0) {
+      const LLStage& st = F.stages[cc_stage];
+      P.cc_bits = st.bits;
+      P.cc_tpr = st.tiles_per_row;
+      P.cc_g = as_global(st.data);
+      const int nt = st.tiles_per_row * ((H + (1 << st.bits) - 1) >> st.bits);
+      P.cc_in_lds = nt <= kCCTabMax;
+      if (P.cc_in_lds)
+        for (int t = threadIdx.x; t < nt; t += blockDim.x) cc_tab[t] = st.data[t];
+    }
     if (pred) {
       const LLStage& ps = F.stages[core];
-      mbits = ps.bits;
-      mtpr = ps.tiles_per_row;
-      const int nt = mtpr * ((H + (1 << mbits) - 1) >> mbits);
-      if (nt <= kModeTabMax) {
+      P.m_bits = ps.bits;
+      P.m_tpr = ps.tiles_per_row;
+      P.m_g = as_global(ps.data);
+      const int nt = P.m_tpr * ((H + (1 << P.m_bits) - 1) >> P.m_bits);
+      P.m_in_lds = nt <= kModeTabMax;
+      if (P.m_in_lds)
         for (int t = threadIdx.x; t < nt; t += blockDim.x) mode_tab[t] = (uint8_t)((ps.data[t] >> 8) & 0xf);
-        modes = mode_tab;
-      } else {
-        gmodes = ps.data;
-      }
     }
     if (threadIdx.x < kWaves) prog[threadIdx.x] = 0;
     __syncthreads();
 
-    const __amdgpu_buffer_rsrc_t in_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(src), 0, src_bytes,
-                                                                           0x00020000);
+    const __amdgpu_buffer_rsrc_t in_rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(src), 0, src_bytes, 0x00020000);
     uint8_t* dst_base = last ? F.rgba : reinterpret_cast<uint8_t*>(F.scratch);
     const int dst_stride = last ? F.rgba_stride : w_out * 4;
     const int dst_bytes = last ? F.rgba_stride * H : F.scratch_bytes;
     const __amdgpu_buffer_rsrc_t out_rs = __builtin_amdgcn_make_buffer_rsrc(dst_base, 0, dst_bytes, 0x00020000);
 
     if (pred) {
-      // ---------------- predictor wavefront
-      const int nbands = (H + kBand - 1) / kBand;
-      const int steps = W + 2 * (kBand - 1);
-      const int nchunks = (steps + kChunk - 1) / kChunk;
-      for (int b = wave; b < nbands; b += kWaves) {
-        const int y = b * kBand + lane;
-        const bool row_ok = y < H;
-        uint32_t* ring_prev = ring + ((b - 1) & (kWaves - 1)) * kRing;  // band b-1's last row
-        uint32_t* ring_mine = ring + (b & (kWaves - 1)) * kRing;
-        // ring slot b&15 was last written by band b-16 and read by band b-15: that reader
-        // must be done before this band overwrites it
-        if (b >= kWaves && !wait_progress(prog + ((b - kWaves + 1) & (kWaves - 1)),
-                                          ((uint32_t)(b - kWaves + 1) << 16) | (uint32_t)steps, err))
-          return;
-        uint32_t h1 = 0, h2 = 0, h3 = 0, first = 0;
-        uint32_t cin[kChunk], cnext[kChunk];
-        auto load_chunk = [&](int c, uint32_t* dstv) {
-#pragma unroll
-          for (int k = 0; k < kChunk; k += 2) {
-            const int x = c * kChunk + k - 2 * lane;
-            const bool ok = row_ok && x >= 0 && x < W;
-            const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(in_rs, ok ? (y * w_in + x) * 4 : (int)kDrop, 0, 0);
-            dstv[k] = v.x;
-            dstv[k + 1] = v.y;
-          }
-        };
-        load_chunk(0, cin);
-        for (int c = 0; c < nchunks; ++c) {
-          if (c + 1 < nchunks) load_chunk(c + 1, cnext);
-          // wait for band b-1 to be 135 steps ahead of this chunk's end; the ring is
-          // not overwritten before band b+1 has consumed it
-          if (b > 0) {
-            const uint32_t need = ((uint32_t)(b - 1) << 16) | (uint32_t)min(c * kChunk + kChunk + 127, steps);
-            if (!wait_progress(prog + ((b - 1) & (kWaves - 1)), need, err)) return;
-          }
-          if (b + 1 < nbands) {
-            const int lag = c * kChunk + kChunk - 2 * (kBand - 1) - kRing + 16;  // oldest column still needed
-            if (lag > 0 &&
-                !wait_progress(prog + ((b + 1) & (kWaves - 1)), ((uint32_t)(b + 1) << 16) | (uint32_t)lag, err))
-              return;
-          }
-          uint32_t cout[kChunk];
-#pragma unroll
-          for (int k = 0; k < kChunk; ++k) {
-            const int s = c * kChunk + k;
-            const int x = s - 2 * lane;
-            const bool ok = row_ok && x >= 0 && x < W;
-            // row above: lane i-1's outputs at steps s-1 (x+1), s-2 (x), s-3 (x-1);
-            // lane 0 reads the previous band's last row from the ring
-            const uint32_t rTR = ring_prev[(x + 1) & (kRing - 1)];
-            const uint32_t rT = ring_prev[x & (kRing - 1)];
-            const uint32_t rTL = ring_prev[(x - 1) & (kRing - 1)];
-            uint32_t TR = shr1(rTR, h1), T = shr1(rT, h2), TL = shr1(rTL, h3);
-            uint32_t v = apply_ops(pre, npre, cin[k], x, y);
-            uint32_t p;
-            if (y == 0) {
-              p = x == 0 ? 0xff000000u : h1;
-            } else if (x == 0) {
-              p = T;
-            } else {
-              if (x == W - 1) TR = first;
-              const int tile = (y >> mbits) * mtpr + (x >> mbits);
-              const int mode = modes ? (int)modes[tile] : (int)((gmodes[tile] >> 8) & 0xf);
-              p = predict(mode, h1, T, TL, TR);
-            }
-            const uint32_t o = add_pixels(v, p);
-            if (x == 0) first = o;
-            if (lane == kBand - 1 && ok) ring_mine[x & (kRing - 1)] = o;
-            h3 = h2;
-            h2 = h1;
-            h1 = o;
-            const uint32_t f = apply_ops(post, npost, o, x, y);
-            cout[k] = last ? bgra_to_rgba(f) : f;
-          }
-#pragma unroll
-          for (int k = 0; k < kChunk; ++k) {
-            const int x = c * kChunk + k - 2 * lane;
-            const bool ok = row_ok && x >= 0 && x < W;
-            __builtin_amdgcn_raw_buffer_store_b32(cout[k], out_rs, ok ? y * dst_stride + 4 * x : (int)kDrop, 0, 0);
-          }
-          if (lane == 0)
-            __hip_atomic_store(prog + (b & (kWaves - 1)), ((uint32_t)b << 16) | (uint32_t)min(c * kChunk + kChunk, steps),
-                               __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-#pragma unroll
-          for (int k = 0; k < kChunk; ++k) cin[k] = cnext[k];
-        }
-      }
+      // ---------------- predictor wavefront: compile-time op variants for the common
+      // transform orders (all tables in LDS), the generic one otherwise
+      bool ok;
+#define WG_PRED(PRE, POST, GEN) \
+  pred_wavefront<PRE, POST, GEN>(P, W, H, w_in, last, in_rs, out_rs, dst_stride, ring, mode_tab, cc_tab, prog, err)
+      if (VARIANT == 1) ok = WG_PRED(1, 2, false);       // CC | PRED | AG (libwebp's usual order)
+      else if (VARIANT == 2) ok = WG_PRED(0, 2, false);  // PRED | AG
+      else if (VARIANT == 3) ok = WG_PRED(1, 0, false);  // CC | PRED
+      else if (VARIANT == 4) ok = WG_PRED(0, 0, false);  // PRED
+      else ok = WG_PRED(0, 0, true);
+#undef WG_PRED
+      if (!ok) return;
     } else {
       // ---------------- per-pixel pass (color indexing or ops only)
       const bool ci = core >= 0;
       const int cbits = ci ? F.stages[core].bits : 0;
-      const uint32_t* pal = ci ? F.stages[core].data : nullptr;
+      const gptr<const uint32_t> pal = as_global(ci ? F.stages[core].data : F.coded);
+      const gptr<const uint32_t> sg = as_global(src);
       const int bpp = 8 >> cbits;
       const int total = w_out * H;
       for (int p = threadIdx.x; p < total; p += blockDim.x) {
@@ -321,14 +401,14 @@ __global__ void __launch_bounds__(1024) vp8l_transforms_kernel(const LLDesc* __r
         uint32_t v;
         if (ci) {
           const int xs = x >> cbits;
-          uint32_t packed = apply_ops(pre, npre, src[y * w_in + xs], xs, y);
+          const uint32_t packed = pre_ops(P, cc_tab, sg[y * w_in + xs], xs, y);
           const int idx = cbits ? (int)(((packed >> 8) >> ((x & ((1 << cbits) - 1)) * bpp)) & ((1u << bpp) - 1))
                                 : (int)((packed >> 8) & 0xff);
           v = pal[idx];
         } else {
-          v = apply_ops(pre, npre, src[y * w_in + x], x, y);
+          v = pre_ops(P, cc_tab, sg[y * w_in + x], x, y);
         }
-        v = apply_ops(post, npost, v, x, y);
+        v = post_ops(P, cc_tab, v, x, y);
         __builtin_amdgcn_raw_buffer_store_b32(last ? bgra_to_rgba(v) : v, out_rs, y * dst_stride + 4 * x, 0, 0);
       }
     }
@@ -343,15 +423,64 @@ __global__ void __launch_bounds__(1024) vp8l_transforms_kernel(const LLDesc* __r
 
 size_t vp8l_lds_bytes() { return kLdsBytes; }
 
-hipError_t launch_vp8l_transforms(const LLDesc* d_frames, int n_frames, int* d_err, hipStream_t stream) {
+int vp8l_variant(const int* types, const int* bits, const int* tiles, int n_stages) {
+  // mirror of the kernel's pass planning for the predictor pass: [ops] PRED [ops]
+  int p = -1;
+  for (int i = 0; i < n_stages; ++i)
+    if (types[i] == T_PRED) p = i;
+  if (p < 0) return 0;
+  int pre = 0, post = 0, npre = 0, npost = 0;
+  bool cc_fits = true;
+  for (int i = p - 1; i >= 0 && (types[i] == T_CC || types[i] == T_AG); --i) {
+    pre = pre * 4 + (types[i] == T_CC ? 1 : 2);  // innermost first
+    ++npre;
+    if (types[i] == T_CC) cc_fits = tiles[i] <= kCCTabMax;
+  }
+  for (int i = p + 1; i < n_stages && (types[i] == T_CC || types[i] == T_AG); ++i) {
+    post = post * 4 + (types[i] == T_CC ? 1 : 2);
+    ++npost;
+    if (types[i] == T_CC) cc_fits = tiles[i] <= kCCTabMax;
+  }
+  if (tiles[p] > kModeTabMax || !cc_fits || npre > 1 || npost > 1) return 0;
+  if (pre == 1 && post == 2) return 1;
+  if (pre == 0 && post == 2) return 2;
+  if (pre == 1 && post == 0) return 3;
+  if (pre == 0 && post == 0) return 4;
+  return 0;
+}
+
+hipError_t launch_vp8l_transforms(const LLDesc* d_frames, const int* group_count, int* d_err, hipStream_t stream) {
   static bool configured = false;
+  auto kern = [](int v) -> const void* {
+    switch (v) {
+      case 1: return reinterpret_cast<const void*>(&vp8l_transforms_kernel<1>);
+      case 2: return reinterpret_cast<const void*>(&vp8l_transforms_kernel<2>);
+      case 3: return reinterpret_cast<const void*>(&vp8l_transforms_kernel<3>);
+      case 4: return reinterpret_cast<const void*>(&vp8l_transforms_kernel<4>);
+      default: return reinterpret_cast<const void*>(&vp8l_transforms_kernel<0>);
+    }
+  };
   if (!configured) {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&vp8l_transforms_kernel),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
-    if (e != hipSuccess) return e;
+    for (int v = 0; v < kVP8LVariants; ++v) {
+      const hipError_t e = hipFuncSetAttribute(kern(v), hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+      if (e != hipSuccess) return e;
+    }
     configured = true;
   }
-  hipLaunchKernelGGL(vp8l_transforms_kernel, dim3(n_frames), dim3(64 * kWaves), kLdsBytes, stream, d_frames, d_err);
+  int start = 0;
+  for (int v = 0; v < kVP8LVariants; ++v) {
+    const int n = group_count[v];
+    if (n <= 0) continue;
+    const LLDesc* f = d_frames + start;
+    switch (v) {
+      case 1: hipLaunchKernelGGL(vp8l_transforms_kernel<1>, dim3(n), dim3(64 * kWaves), kLdsBytes, stream, f, d_err); break;
+      case 2: hipLaunchKernelGGL(vp8l_transforms_kernel<2>, dim3(n), dim3(64 * kWaves), kLdsBytes, stream, f, d_err); break;
+      case 3: hipLaunchKernelGGL(vp8l_transforms_kernel<3>, dim3(n), dim3(64 * kWaves), kLdsBytes, stream, f, d_err); break;
+      case 4: hipLaunchKernelGGL(vp8l_transforms_kernel<4>, dim3(n), dim3(64 * kWaves), kLdsBytes, stream, f, d_err); break;
+      default: hipLaunchKernelGGL(vp8l_transforms_kernel<0>, dim3(n), dim3(64 * kWaves), kLdsBytes, stream, f, d_err);
+    }
+    start += n;
+  }
   return hipGetLastError();
 }
 
