@@ -94,36 +94,21 @@ __device__ __forceinline__ uint32_t predict(int mode, uint32_t L, uint32_t T, ui
   }
 }
 
-// All fourteen predictors by per-lane mode without a divergent switch: the cheap ones
-// (copies, Average2 family, Select) computed for every lane, ClampedAddSubtract{Full,Half}
-// only when some lane of the wave uses them, then a 4-level v_cndmask tree on the mode
-// bits.  Modes 0, 14, 15 -> ARGB black.
-__device__ __forceinline__ uint32_t predict_tree(int mode, uint32_t L, uint32_t T, uint32_t TL, uint32_t TR) {
-  const uint32_t a6 = avg2(L, TL), a9 = avg2(T, TR);
-  uint32_t v[16];
-  v[0] = 0xff000000u;
-  v[1] = L;
-  v[2] = T;
-  v[3] = TR;
-  v[4] = TL;
-  v[5] = avg2(avg2(L, TR), T);
-  v[6] = a6;
-  v[7] = avg2(L, T);
-  v[8] = avg2(TL, T);
-  v[9] = a9;
-  v[10] = avg2(a6, a9);
-  v[11] = select_px(T, L, TL);
-  v[12] = v[13] = 0;
-  if (__any(mode == 12)) v[12] = add_sub_full(L, T, TL);
-  if (__any(mode == 13)) v[13] = add_sub_half(L, T, TL);
-  v[14] = v[15] = 0xff000000u;
-#pragma unroll
-  for (int lvl = 0, w = 16; lvl < 4; ++lvl, w >>= 1) {
-    const bool bit = (mode >> lvl) & 1;
-#pragma unroll
-    for (int k = 0; k < w / 2; ++k) v[k] = bit ? v[2 * k + 1] : v[2 * k];
+// Per-lane predictor with the common modes cheap: ClampedAverage of four (mode 10, most
+// tiles of a natural image) for every lane; the copies 1..4 by a two-level select on the
+// mode bits when some lane uses them; the per-lane switch only for lanes on the remaining
+// modes, skipped when none is.
+__device__ __forceinline__ uint32_t predict_fast(int m, uint32_t L, uint32_t T, uint32_t TL, uint32_t TR) {
+  uint32_t p = avg2(avg2(L, TL), avg2(T, TR));
+  if (__any(m != 10)) {
+    const uint32_t cp = (m & 1) ? ((m & 2) ? TR : L) : ((m & 2) ? T : TL);  // 1 L, 2 T, 3 TR, 4 TL
+    p = (unsigned)(m - 1) < 4u ? cp : p;
+    const bool rest = ((unsigned)(m - 1) >= 4u) & (m != 10);
+    if (__any(rest)) {
+      if (rest) p = predict(m, L, T, TL, TR);
+    }
   }
-  return v[0];
+  return p;
 }
 
 __device__ __forceinline__ int cdelta(int t, int c) {  // ColorTransformDelta on int8 values
@@ -194,33 +179,45 @@ __device__ __forceinline__ uint32_t post_ops(const Pass& P, const uint32_t* cc_l
 }
 
 // Compile-time per-pixel op sequences: 0 none, 1 cross-color, 2 add-green,
-// 3 cross-color then add-green, 4 add-green then cross-color.
+// 3 cross-color then add-green, 4 add-green then cross-color.  ccw: the pixel's
+// cross-color tile word.
 template <int OPS>
-__device__ __forceinline__ uint32_t ops_ct(const Pass& P, const uint32_t* cc_lds, uint32_t v, int x, int y) {
-  auto cc = [&](uint32_t a) {
-    return cross_color_inv(a, cc_lds[(y >> P.cc_bits) * P.cc_tpr + (x >> P.cc_bits)]);
-  };
-  if (OPS == 1) return cc(v);
+__device__ __forceinline__ uint32_t ops_ct(uint32_t v, uint32_t ccw) {
+  if (OPS == 1) return cross_color_inv(v, ccw);
   if (OPS == 2) return add_green(v);
-  if (OPS == 3) return add_green(cc(v));
-  if (OPS == 4) return cc(add_green(v));
+  if (OPS == 3) return add_green(cross_color_inv(v, ccw));
+  if (OPS == 4) return cross_color_inv(add_green(v), ccw);
   return v;
 }
+constexpr bool ops_cc(int ops) { return ops == 1 || ops == 3 || ops == 4; }
 
 // The predictor wavefront of one pass (see the file comment).  GENERIC: ops and tables
 // at run time (tables may be in HBM); otherwise PRE/POST ops are compile-time and both
 // tables are in LDS.  Returns false if a wave gave up waiting.
+//
+// Per 8-step chunk: the row above arrives as ONE DPP per step (lane i-1's previous output
+// = this step's TR; T and TL are the TRs of the two steps before), lane 0's from nine ring
+// columns read once per chunk.  Interior chunks (every lane's columns inside
+// [1, W-2]) carry no edge logic and move pixels with 8-byte loads/stores at immediate
+// offsets; edge chunks predicate per pixel.  The chunk's LDS reads (modes, cross-color
+// words, ring) issue together at its start and are waited on once.  Row 0 / column 0 use fixed modes (L / T,
+// black at the origin), folded into the prefetched modes.
 template <int PRE, int POST, bool GENERIC>
 __device__ __forceinline__ bool pred_wavefront(const Pass& P, int W, int H, int w_in, bool last, __amdgpu_buffer_rsrc_t in_rs,
                                __amdgpu_buffer_rsrc_t out_rs, int dst_stride, uint32_t* ring, const uint8_t* mode_tab,
                                const uint32_t* cc_tab, uint32_t* prog, int* err) {
+  constexpr bool kCC = !GENERIC && (ops_cc(PRE) || ops_cc(POST));
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int nbands = (H + kBand - 1) / kBand;
   const int steps = W + 2 * (kBand - 1);
   const int nchunks = (steps + kChunk - 1) / kChunk;
+  // interior chunks: 8c - 2*63 >= 1 and 8c + 7 <= W - 2
+  const int c_lo = (2 * (kBand - 1) + kChunk) / kChunk, c_hi = (W - 1 - kChunk) / kChunk;
   for (int b = wave; b < nbands; b += kWaves) {
     const int y = b * kBand + lane;
     const bool row_ok = y < H;
+    const bool row0 = y == 0;
+    const int yc = min(y, H - 1);
     const uint32_t* ring_prev = ring + ((b - 1) & (kWaves - 1)) * kRing;  // band b-1's last row
     uint32_t* ring_mine = ring + (b & (kWaves - 1)) * kRing;
     // ring slot b&15 was last written by band b-16 and read by band b-15: that reader
@@ -228,22 +225,59 @@ __device__ __forceinline__ bool pred_wavefront(const Pass& P, int W, int H, int 
     if (b >= kWaves && !wait_progress(prog + ((b - kWaves + 1) & (kWaves - 1)),
                                       ((uint32_t)(b - kWaves + 1) << 16) | (uint32_t)steps, err))
       return false;
-    const int mrow = (y >> P.m_bits) * P.m_tpr;
-    uint32_t h1 = 0, h2 = 0, h3 = 0, first = 0;
-    uint32_t cin[kChunk], cnext[kChunk];
+    const int mrow = (yc >> P.m_bits) * P.m_tpr;
+    const int crow = (yc >> P.cc_bits) * P.cc_tpr;
+    const uint32_t in_row = row_ok ? (uint32_t)(y * w_in * 4) : kDrop;
+    const uint32_t out_row = row_ok ? (uint32_t)(y * dst_stride) : kDrop;
+
     auto load_chunk = [&](int c, uint32_t* dstv) {
+      const int x0 = c * kChunk - 2 * lane;
+      if (c >= c_lo && c <= c_hi) {
 #pragma unroll
-      for (int k = 0; k < kChunk; k += 2) {
-        const int x = c * kChunk + k - 2 * lane;
-        const bool ok = row_ok && x >= 0 && x < W;
-        const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(in_rs, ok ? (y * w_in + x) * 4 : (int)kDrop, 0, 0);
-        dstv[k] = v.x;
-        dstv[k + 1] = v.y;
+        for (int k = 0; k < kChunk; k += 2) {
+          const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(in_rs, in_row + 4 * x0, 4 * k, 0);
+          dstv[k] = v.x;
+          dstv[k + 1] = v.y;
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < kChunk; k += 2) {
+          const int x = x0 + k;
+          const bool ok = x >= 0 && x < W;
+          const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(in_rs, ok ? in_row + 4 * x : kDrop, 0, 0);
+          dstv[k] = v.x;
+          dstv[k + 1] = v.y;
+        }
       }
     };
+    // modes (fixed ones folded in) and cross-color words of chunk c
+    auto fetch_tables = [&](int c, int* md, uint32_t* cw) {
+      const bool edge = !(c >= c_lo && c <= c_hi);
+#pragma unroll
+      for (int k = 0; k < kChunk; ++k) {
+        const int xr = c * kChunk + k - 2 * lane;
+        const int x = edge ? min(max(xr, 0), W - 1) : xr;
+        int m;
+        if (GENERIC && !P.m_in_lds)
+          m = (int)((P.m_g[mrow + (x >> P.m_bits)] >> 8) & 0xf);
+        else
+          m = mode_tab[mrow + (x >> P.m_bits)];
+        if (edge) m = row0 ? (xr == 0 ? 0 : 1) : (xr == 0 ? 2 : m);
+        else if (b == 0) m = row0 ? 1 : m;
+        md[k] = m;
+        if (kCC) cw[k] = cc_tab[crow + (x >> P.cc_bits)];
+      }
+    };
+
+    uint32_t o_prev = 0, t1 = 0, t2 = 0, first = 0;  // L; TR of the last two steps (= T, TL)
+    uint32_t cin[kChunk], cnext[kChunk];
     load_chunk(0, cin);
     for (int c = 0; c < nchunks; ++c) {
+      const bool interior = c >= c_lo && c <= c_hi;
       if (c + 1 < nchunks) load_chunk(c + 1, cnext);
+      uint32_t ccw[kChunk];
+      int md[kChunk];
+      fetch_tables(c, md, ccw);
       // band b-1 must be 135 steps ahead of this chunk's end (its last row, lane 63, then
       // covers column x+1 of lane 0); band b+1 must have consumed the ring columns this
       // chunk overwrites
@@ -257,43 +291,70 @@ __device__ __forceinline__ bool pred_wavefront(const Pass& P, int W, int H, int 
             !wait_progress(prog + ((b + 1) & (kWaves - 1)), ((uint32_t)(b + 1) << 16) | (uint32_t)lag, err))
           return false;
       }
-      uint32_t cout[kChunk];
-#pragma unroll
-      for (int k = 0; k < kChunk; ++k) {
-        const int s = c * kChunk + k;
-        const int x = s - 2 * lane;
-        const bool ok = row_ok && x >= 0 && x < W;
-        // row above: lane i-1's outputs at steps s-1 (x+1), s-2 (x), s-3 (x-1); lane 0
-        // reads the previous band's last row from the ring
-        const uint32_t rTR = ring_prev[(x + 1) & (kRing - 1)];
-        const uint32_t rT = ring_prev[x & (kRing - 1)];
-        const uint32_t rTL = ring_prev[(x - 1) & (kRing - 1)];
-        uint32_t TR = shr1(rTR, h1);
-        const uint32_t T = shr1(rT, h2), TL = shr1(rTL, h3);
-        const uint32_t v = GENERIC ? pre_ops(P, cc_tab, cin[k], x, y) : ops_ct<PRE>(P, cc_tab, cin[k], x, y);
-        if (x == W - 1) TR = first;  // rightmost top-right: this row's first pixel
-        const int tile = mrow + (max(x, 0) >> P.m_bits);
-        int mode;
-        if (GENERIC)
-          mode = P.m_in_lds ? (int)mode_tab[tile] : (int)((P.m_g[tile] >> 8) & 0xf);
-        else
-          mode = mode_tab[tile];
-        // row 0: black then L; column 0: T
-        mode = y == 0 ? (x == 0 ? 0 : 1) : (x == 0 ? 2 : mode);
-        const uint32_t o = add_pixels(v, predict(mode, h1, T, TL, TR));
-        if (x == 0) first = o;
-        if (lane == kBand - 1 && ok) ring_mine[x & (kRing - 1)] = o;
-        h3 = h2;
-        h2 = h1;
-        h1 = o;
-        const uint32_t f = GENERIC ? post_ops(P, cc_tab, o, x, y) : ops_ct<POST>(P, cc_tab, o, x, y);
-        cout[k] = last ? bgra_to_rgba(f) : f;
+      // lane 0's row above: columns 8c .. 8c+8 of band b-1's last row
+      uint32_t r[kChunk + 1];
+      {
+        const int base = (c * kChunk) & (kRing - 1);
+        const uint4 r0 = *reinterpret_cast<const uint4*>(ring_prev + base);
+        const uint4 r1 = *reinterpret_cast<const uint4*>(ring_prev + base + 4);
+        r[0] = r0.x; r[1] = r0.y; r[2] = r0.z; r[3] = r0.w;
+        r[4] = r1.x; r[5] = r1.y; r[6] = r1.z; r[7] = r1.w;
+        r[8] = ring_prev[(c * kChunk + kChunk) & (kRing - 1)];
       }
+      if (c == 0) t1 = r[0];
+      uint32_t ov[kChunk];
 #pragma unroll
       for (int k = 0; k < kChunk; ++k) {
         const int x = c * kChunk + k - 2 * lane;
-        const bool ok = row_ok && x >= 0 && x < W;
-        __builtin_amdgcn_raw_buffer_store_b32(cout[k], out_rs, ok ? y * dst_stride + 4 * x : (int)kDrop, 0, 0);
+        const uint32_t tr = shr1(r[k + 1], o_prev);
+        const uint32_t TR = (!interior && x == W - 1) ? first : tr;  // rightmost: this row's first pixel
+        // (generic: tables may be in HBM, so the column is clamped into the frame)
+        const uint32_t v =
+            GENERIC ? pre_ops(P, cc_tab, cin[k], min(max(x, 0), W - 1), yc) : ops_ct<PRE>(cin[k], ccw[k]);
+        const uint32_t o = add_pixels(v, predict_fast(md[k], o_prev, t1, t2, TR));
+        if (!interior && x == 0) first = o;
+        t2 = t1;
+        t1 = tr;
+        o_prev = o;
+        ov[k] = o;
+      }
+      // band b's last row into the ring (lane 63), then the chunk's outputs
+      if (interior) {
+        if (lane == kBand - 1) {
+#pragma unroll
+          for (int k = 0; k < kChunk; k += 2)
+            *reinterpret_cast<uint2*>(ring_mine + ((c * kChunk + k - 2 * lane) & (kRing - 1))) = make_uint2(ov[k], ov[k + 1]);
+        }
+        const uint32_t off = out_row + 4 * (c * kChunk - 2 * lane);
+#pragma unroll
+        for (int k = 0; k < kChunk; k += 2) {
+          uint32_t f0, f1;
+          if (GENERIC) {
+            f0 = post_ops(P, cc_tab, ov[k], c * kChunk + k - 2 * lane, yc);
+            f1 = post_ops(P, cc_tab, ov[k + 1], c * kChunk + k + 1 - 2 * lane, yc);
+          } else {
+            f0 = ops_ct<POST>(ov[k], ccw[k]);
+            f1 = ops_ct<POST>(ov[k + 1], ccw[k + 1]);
+          }
+          if (last) {
+            f0 = bgra_to_rgba(f0);
+            f1 = bgra_to_rgba(f1);
+          }
+          u32x2 pair;
+          pair.x = f0;
+          pair.y = f1;
+          __builtin_amdgcn_raw_buffer_store_b64(pair, out_rs, off, 4 * k, 0);
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < kChunk; ++k) {
+          const int x = c * kChunk + k - 2 * lane;
+          const bool ok = row_ok && x >= 0 && x < W;
+          if (lane == kBand - 1 && ok) ring_mine[x & (kRing - 1)] = ov[k];
+          uint32_t f = GENERIC ? post_ops(P, cc_tab, ov[k], min(max(x, 0), W - 1), yc) : ops_ct<POST>(ov[k], ccw[k]);
+          if (last) f = bgra_to_rgba(f);
+          __builtin_amdgcn_raw_buffer_store_b32(f, out_rs, ok ? out_row + 4 * x : kDrop, 0, 0);
+        }
       }
       if (lane == 0)
         __hip_atomic_store(prog + (b & (kWaves - 1)), ((uint32_t)b << 16) | (uint32_t)min(c * kChunk + kChunk, steps),
