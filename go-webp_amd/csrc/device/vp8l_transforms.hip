@@ -39,11 +39,41 @@ constexpr int kRing = 512;  // columns per inter-band ring slot (power of two)
 constexpr int kRingBytes = kWaves * kRing * 4;
 constexpr int kModeTabMax = 16384;  // predictor tiles staged in LDS (1 byte each)
 constexpr int kCCTabMax = 4096;     // cross-color tiles staged in LDS (4 bytes each)
-constexpr int kLdsBytes = kRingBytes + kModeTabMax + kCCTabMax * 4;
+// Per-wave staging slot: the band's 64 rows x 16 columns of one group (two chunks), row
+// stride padded to 80 B so the row-per-lane b128 accesses are bank-conflict free.
+constexpr int kGroup = 2 * kChunk;
+constexpr int kSlotStride = 4 * kGroup + 16;
+constexpr int kSlotBytes = kBand * kSlotStride;
+constexpr int kLdsBytes = kRingBytes + kModeTabMax + kCCTabMax * 4 + kWaves * kSlotBytes;
 constexpr uint32_t kDrop = 0x80000000u;
 constexpr int T_PRED = 0, T_CC = 1, T_AG = 2;  // 3 = color indexing
 
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t uint32x4_t __attribute__((ext_vector_type(4)));
+
+// Opt-in per-section cycle accounting (make VARIANT=timing, read back by
+// scripts/k3_sections.py): s_memtime deltas summed per chunk section in registers,
+// flushed with one atomic per section per wave.  Measurement only.
+[[maybe_unused]] constexpr int kK3Sections = 8;
+#ifdef WG_K3_SECTION_TIMING
+__device__ unsigned long long g_k3_sections[kK3Sections];
+#define K3_SECT_DECL() uint64_t sect_acc[kK3Sections] = {}, sect_t = __builtin_amdgcn_s_memtime()
+#define K3_SECT(id)                                       \
+  do {                                                    \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime();     \
+    sect_acc[id] += t_ - sect_t;                          \
+    sect_t = t_;                                          \
+  } while (0)
+#define K3_SECT_FLUSH()                                                                   \
+  do {                                                                                    \
+    if ((threadIdx.x & 63) == 0)                                                          \
+      for (int s_ = 0; s_ < kK3Sections; ++s_) atomicAdd(&g_k3_sections[s_], sect_acc[s_]); \
+  } while (0)
+#else
+#define K3_SECT_DECL() (void)0
+#define K3_SECT(id) (void)0
+#define K3_SECT_FLUSH() (void)0
+#endif
 
 __device__ __forceinline__ uint32_t add_pixels(uint32_t a, uint32_t b) {
   return (((a & 0xff00ff00u) + (b & 0xff00ff00u)) & 0xff00ff00u) |
@@ -141,7 +171,7 @@ __device__ __forceinline__ bool wait_progress(uint32_t* pr, uint32_t need, int* 
   while (__hip_atomic_load(pr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
     __builtin_amdgcn_s_sleep(1);
     if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {
-      atomicOr(err, 2);
+      __hip_atomic_fetch_or(as_global(err), 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return false;
     }
   }
@@ -197,25 +227,38 @@ constexpr bool ops_cc(int ops) { return ops == 1 || ops == 3 || ops == 4; }
 //
 // Per 8-step chunk: the row above arrives as ONE DPP per step (lane i-1's previous output
 // = this step's TR; T and TL are the TRs of the two steps before), lane 0's from nine ring
-// columns read once per chunk.  Interior chunks (every lane's columns inside
-// [1, W-2]) carry no edge logic and move pixels with 8-byte loads/stores at immediate
-// offsets; edge chunks predicate per pixel.  The chunk's LDS reads (modes, cross-color
-// words, ring) issue together at its start and are waited on once.  Row 0 / column 0 use fixed modes (L / T,
-// black at the origin), folded into the prefetched modes.
+// columns read once per chunk.  Interior chunks (every lane's columns inside [1, W-2])
+// carry no edge logic.  The chunk's LDS reads (inputs, modes, cross-color words, ring)
+// issue together at its start and are waited on once.  Row 0 / column 0 use fixed modes
+// (L / T, black at the origin), folded into the fetched modes.
+//
+// HBM traffic goes through the wave's staging slot, one group (two chunks, 16 columns
+// of the band's skewed rows) at a time: row-wise 16-byte loads/stores with four lanes per
+// row segment (16 rows per instruction), so an instruction touches ~24 cache lines
+// instead of 64 and every 64-byte row segment moves in one request.  The steps read
+// and overwrite the slot transposed (lane = row).  Inputs of group g+1 are in flight in
+// registers while group g computes.
 template <int PRE, int POST, bool GENERIC>
 __device__ __forceinline__ bool pred_wavefront(const Pass& P, int W, int H, int w_in, bool last, __amdgpu_buffer_rsrc_t in_rs,
                                __amdgpu_buffer_rsrc_t out_rs, int dst_stride, uint32_t* ring, const uint8_t* mode_tab,
-                               const uint32_t* cc_tab, uint32_t* prog, int* err) {
+                               const uint32_t* cc_tab, uint8_t* slots, uint32_t* prog, int* err) {
   constexpr bool kCC = !GENERIC && (ops_cc(PRE) || ops_cc(POST));
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int nbands = (H + kBand - 1) / kBand;
   const int steps = W + 2 * (kBand - 1);
-  const int nchunks = (steps + kChunk - 1) / kChunk;
+  const int ngroups = (steps + kGroup - 1) / kGroup;
   // interior chunks: 8c - 2*63 >= 1 and 8c + 7 <= W - 2
   const int c_lo = (2 * (kBand - 1) + kChunk) / kChunk, c_hi = (W - 1 - kChunk) / kChunk;
+  // groups whose columns all lie in [0, W-1]: 16g - 126 >= 0 and 16g + 15 <= W - 1
+  const int g_lo = (2 * (kBand - 1) + kGroup - 1) / kGroup, g_hi = (W - kGroup) / kGroup;
+  uint8_t* slot = slots + wave * kSlotBytes;
+  // row-wise I/O mapping: lane -> rows io_r + 16q (q = 0..3), 16-byte quad io_p
+  const int io_r = lane >> 2, io_p = lane & 3;
+  uint8_t* io_lds = slot + io_r * kSlotStride + 16 * io_p;
+  uint8_t* my_lds = slot + lane * kSlotStride;
+  K3_SECT_DECL();
   for (int b = wave; b < nbands; b += kWaves) {
     const int y = b * kBand + lane;
-    const bool row_ok = y < H;
     const bool row0 = y == 0;
     const int yc = min(y, H - 1);
     const uint32_t* ring_prev = ring + ((b - 1) & (kWaves - 1)) * kRing;  // band b-1's last row
@@ -225,59 +268,92 @@ __device__ __forceinline__ bool pred_wavefront(const Pass& P, int W, int H, int 
     if (b >= kWaves && !wait_progress(prog + ((b - kWaves + 1) & (kWaves - 1)),
                                       ((uint32_t)(b - kWaves + 1) << 16) | (uint32_t)steps, err))
       return false;
+    K3_SECT(6);
     const int mrow = (yc >> P.m_bits) * P.m_tpr;
     const int crow = (yc >> P.cc_bits) * P.cc_tpr;
-    const uint32_t in_row = row_ok ? (uint32_t)(y * w_in * 4) : kDrop;
-    const uint32_t out_row = row_ok ? (uint32_t)(y * dst_stride) : kDrop;
+    // byte offsets of the I/O lane's quad in group 0 for q = 0 (row io_r, column
+    // -2*io_r + 4*io_p); +64 per group, +q*(16 rows - 32 columns) per q.  Rows past the
+    // frame get kDrop.  Columns left of the frame read the previous row (ignored) or, in
+    // row 0, wrap to an out-of-range offset (reads 0).
+    const int rows_left = H - b * kBand;
+    const uint32_t in_q = 16u * (uint32_t)w_in * 4u - 128u, out_q = 16u * (uint32_t)dst_stride - 128u;
+    const uint32_t in_base = (uint32_t)((b * kBand + io_r) * w_in * 4) + 16u * io_p - 8u * io_r;
+    const uint32_t out_base = (uint32_t)((b * kBand + io_r) * dst_stride) + 16u * io_p - 8u * io_r;
+    const int x_io = 4 * io_p - 2 * io_r;  // column of the quad (group 0, q = 0)
 
-    auto load_chunk = [&](int c, uint32_t* dstv) {
-      const int x0 = c * kChunk - 2 * lane;
-      if (c >= c_lo && c <= c_hi) {
+    uint32x4_t R[4];  // the next group's inputs, in flight
+    auto load_group = [&](int g) {
 #pragma unroll
-        for (int k = 0; k < kChunk; k += 2) {
-          const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(in_rs, in_row + 4 * x0, 4 * k, 0);
-          dstv[k] = v.x;
-          dstv[k + 1] = v.y;
-        }
-      } else {
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t off = io_r + 16 * q < rows_left ? in_base + q * in_q + 64u * g : kDrop;
+        R[q] = __builtin_amdgcn_raw_buffer_load_b128(in_rs, off, 0, 0);
+      }
+    };
+    auto stage_group = [&]() {
 #pragma unroll
-        for (int k = 0; k < kChunk; k += 2) {
-          const int x = x0 + k;
-          const bool ok = x >= 0 && x < W;
-          const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(in_rs, ok ? in_row + 4 * x : kDrop, 0, 0);
-          dstv[k] = v.x;
-          dstv[k + 1] = v.y;
+      for (int q = 0; q < 4; ++q) *reinterpret_cast<uint32x4_t*>(io_lds + 16 * q * kSlotStride) = R[q];
+    };
+    auto emit_group = [&](int g) {
+      uint32x4_t S[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) S[q] = *reinterpret_cast<const uint32x4_t*>(io_lds + 16 * q * kSlotStride);
+      // full quads with one 16-byte store each (always issued, so the wait before the
+      // next staging keeps them in flight); edge groups add per-pixel stores for the
+      // quads that straddle a frame edge
+      const bool inner = g >= g_lo && g <= g_hi;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int x = x_io + kGroup * g - 32 * q;
+        const bool full = io_r + 16 * q < rows_left && (inner || (x >= 0 && x + 3 < W));
+        __builtin_amdgcn_raw_buffer_store_b128(S[q], out_rs, full ? out_base + q * out_q + 64u * g : kDrop, 0, 0);
+      }
+      if (!inner) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int x = x_io + kGroup * g - 32 * q;
+          const bool part = io_r + 16 * q < rows_left && !(x >= 0 && x + 3 < W);
+          const uint32_t off = out_base + q * out_q + 64u * g;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const bool ok = part && x + j >= 0 && x + j < W;
+            __builtin_amdgcn_raw_buffer_store_b32(S[q][j], out_rs, ok ? off + 4 * j : kDrop, 0, 0);
+          }
         }
       }
     };
-    // modes (fixed ones folded in) and cross-color words of chunk c
+    // modes and cross-color words of chunk c: all reads issued back to back (column
+    // clamped into the frame), the fixed modes of row 0 / column 0 applied afterwards
     auto fetch_tables = [&](int c, int* md, uint32_t* cw) {
-      const bool edge = !(c >= c_lo && c <= c_hi);
 #pragma unroll
       for (int k = 0; k < kChunk; ++k) {
-        const int xr = c * kChunk + k - 2 * lane;
-        const int x = edge ? min(max(xr, 0), W - 1) : xr;
-        int m;
+        const int x = min(max(c * kChunk + k - 2 * lane, 0), W - 1);
         if (GENERIC && !P.m_in_lds)
-          m = (int)((P.m_g[mrow + (x >> P.m_bits)] >> 8) & 0xf);
+          md[k] = (int)((P.m_g[mrow + (x >> P.m_bits)] >> 8) & 0xf);
         else
-          m = mode_tab[mrow + (x >> P.m_bits)];
-        if (edge) m = row0 ? (xr == 0 ? 0 : 1) : (xr == 0 ? 2 : m);
-        else if (b == 0) m = row0 ? 1 : m;
-        md[k] = m;
+          md[k] = mode_tab[mrow + (x >> P.m_bits)];
         if (kCC) cw[k] = cc_tab[crow + (x >> P.cc_bits)];
+      }
+    };
+    auto fix_modes = [&](int c, int* md) {
+      if (!(c >= c_lo && c <= c_hi) || b == 0) {
+#pragma unroll
+        for (int k = 0; k < kChunk; ++k) {
+          const int xr = c * kChunk + k - 2 * lane;
+          md[k] = row0 ? (xr == 0 ? 0 : 1) : (xr == 0 ? 2 : md[k]);
+        }
       }
     };
 
     uint32_t o_prev = 0, t1 = 0, t2 = 0, first = 0;  // L; TR of the last two steps (= T, TL)
-    uint32_t cin[kChunk], cnext[kChunk];
-    load_chunk(0, cin);
-    for (int c = 0; c < nchunks; ++c) {
+    // one chunk (cl = 0/1 within its group): inputs from the slot, outputs back to it
+    auto chunk = [&](const int c, const int cl) -> bool {
       const bool interior = c >= c_lo && c <= c_hi;
-      if (c + 1 < nchunks) load_chunk(c + 1, cnext);
+      const uint32x4_t in0 = *reinterpret_cast<const uint32x4_t*>(my_lds + 32 * cl);
+      const uint32x4_t in1 = *reinterpret_cast<const uint32x4_t*>(my_lds + 32 * cl + 16);
       uint32_t ccw[kChunk];
       int md[kChunk];
       fetch_tables(c, md, ccw);
+      K3_SECT(0);
       // band b-1 must be 135 steps ahead of this chunk's end (its last row, lane 63, then
       // covers column x+1 of lane 0); band b+1 must have consumed the ring columns this
       // chunk overwrites
@@ -285,12 +361,15 @@ __device__ __forceinline__ bool pred_wavefront(const Pass& P, int W, int H, int 
         const uint32_t need = ((uint32_t)(b - 1) << 16) | (uint32_t)min(c * kChunk + kChunk + 127, steps);
         if (!wait_progress(prog + ((b - 1) & (kWaves - 1)), need, err)) return false;
       }
+      K3_SECT(1);
       if (b + 1 < nbands) {
         const int lag = c * kChunk + kChunk - 2 * (kBand - 1) - kRing + 16;  // oldest column still needed
         if (lag > 0 &&
             !wait_progress(prog + ((b + 1) & (kWaves - 1)), ((uint32_t)(b + 1) << 16) | (uint32_t)lag, err))
           return false;
       }
+      K3_SECT(2);
+      fix_modes(c, md);
       // lane 0's row above: columns 8c .. 8c+8 of band b-1's last row
       uint32_t r[kChunk + 1];
       {
@@ -302,6 +381,8 @@ __device__ __forceinline__ bool pred_wavefront(const Pass& P, int W, int H, int 
         r[8] = ring_prev[(c * kChunk + kChunk) & (kRing - 1)];
       }
       if (c == 0) t1 = r[0];
+      const uint32_t cin[kChunk] = {in0[0], in0[1], in0[2], in0[3], in1[0], in1[1], in1[2], in1[3]};
+      K3_SECT(3);
       uint32_t ov[kChunk];
 #pragma unroll
       for (int k = 0; k < kChunk; ++k) {
@@ -318,51 +399,50 @@ __device__ __forceinline__ bool pred_wavefront(const Pass& P, int W, int H, int 
         o_prev = o;
         ov[k] = o;
       }
-      // band b's last row into the ring (lane 63), then the chunk's outputs
-      if (interior) {
-        if (lane == kBand - 1) {
+      K3_SECT(4);
+      // band b's last row into the ring (lane 63)
+      if (lane == kBand - 1) {
+        if (interior) {
 #pragma unroll
           for (int k = 0; k < kChunk; k += 2)
             *reinterpret_cast<uint2*>(ring_mine + ((c * kChunk + k - 2 * lane) & (kRing - 1))) = make_uint2(ov[k], ov[k + 1]);
-        }
-        const uint32_t off = out_row + 4 * (c * kChunk - 2 * lane);
+        } else {
 #pragma unroll
-        for (int k = 0; k < kChunk; k += 2) {
-          uint32_t f0, f1;
-          if (GENERIC) {
-            f0 = post_ops(P, cc_tab, ov[k], c * kChunk + k - 2 * lane, yc);
-            f1 = post_ops(P, cc_tab, ov[k + 1], c * kChunk + k + 1 - 2 * lane, yc);
-          } else {
-            f0 = ops_ct<POST>(ov[k], ccw[k]);
-            f1 = ops_ct<POST>(ov[k + 1], ccw[k + 1]);
+          for (int k = 0; k < kChunk; ++k) {
+            const int x = c * kChunk + k - 2 * lane;
+            if (x >= 0 && x < W) ring_mine[x & (kRing - 1)] = ov[k];
           }
-          if (last) {
-            f0 = bgra_to_rgba(f0);
-            f1 = bgra_to_rgba(f1);
-          }
-          u32x2 pair;
-          pair.x = f0;
-          pair.y = f1;
-          __builtin_amdgcn_raw_buffer_store_b64(pair, out_rs, off, 4 * k, 0);
-        }
-      } else {
-#pragma unroll
-        for (int k = 0; k < kChunk; ++k) {
-          const int x = c * kChunk + k - 2 * lane;
-          const bool ok = row_ok && x >= 0 && x < W;
-          if (lane == kBand - 1 && ok) ring_mine[x & (kRing - 1)] = ov[k];
-          uint32_t f = GENERIC ? post_ops(P, cc_tab, ov[k], min(max(x, 0), W - 1), yc) : ops_ct<POST>(ov[k], ccw[k]);
-          if (last) f = bgra_to_rgba(f);
-          __builtin_amdgcn_raw_buffer_store_b32(f, out_rs, ok ? out_row + 4 * x : kDrop, 0, 0);
         }
       }
+      // the chunk's outputs (post ops, RGBA on the last pass) over its inputs in the slot
+      uint32_t f[kChunk];
+#pragma unroll
+      for (int k = 0; k < kChunk; ++k) {
+        f[k] = GENERIC ? post_ops(P, cc_tab, ov[k], min(max(c * kChunk + k - 2 * lane, 0), W - 1), yc)
+                       : ops_ct<POST>(ov[k], ccw[k]);
+        if (last) f[k] = bgra_to_rgba(f[k]);
+      }
+      *reinterpret_cast<uint32x4_t*>(my_lds + 32 * cl) = uint32x4_t{f[0], f[1], f[2], f[3]};
+      *reinterpret_cast<uint32x4_t*>(my_lds + 32 * cl + 16) = uint32x4_t{f[4], f[5], f[6], f[7]};
       if (lane == 0)
         __hip_atomic_store(prog + (b & (kWaves - 1)), ((uint32_t)b << 16) | (uint32_t)min(c * kChunk + kChunk, steps),
                            __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-#pragma unroll
-      for (int k = 0; k < kChunk; ++k) cin[k] = cnext[k];
+      K3_SECT(5);
+      return true;
+    };
+    load_group(0);
+    stage_group();
+    load_group(1);
+    for (int g = 0; g < ngroups; ++g) {
+      if (!chunk(2 * g, 0)) return false;
+      if (!chunk(2 * g + 1, 1)) return false;
+      emit_group(g);
+      stage_group();     // group g+1's inputs (in flight since group g started)
+      load_group(g + 2);  // past the end: all out of range, reads 0
+      K3_SECT(7);
     }
   }
+  K3_SECT_FLUSH();
   return true;
 }
 
@@ -377,6 +457,7 @@ __global__ void __launch_bounds__(1024) vp8l_transforms_kernel(const LLDesc* __r
   uint32_t* ring = reinterpret_cast<uint32_t*>(lds);
   uint8_t* mode_tab = lds + kRingBytes;
   uint32_t* cc_tab = reinterpret_cast<uint32_t*>(lds + kRingBytes + kModeTabMax);
+  uint8_t* slots = lds + kRingBytes + kModeTabMax + kCCTabMax * 4;
   const int W = F.width, H = F.height, n = F.n_stages;
 
   int i = 0, w_in = F.coded_width;
@@ -414,7 +495,7 @@ __global__ void __launch_bounds__(1024) vp8l_transforms_kernel(const LLDesc* __r
       const int nt = st.tiles_per_row * ((H + (1 << st.bits) - 1) >> st.bits);
       P.cc_in_lds = nt <= kCCTabMax;
       if (P.cc_in_lds)
-        for (int t = threadIdx.x; t < nt; t += blockDim.x) cc_tab[t] = st.data[t];
+        for (int t = threadIdx.x; t < nt; t += blockDim.x) cc_tab[t] = P.cc_g[t];
     }
     if (pred) {
       const LLStage& ps = F.stages[core];
@@ -424,7 +505,7 @@ __global__ void __launch_bounds__(1024) vp8l_transforms_kernel(const LLDesc* __r
       const int nt = P.m_tpr * ((H + (1 << P.m_bits) - 1) >> P.m_bits);
       P.m_in_lds = nt <= kModeTabMax;
       if (P.m_in_lds)
-        for (int t = threadIdx.x; t < nt; t += blockDim.x) mode_tab[t] = (uint8_t)((ps.data[t] >> 8) & 0xf);
+        for (int t = threadIdx.x; t < nt; t += blockDim.x) mode_tab[t] = (uint8_t)((P.m_g[t] >> 8) & 0xf);
     }
     if (threadIdx.x < kWaves) prog[threadIdx.x] = 0;
     __syncthreads();
@@ -441,7 +522,7 @@ __global__ void __launch_bounds__(1024) vp8l_transforms_kernel(const LLDesc* __r
       // transform orders (all tables in LDS), the generic one otherwise
       bool ok;
 #define WG_PRED(PRE, POST, GEN) \
-  pred_wavefront<PRE, POST, GEN>(P, W, H, w_in, last, in_rs, out_rs, dst_stride, ring, mode_tab, cc_tab, prog, err)
+  pred_wavefront<PRE, POST, GEN>(P, W, H, w_in, last, in_rs, out_rs, dst_stride, ring, mode_tab, cc_tab, slots, prog, err)
       if (VARIANT == 1) ok = WG_PRED(1, 2, false);       // CC | PRED | AG (libwebp's usual order)
       else if (VARIANT == 2) ok = WG_PRED(0, 2, false);  // PRED | AG
       else if (VARIANT == 3) ok = WG_PRED(1, 0, false);  // CC | PRED
@@ -483,6 +564,18 @@ __global__ void __launch_bounds__(1024) vp8l_transforms_kernel(const LLDesc* __r
 }  // namespace
 
 size_t vp8l_lds_bytes() { return kLdsBytes; }
+
+#ifdef WG_K3_SECTION_TIMING
+extern "C" int wg_debug_k3_sections(unsigned long long* out, int n, int reset) {
+  if (n > kK3Sections) n = kK3Sections;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_k3_sections), n * sizeof(unsigned long long)) != hipSuccess) return -1;
+  if (reset) {
+    unsigned long long z[kK3Sections] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_k3_sections), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return n;
+}
+#endif
 
 int vp8l_variant(const int* types, const int* bits, const int* tiles, int n_stages) {
   // mirror of the kernel's pass planning for the predictor pass: [ops] PRED [ops]

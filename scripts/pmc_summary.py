@@ -11,7 +11,7 @@ for d in sys.argv[1:]:
         for r in csv.DictReader(open(f)):
             if r["Kernel_Name"].startswith("__amd"):
                 continue
-            k = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("(anonymous namespace)::", "")
+            k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
             acc[(k, r["Counter_Name"], r["VGPR_Count"], r["Grid_Size"])].append(float(r["Counter_Value"]))
     for (k, c, vg, gs), v in sorted(acc.items()):
         print(f"{k:48s} vgpr={vg:4s} grid={gs:10s} {c:22s} n={len(v):2d} avg={sum(v) / len(v):.6g}")
