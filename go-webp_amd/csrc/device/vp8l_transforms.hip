@@ -54,7 +54,7 @@ typedef uint32_t uint32x4_t __attribute__((ext_vector_type(4)));
 // Opt-in per-section cycle accounting (make VARIANT=timing, read back by
 // scripts/k3_sections.py): s_memtime deltas summed per chunk section in registers,
 // flushed with one atomic per section per wave.  Measurement only.
-[[maybe_unused]] constexpr int kK3Sections = 8;
+[[maybe_unused]] constexpr int kK3Sections = 10;
 #ifdef WG_K3_SECTION_TIMING
 __device__ unsigned long long g_k3_sections[kK3Sections];
 #define K3_SECT_DECL() uint64_t sect_acc[kK3Sections] = {}, sect_t = __builtin_amdgcn_s_memtime()
@@ -75,11 +75,17 @@ __device__ unsigned long long g_k3_sections[kK3Sections];
 #define K3_SECT_FLUSH() (void)0
 #endif
 
+// Per-byte a + b mod 256: add the low 7 bits of every byte (no carry can leave a byte),
+// then set each top bit to the xor of the operands' top bits and the carry into it; the
+// masked xor is one v_bitop3 (truth table 0x28 = (S0 ^ S1) & S2).
 __device__ __forceinline__ uint32_t add_pixels(uint32_t a, uint32_t b) {
-  return (((a & 0xff00ff00u) + (b & 0xff00ff00u)) & 0xff00ff00u) |
-         (((a & 0x00ff00ffu) + (b & 0x00ff00ffu)) & 0x00ff00ffu);
+  return ((a & 0x7f7f7f7fu) + (b & 0x7f7f7f7fu)) ^ (uint32_t)__builtin_amdgcn_bitop3_b32(a, b, 0x80808080u, 0x28);
 }
-__device__ __forceinline__ uint32_t avg2(uint32_t a, uint32_t b) { return (((a ^ b) & 0xfefefefeu) >> 1) + (a & b); }
+// Per-byte floor((a + b) / 2): (a & b) + ((a ^ b) & 0xfe..) / 2, the masked xor as one
+// v_bitop3 (truth table 0x28 = (S0 ^ S1) & S2).
+__device__ __forceinline__ uint32_t avg2(uint32_t a, uint32_t b) {
+  return ((uint32_t)__builtin_amdgcn_bitop3_b32(a, b, 0xfefefefeu, 0x28) >> 1) + (a & b);
+}
 __device__ __forceinline__ int clamp255(int v) { return min(max(v, 0), 255); }
 __device__ __forceinline__ int chan(uint32_t v, int s) { return (int)((v >> s) & 0xff); }
 
@@ -437,9 +443,11 @@ __device__ __forceinline__ bool pred_wavefront(const Pass& P, int W, int H, int 
       if (!chunk(2 * g, 0)) return false;
       if (!chunk(2 * g + 1, 1)) return false;
       emit_group(g);
-      stage_group();     // group g+1's inputs (in flight since group g started)
-      load_group(g + 2);  // past the end: all out of range, reads 0
       K3_SECT(7);
+      stage_group();     // group g+1's inputs (in flight since group g started)
+      K3_SECT(8);
+      load_group(g + 2);  // past the end: all out of range, reads 0
+      K3_SECT(9);
     }
   }
   K3_SECT_FLUSH();

@@ -15,7 +15,7 @@ os.environ["WG_LIB_VARIANT"] = "timing"
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "go-webp_amd"), os.path.join(ROOT, "tests")]
 
-NAMES = ["issue", "wait-prev", "wait-next", "ring", "steps", "emit", "band-start", "spare"]
+NAMES = ["issue", "wait-prev", "wait-next", "ring", "steps", "slot-out", "band-start", "emit", "stage", "load"]
 
 
 def main():

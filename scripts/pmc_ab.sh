@@ -6,7 +6,8 @@ for v in "$@"; do
   TAG=ab_$v WL=c5 STEPS=2 \
     PMC1="SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES" \
     PMC2="SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_BRANCH SQ_BUSY_CYCLES" \
-    PMC3="SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_RD" \
+    PMC3="TA_TA_BUSY TA_ADDR_STALLED_BY_TC_CYCLES SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_WR" \
+    PMC4="TCP_PENDING_STALL_CYCLES SQ_VMEM_TA_CMD_FIFO_FULL" \
     bash scripts/profile.sh > gpurun_out/pmc_ab_$v.log 2>&1 || { echo "STOP $v"; tail -5 gpurun_out/pmc_ab_$v.log; exit 1; }
-  echo "== $v"; python3 scripts/pmc_summary.py gpurun_out/prof_ab_$v | grep vp8l
+  echo "== $v"; python3 scripts/pmc_summary.py gpurun_out/prof_ab_$v | grep "vp8l" | awk '{print $4, $7}'
 done

@@ -15,9 +15,11 @@ run() {  # run <name> <timeout> <rocprofv3 args...>
   echo "=== $name rc=$rc"; tail -n 3 $OUT/$name.log
   if [ $rc -ne 0 ]; then exit $rc; fi
 }
-run trace 600 --kernel-trace --stats
-if [ -n "$PMC1" ]; then run pmc1 600 --pmc $PMC1; fi
-if [ -n "$PMC2" ]; then run pmc2 600 --pmc $PMC2; fi
-if [ -n "$PMC3" ]; then run pmc3 600 --pmc $PMC3; fi
-if [ -n "$PMC4" ]; then run pmc4 600 --pmc $PMC4; fi
+run trace 240 --kernel-trace --stats
+if [ -n "$PMC1" ]; then run pmc1 240 --pmc $PMC1; fi
+if [ -n "$PMC2" ]; then run pmc2 240 --pmc $PMC2; fi
+if [ -n "$PMC3" ]; then run pmc3 240 --pmc $PMC3; fi
+if [ -n "$PMC4" ]; then run pmc4 240 --pmc $PMC4; fi
+if [ -n "$PMC5" ]; then run pmc5 240 --pmc $PMC5; fi
+if [ -n "$PMC6" ]; then run pmc6 240 --pmc $PMC6; fi
 find $OUT -name "*.csv" | head -50
