@@ -33,7 +33,7 @@ WORKLOADS = {
     "c5": dict(prefix="c5_ll2048", name="c5_ll2048_x256",
                desc="2048x2048 VP8L lossless (predictor + cross-color + subtract-green + color cache), batch 256"),
 }
-KERNELS = ("vp8_recon_filter_kernel", "yuv_to_rgba_kernel", "vp8l_transforms_kernel")
+KERNELS = ("vp8_recon_filter_kernel", "yuv_to_rgba_kernel", "vp8l_transforms_kernel", "alpha_kernel")
 
 
 def _load_frames(prefix):
@@ -194,7 +194,7 @@ def main():
     torch.cuda.synchronize()
     barrier()
     dt = time.perf_counter() - t0
-    kms = b.kernel_ms()  # per-launch averages over the timed steps (HIP events): K1, K2, K3
+    kms = b.kernel_ms()  # per-launch averages over the timed steps (HIP events): K1..K4
     kby = b.kernel_bytes()
     px_rank = b.pixels
     dt, total_px = reduce_job(dist, "cuda", dt, px_rank * args.steps)
@@ -208,7 +208,7 @@ def main():
                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                     "traffic": ((tr or {}).get(kernel) or {}).get("bytes"), "algorithmic_bytes": int(bytes_),
                     "avg_launch_ms": round(ms, 4)}
-        ran = [k for k in range(3) if kms[k] > 0]
+        ran = [k for k in range(len(KERNELS)) if kms[k] > 0]
         roofs = {KERNELS[k]: roof(kby[k], kms[k], KERNELS[k]) for k in ran}
         dominant = roofs[KERNELS[max(ran, key=lambda k: kms[k])]]
         out = {

@@ -22,6 +22,7 @@
 
 using wg::FrameDesc;
 using wg::LLDesc;
+using wg::AlphaDesc;
 using wg::MbRec;
 
 struct wg_ctx {
@@ -47,10 +48,17 @@ struct FrameParse {
   size_t off_scratch = 0;                             // lossless two-pass scratch (plane buffer)
   size_t off_rgba = 0;                                // within the RGBA buffer
   int width = 0, height = 0;
+  // ALPH plane of a lossy frame (f2): raw bytes, or a lossless stream K3 decodes
+  bool alpha = false;
+  wg::AlphaHeader ah;
+  wg::VP8LFrame af;
+  const uint8_t* alpha_raw = nullptr;  // into the caller's input (valid during batch creation)
+  size_t off_araw = 0, off_acoded = 0, off_atdata[4] = {0, 0, 0, 0};  // input buffer
+  size_t off_ascratch = 0, off_argba = 0, off_aplane = 0;            // plane buffer
 };
 
 struct Timing {
-  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
 };
 
 // Does the lossless frame need a second pass (predictor and color indexing both present)?
@@ -73,12 +81,23 @@ int parse_one(const uint8_t* data, size_t size, int flags, FrameParse* fp) {
     fp->height = fp->lf.height;
     return WG_STATUS_OK;
   }
-  if (c.alpha_size > 0) return WG_STATUS_UNSUPPORTED_FEATURE;  // ALPH: next row (f2)
   st = wg::vp8_parse(data, size, flags, nullptr, nullptr, &fp->sf);
   if (st != WG_STATUS_OK) return st;
   if (fp->sf.info.mb_w > wg::vp8_recon_max_mb_w()) return WG_STATUS_UNSUPPORTED_FEATURE;
   fp->width = fp->sf.info.width;
   fp->height = fp->sf.info.height;
+  if (c.alpha_size > 0) {  // ALPH (VP8DecompressAlphaRows, alpha_dec.go:164-213)
+    const uint8_t* ad = data + c.alpha_off;
+    fp->alpha = true;
+    if (!wg::parse_alpha_header(ad, c.alpha_size, fp->width, fp->height, &fp->ah))
+      return WG_STATUS_OUT_OF_MEMORY;  // ALPHInit failure without a VP8L decoder
+    if (fp->ah.method == 1) {
+      st = wg::vp8l_parse_alpha(ad + 1, c.alpha_size - 1, fp->width, fp->height, &fp->af);
+      if (st != WG_STATUS_OK) return st;
+    } else {
+      fp->alpha_raw = ad + 1;
+    }
+  }
   return WG_STATUS_OK;
 }
 
@@ -115,10 +134,12 @@ struct wg_batch {
   int flags = 0;
   std::vector<FrameParse> fp;
   std::vector<FrameDesc> desc;
-  std::vector<LLDesc> lldesc;
+  std::vector<LLDesc> lldesc;     // lossless frames and lossless alpha streams (K3)
+  std::vector<AlphaDesc> adesc;   // alpha planes (K4)
   FrameDesc* d_desc = nullptr;
   LLDesc* d_lldesc = nullptr;
-  int n_lossy = 0, n_lossless = 0;
+  AlphaDesc* d_adesc = nullptr;
+  int n_lossy = 0, n_lossless = 0, n_alpha = 0, n_k3 = 0;
   int ll_groups[wg::kVP8LVariants] = {0, 0, 0, 0, 0};  // K3 frames per kernel variant
   int* d_err = nullptr;
   uint8_t* d_in = nullptr;
@@ -128,10 +149,14 @@ struct wg_batch {
   int max_mb_w = 1, max_w = 1, max_h = 1;
   int n_valid = 0;
   int64_t pixels = 0;
-  double kbytes[3] = {0, 0, 0};
+  double kbytes[4] = {0, 0, 0, 0};
   std::vector<Timing> timings;  // one per run since the last query
   size_t n_runs_pending = 0;
 };
+
+namespace {
+void fill_vp8l_info(const wg::VP8LFrame& f, wg_vp8l_info* info, uint32_t* argb, uint32_t* const* transform_data);
+}  // namespace
 
 extern "C" {
 
@@ -169,6 +194,46 @@ int wg_vp8l_parse(const uint8_t* data, size_t size, wg_vp8l_info* info, uint32_t
   wg::VP8LFrame f;
   st = wg::vp8l_parse(data + c.payload_off, c.payload_size, &f);
   if (st != WG_STATUS_OK) return st;
+  fill_vp8l_info(f, info, argb, transform_data);
+  return WG_STATUS_OK;
+}
+
+int wg_alpha_parse(const uint8_t* data, size_t size, wg_alpha_info* info, uint8_t* filtered,
+                   wg_vp8l_info* ll_info, uint32_t* argb, uint32_t* const* transform_data) {
+  if (data == nullptr) return WG_STATUS_INVALID_PARAM;
+  wg::Container c;
+  wg_features feat{};
+  int st = wg::parse_container(data, size, &c, &feat);
+  if (st != WG_STATUS_OK) return st;
+  if (c.is_lossless || c.alpha_size == 0) return WG_STATUS_UNSUPPORTED_FEATURE;
+  const uint8_t* ad = data + c.alpha_off;
+  wg::AlphaHeader ah;
+  if (info) {
+    std::memset(info, 0, sizeof(*info));
+    info->width = c.width;
+    info->height = c.height;
+  }
+  if (!wg::parse_alpha_header(ad, c.alpha_size, c.width, c.height, &ah)) return WG_STATUS_OUT_OF_MEMORY;
+  if (info) {
+    info->method = ah.method;
+    info->filter = ah.filter;
+    info->pre_processing = ah.pre_processing;
+  }
+  if (ah.method == 0) {
+    if (filtered) std::memcpy(filtered, ad + 1, (size_t)c.width * c.height);
+    return WG_STATUS_OK;
+  }
+  wg::VP8LFrame f;
+  st = wg::vp8l_parse_alpha(ad + 1, c.alpha_size - 1, c.width, c.height, &f);
+  if (st != WG_STATUS_OK) return st;
+  if (ll_info) fill_vp8l_info(f, ll_info, argb, transform_data);
+  return WG_STATUS_OK;
+}
+
+}  // extern "C"
+
+namespace {
+void fill_vp8l_info(const wg::VP8LFrame& f, wg_vp8l_info* info, uint32_t* argb, uint32_t* const* transform_data) {
   std::memset(info, 0, sizeof(*info));
   info->width = f.width;
   info->height = f.height;
@@ -184,8 +249,10 @@ int wg_vp8l_parse(const uint8_t* data, size_t size, wg_vp8l_info* info, uint32_t
       std::memcpy(transform_data[i], f.transforms[i].data.data(), f.transforms[i].data.size() * 4);
   }
   if (argb) std::memcpy(argb, f.argb.data(), f.argb.size() * 4);
-  return WG_STATUS_OK;
 }
+}  // namespace
+
+extern "C" {
 
 wg_ctx* wg_ctx_create(int device, int host_threads) {
   int n = 0;
@@ -217,6 +284,7 @@ void wg_batch_destroy(wg_batch* b) {
       if (e) hipEventDestroy(e);
   if (b->d_desc) hipFree(b->d_desc);
   if (b->d_lldesc) hipFree(b->d_lldesc);
+  if (b->d_adesc) hipFree(b->d_adesc);
   if (b->d_err) hipFree(b->d_err);
   if (b->d_in) hipFree(b->d_in);
   if (b->d_planes) hipFree(b->d_planes);
@@ -236,8 +304,27 @@ wg_batch* wg_batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t*
   parse_all(data, sizes, n, flags, ctx->host_threads, b->fp);
   // layout
   size_t in_b = 0, pl_b = 0, rg_b = 0;
-  double k1 = 0, k2 = 0;
-  double k3 = 0;
+  double k1 = 0, k2 = 0, k3 = 0, k4 = 0;
+  // K3 input (coded image + transform data) and two-pass scratch of one lossless stream;
+  // returns its algorithmic bytes (reads + RGBA write)
+  auto layout_ll = [&](const wg::VP8LFrame& lf, int w, int h, size_t* off_coded, size_t* off_tdata,
+                       size_t* off_scratch) {
+    const double px = (double)w * h;
+    *off_coded = in_b;
+    in_b = align_up(in_b + lf.argb.size() * 4);
+    double bytes = lf.argb.size() * 4.0 + 4.0 * px;
+    for (size_t t = 0; t < lf.transforms.size(); ++t) {
+      off_tdata[t] = in_b;
+      in_b = align_up(in_b + std::max<size_t>(lf.transforms[t].data.size(), 1) * 4);
+      bytes += lf.transforms[t].data.size() * 4.0;
+    }
+    if (ll_two_pass(lf)) {
+      *off_scratch = pl_b;
+      pl_b = align_up(pl_b + (size_t)w * h * 4);
+      bytes += 8.0 * px;
+    }
+    return bytes;
+  };
   for (int i = 0; i < n; ++i) {
     FrameParse& f = b->fp[i];
     if (status) status[i] = f.status;
@@ -250,22 +337,9 @@ wg_batch* wg_batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t*
     b->pixels += (int64_t)f.width * f.height;
     const double px = (double)f.width * f.height;
     if (f.lossless) {
-      // K3 reads the coded image + transform data, writes RGBA (and a scratch image when
-      // two passes are needed).
       b->n_lossless++;
-      f.off_coded = in_b;
-      in_b = align_up(in_b + f.lf.argb.size() * 4);
-      k3 += f.lf.argb.size() * 4.0 + 4.0 * px;
-      for (size_t t = 0; t < f.lf.transforms.size(); ++t) {
-        f.off_tdata[t] = in_b;
-        in_b = align_up(in_b + std::max<size_t>(f.lf.transforms[t].data.size(), 1) * 4);
-        k3 += f.lf.transforms[t].data.size() * 4.0;
-      }
-      if (ll_two_pass(f.lf)) {
-        f.off_scratch = pl_b;
-        pl_b = align_up(pl_b + (size_t)f.width * f.height * 4);
-        k3 += 8.0 * px;
-      }
+      b->n_k3++;
+      k3 += layout_ll(f.lf, f.width, f.height, &f.off_coded, f.off_tdata, &f.off_scratch);
       continue;
     }
     b->n_lossy++;
@@ -289,7 +363,27 @@ wg_batch* wg_batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t*
     const double uvpx = 2.0 * ((inf.width + 1) / 2) * (double)((inf.height + 1) / 2);
     k1 += (double)nmb * sizeof(MbRec) + inf.mb_h * 4.0 + f.sf.blocks.size() * 2.0 + nmb * 384.0;
     k2 += px + uvpx + 4.0 * px;
+    if (f.alpha) {
+      // K4 reads the filtered alpha (raw bytes, or K3's RGBA of the alpha stream) and
+      // rewrites the RGBA A bytes (dword read-modify-write)
+      b->n_alpha++;
+      if (f.ah.method == 1) {
+        b->n_k3++;
+        k3 += layout_ll(f.af, f.width, f.height, &f.off_acoded, f.off_atdata, &f.off_ascratch);
+        f.off_argba = pl_b;
+        pl_b = align_up(pl_b + (size_t)f.width * f.height * 4);
+        k4 += 4.0 * px;
+      } else {
+        f.off_araw = in_b;
+        in_b = align_up(in_b + (size_t)f.width * f.height);
+        k4 += px;
+      }
+      f.off_aplane = pl_b;
+      pl_b = align_up(pl_b + (size_t)f.width * f.height);
+      k4 += 8.0 * px;
+    }
   }
+  b->kbytes[3] = k4;
   b->kbytes[2] = k3;
   b->kbytes[0] = k1;
   b->kbytes[1] = k2;
@@ -306,13 +400,53 @@ wg_batch* wg_batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t*
   if (hipMalloc(&b->d_in, b->in_bytes) != hipSuccess || hipMalloc(&b->d_planes, b->plane_bytes) != hipSuccess ||
       hipMalloc(&b->d_rgba, b->rgba_bytes) != hipSuccess ||
       hipMalloc(&b->d_desc, sizeof(FrameDesc) * (size_t)n) != hipSuccess ||
-      hipMalloc(&b->d_lldesc, sizeof(LLDesc) * (size_t)std::max(b->n_lossless, 1)) != hipSuccess ||
+      hipMalloc(&b->d_lldesc, sizeof(LLDesc) * (size_t)std::max(b->n_k3, 1)) != hipSuccess ||
+      hipMalloc(&b->d_adesc, sizeof(AlphaDesc) * (size_t)std::max(b->n_alpha, 1)) != hipSuccess ||
       hipMalloc(&b->d_err, sizeof(int)) != hipSuccess || hipMemset(b->d_err, 0, sizeof(int)) != hipSuccess)
     return fail(WG_STATUS_OUT_OF_MEMORY);
   // stage inputs in pinned memory, one H2D copy
   uint8_t* h_in = nullptr;
   if (hipHostMalloc(reinterpret_cast<void**>(&h_in), b->in_bytes, hipHostMallocDefault) != hipSuccess)
     return fail(WG_STATUS_OUT_OF_MEMORY);
+  // the LLDesc of one lossless stream (transforms in application order = reverse of read
+  // order); its coded image and transform data go to the staging buffer
+  auto make_ll = [&](wg::VP8LFrame& lf, int w, int h, size_t off_coded, const size_t* off_tdata,
+                     size_t off_scratch, uint8_t* rgba, int stride) {
+    LLDesc l{};
+    std::memcpy(h_in + off_coded, lf.argb.data(), lf.argb.size() * 4);
+    l.coded = reinterpret_cast<const uint32_t*>(b->d_in + off_coded);
+    l.coded_bytes = (int32_t)(lf.argb.size() * 4);
+    l.scratch = ll_two_pass(lf) ? reinterpret_cast<uint32_t*>(b->d_planes + off_scratch) : nullptr;
+    l.scratch_bytes = l.scratch ? w * h * 4 : 0;
+    l.rgba = rgba;
+    l.rgba_stride = stride;
+    l.width = w;
+    l.height = h;
+    l.coded_width = lf.coded_width;
+    l.n_stages = (int32_t)lf.transforms.size();
+    int types[4], bits[4], tiles[4];
+    for (int t = 0; t < l.n_stages; ++t) {
+      const wg::VP8LTransform& tr = lf.transforms[(size_t)(l.n_stages - 1 - t)];
+      const size_t off = off_tdata[l.n_stages - 1 - t];
+      if (!tr.data.empty()) std::memcpy(h_in + off, tr.data.data(), tr.data.size() * 4);
+      wg::LLStage& st = l.stages[t];
+      st.type = tr.type;
+      st.bits = tr.bits;
+      st.xsize = tr.xsize;
+      st.tiles_per_row = (tr.type == wg::kVP8LPredictor || tr.type == wg::kVP8LCrossColor)
+                             ? (tr.xsize + (1 << tr.bits) - 1) >> tr.bits
+                             : 0;
+      st.data = reinterpret_cast<const uint32_t*>(b->d_in + off);
+      types[t] = st.type;
+      bits[t] = st.bits;
+      tiles[t] = st.tiles_per_row ? st.tiles_per_row * ((h + (1 << st.bits) - 1) >> st.bits) : 0;
+    }
+    l.valid = 1;
+    l.pad1[0] = (uint64_t)wg::vp8l_variant(types, bits, tiles, l.n_stages);  // sort key
+    wg::VP8LFrame().transforms.swap(lf.transforms);
+    std::vector<uint32_t>().swap(lf.argb);
+    return l;
+  };
   b->desc.assign(n, FrameDesc{});
   for (int i = 0; i < n; ++i) {
     FrameParse& f = b->fp[i];
@@ -323,44 +457,8 @@ wg_batch* wg_batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t*
     d.height = f.height;
     d.rgba_stride = 4 * f.width;
     if (f.lossless) {  // K1/K2 skip it (valid = 0); K3 gets an LLDesc
-      LLDesc l{};
-      std::memcpy(h_in + f.off_coded, f.lf.argb.data(), f.lf.argb.size() * 4);
-      l.coded = reinterpret_cast<const uint32_t*>(b->d_in + f.off_coded);
-      l.coded_bytes = (int32_t)(f.lf.argb.size() * 4);
-      l.scratch = ll_two_pass(f.lf) ? reinterpret_cast<uint32_t*>(b->d_planes + f.off_scratch) : nullptr;
-      l.scratch_bytes = l.scratch ? f.width * f.height * 4 : 0;
-      l.rgba = d.rgba;
-      l.rgba_stride = d.rgba_stride;
-      l.width = f.width;
-      l.height = f.height;
-      l.coded_width = f.lf.coded_width;
-      l.n_stages = (int32_t)f.lf.transforms.size();
-      for (int t = 0; t < l.n_stages; ++t) {  // application order = reverse of read order
-        const wg::VP8LTransform& tr = f.lf.transforms[(size_t)(l.n_stages - 1 - t)];
-        const size_t off = f.off_tdata[l.n_stages - 1 - t];
-        if (!tr.data.empty()) std::memcpy(h_in + off, tr.data.data(), tr.data.size() * 4);
-        l.stages[t].type = tr.type;
-        l.stages[t].bits = tr.bits;
-        l.stages[t].xsize = tr.xsize;
-        l.stages[t].tiles_per_row = (tr.type == wg::kVP8LPredictor || tr.type == wg::kVP8LCrossColor)
-                                        ? (tr.xsize + (1 << tr.bits) - 1) >> tr.bits
-                                        : 0;
-        l.stages[t].data = reinterpret_cast<const uint32_t*>(b->d_in + off);
-      }
-      l.valid = 1;
-      {
-        int types[4], bits[4], tiles[4];
-        for (int t = 0; t < l.n_stages; ++t) {
-          const wg::LLStage& st = l.stages[t];
-          types[t] = st.type;
-          bits[t] = st.bits;
-          tiles[t] = st.tiles_per_row ? st.tiles_per_row * ((f.height + (1 << st.bits) - 1) >> st.bits) : 0;
-        }
-        l.pad1[0] = (uint64_t)wg::vp8l_variant(types, bits, tiles, l.n_stages);  // sort key
-      }
-      b->lldesc.push_back(l);
-      wg::VP8LFrame().transforms.swap(f.lf.transforms);
-      std::vector<uint32_t>().swap(f.lf.argb);
+      b->lldesc.push_back(make_ll(f.lf, f.width, f.height, f.off_coded, f.off_tdata, f.off_scratch, d.rgba,
+                                  d.rgba_stride));
       continue;
     }
     const wg_vp8_info& inf = f.sf.info;
@@ -381,6 +479,26 @@ wg_batch* wg_batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t*
     d.filter_type = inf.filter_type;
     d.flags = flags;
     d.valid = 1;
+    if (f.alpha) {
+      AlphaDesc a{};
+      if (f.ah.method == 1) {
+        b->lldesc.push_back(make_ll(f.af, f.width, f.height, f.off_acoded, f.off_atdata, f.off_ascratch,
+                                    b->d_planes + f.off_argba, 4 * f.width));
+        a.green = b->d_planes + f.off_argba;
+      } else {
+        std::memcpy(h_in + f.off_araw, f.alpha_raw, (size_t)f.width * f.height);
+        a.raw = b->d_in + f.off_araw;
+      }
+      a.plane = b->d_planes + f.off_aplane;
+      a.rgba = d.rgba;
+      a.width = f.width;
+      a.height = f.height;
+      a.rgba_stride = d.rgba_stride;
+      a.filter = f.ah.filter;
+      a.valid = 1;
+      b->adesc.push_back(a);
+      f.alpha_raw = nullptr;
+    }
     // release host-side copies of the parsed data: the device owns them now
     std::vector<MbRec>().swap(f.sf.mbs);
     std::vector<int16_t>().swap(f.sf.blocks);
@@ -396,6 +514,9 @@ wg_batch* wg_batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t*
   for (const LLDesc& l : b->lldesc) b->ll_groups[l.pad1[0]]++;
   if (e == hipSuccess && !b->lldesc.empty())
     e = hipMemcpyAsync(b->d_lldesc, b->lldesc.data(), sizeof(LLDesc) * b->lldesc.size(), hipMemcpyHostToDevice,
+                       ctx->stream);
+  if (e == hipSuccess && !b->adesc.empty())
+    e = hipMemcpyAsync(b->d_adesc, b->adesc.data(), sizeof(AlphaDesc) * b->adesc.size(), hipMemcpyHostToDevice,
                        ctx->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
   hipHostFree(h_in);
@@ -427,11 +548,16 @@ int wg_batch_run(wg_batch* b, void* stream) {
     if (e != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
   }
   hipEventRecord(t.ev[2], s);
-  if (b->n_lossless > 0) {
+  if (b->n_k3 > 0) {
     hipError_t e = wg::launch_vp8l_transforms(b->d_lldesc, b->ll_groups, b->d_err, s);
     if (e != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
   }
   hipEventRecord(t.ev[3], s);
+  if (b->n_alpha > 0) {  // after K2 (A = 255) and K3 (alpha streams)
+    hipError_t e = wg::launch_alpha(b->d_adesc, b->n_alpha, s);
+    if (e != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
+  }
+  hipEventRecord(t.ev[4], s);
   return WG_STATUS_OK;
 }
 
@@ -440,11 +566,11 @@ int wg_batch_kernel_ms(const wg_batch* bc, float* ms, int n_ms) {
   if (!b || !ms || n_ms < 1) return WG_STATUS_INVALID_PARAM;
   for (int k = 0; k < n_ms; ++k) ms[k] = 0.f;
   if (b->n_runs_pending == 0) return WG_STATUS_OK;
-  double acc[3] = {0, 0, 0};
+  double acc[4] = {0, 0, 0, 0};
   for (size_t i = 0; i < b->n_runs_pending; ++i) {
     Timing& t = b->timings[i];
-    if (hipEventSynchronize(t.ev[3]) != hipSuccess) return WG_STATUS_USER_ABORT;
-    for (int k = 0; k < 3; ++k) {
+    if (hipEventSynchronize(t.ev[4]) != hipSuccess) return WG_STATUS_USER_ABORT;
+    for (int k = 0; k < 4; ++k) {
       float a = 0;
       hipEventElapsedTime(&a, t.ev[k], t.ev[k + 1]);
       acc[k] += a;
@@ -452,15 +578,15 @@ int wg_batch_kernel_ms(const wg_batch* bc, float* ms, int n_ms) {
   }
   int err = 0;
   if (hipMemcpy(&err, b->d_err, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess || err) return WG_STATUS_USER_ABORT;
-  const bool ran[3] = {b->n_lossy > 0, b->n_lossy > 0, b->n_lossless > 0};
-  for (int k = 0; k < std::min(n_ms, 3); ++k) ms[k] = ran[k] ? (float)(acc[k] / b->n_runs_pending) : 0.f;
+  const bool ran[4] = {b->n_lossy > 0, b->n_lossy > 0, b->n_k3 > 0, b->n_alpha > 0};
+  for (int k = 0; k < std::min(n_ms, 4); ++k) ms[k] = ran[k] ? (float)(acc[k] / b->n_runs_pending) : 0.f;
   b->n_runs_pending = 0;
   return WG_STATUS_OK;
 }
 
 int wg_batch_kernel_bytes(const wg_batch* b, double* bytes, int n_bytes) {
   if (!b || !bytes || n_bytes < 1) return WG_STATUS_INVALID_PARAM;
-  for (int k = 0; k < n_bytes; ++k) bytes[k] = k < 3 ? b->kbytes[k] : 0.0;
+  for (int k = 0; k < n_bytes; ++k) bytes[k] = k < 4 ? b->kbytes[k] : 0.0;
   return WG_STATUS_OK;
 }
 

@@ -1,0 +1,219 @@
+// K4: ALPH alpha planes of lossy frames -> the A channel of their RGBA output.
+//
+// Replaces the reference's alpha stage (pkg/libwebp/decoder/alpha_dec.go:47-213):
+//   ALPHDecode / ExtractAlphaRows (vp8l_dec.c.go:1462-1489): alpha = green channel of the
+//     lossless stream after its inverse transforms (here: K3's RGBA output, byte 1), or the
+//     raw bytes for method 0;
+//   WebPUnfilters (dsp/filters.go:130-171): HorizontalUnfilter_C, VerticalUnfilter_C,
+//     GradientUnfilter_C, row by row with the previous output row as `prev` (none for row 0);
+//   EmitAlphaRGB (io_dec.c.go:175-195): A bytes of the (non-premultiplied) RGBA output.
+// WebPDequantizeLevels only runs with alpha dithering > 0 (alpha_dec.go:199-206); the
+// decode options here keep it 0, as WebPDecode's defaults do, so pre-processed (level
+// quantized) planes are emitted as decoded.
+//
+// One 1024-thread workgroup per plane, after K2 (which wrote A = 255).  Passes:
+//   1. gather the filtered bytes into `plane` (green extraction or a copy);
+//   2. unfilter in place.  The unfilters are per-byte sums mod 256 except gradient:
+//        horizontal  out[y][x] = c[y-1] + sum_{i<=x} in[y][i], c = column-0 prefix sums
+//                    -> one block scan down column 0, then a wave scan per row;
+//        vertical    row 0 as horizontal, then out[y][x] = out[y-1][x] + in[y][x]
+//                    -> a running sum per column (threads across columns);
+//        gradient    row 0 as horizontal, then out = in + clip(L + T - TL): a wavefront
+//                    over 1024-row bands (thread = row, one column per step, T from the
+//                    thread above via DPP / LDS, the band's top row from LDS);
+//   3. write the plane into the A bytes (dword read-modify-write, coalesced).
+// The plane traffic is small next to K1/K2 (1 B/px vs 5.5 B/px); the gradient wavefront is
+// latency-bound (one barrier per column step) and is the slow case.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../device_format.h"
+#include "kernels.h"
+
+namespace wg {
+namespace {
+
+constexpr int kThreads = 1024;
+constexpr int kWaves = kThreads / 64;
+constexpr int kMaxDim = 16384;
+
+__device__ __forceinline__ int wave_incl_scan(int v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int u = __shfl_up(v, d, 64);
+    if (lane >= d) v += u;
+  }
+  return v;
+}
+
+// Exclusive scan of one int per thread over the block; `tot` gets the block total.
+__device__ __forceinline__ int block_excl_scan(int v, int* wsum, int* tot) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int inc = wave_incl_scan(v);
+  if (lane == 63) wsum[wave] = inc;
+  __syncthreads();
+  if (wave == 0) {
+    const int w = lane < kWaves ? wsum[lane] : 0;
+    const int wi = wave_incl_scan(w);
+    if (lane < kWaves) wsum[lane] = wi - w;
+    if (lane == kWaves - 1) *tot = wi;
+  }
+  __syncthreads();
+  return wsum[wave] + inc - v;
+}
+
+// One row as HorizontalUnfilter_C with `pred` for its first byte, by wave `wave` (all
+// lanes of that wave call it): 64-byte chunks, wave scan + running carry.
+__device__ __forceinline__ void scan_row(uint8_t* row, int W, uint32_t pred) {
+  const int lane = threadIdx.x & 63;
+  uint32_t carry = pred;
+  for (int x0 = 0; x0 < W; x0 += 64) {
+    const int x = x0 + lane;
+    const int v = x < W ? row[x] : 0;
+    const int inc = wave_incl_scan(v);
+    if (x < W) row[x] = (uint8_t)(carry + (uint32_t)inc);
+    carry += (uint32_t)__shfl(inc, 63, 64);
+  }
+}
+
+__device__ __forceinline__ uint32_t shr1(uint32_t old, uint32_t v) {  // lane i <- lane i-1; lane 0 <- old
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x138, 0xF, 0xF, false);
+}
+
+__global__ void __launch_bounds__(kThreads) alpha_kernel(const AlphaDesc* __restrict__ frames) {
+  __shared__ uint8_t rowbuf[kMaxDim];  // horizontal: column-0 prefix; gradient: the band's top row
+  __shared__ int wsum[kWaves];
+  __shared__ int total;
+  __shared__ uint32_t edge[2][kWaves];  // gradient: each wave's lane-63 output of the last step
+  const AlphaDesc& F = frames[blockIdx.x];
+  if (!F.valid) return;
+  const int W = F.width, H = F.height, tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const size_t n = (size_t)W * H;
+  uint8_t* plane = F.plane;
+
+  // ---- 1. filtered bytes into the plane (4 px per thread step)
+  if (F.green) {
+    const uint32_t* g = reinterpret_cast<const uint32_t*>(F.green);
+    uint32_t* p4 = reinterpret_cast<uint32_t*>(plane);
+    const size_t n4 = n / 4;
+    for (size_t i = tid; i < n4; i += kThreads) {
+      const uint32_t a = g[4 * i], b = g[4 * i + 1], c = g[4 * i + 2], d = g[4 * i + 3];
+      p4[i] = ((a >> 8) & 0xff) | (b & 0xff00) | ((c << 8) & 0xff0000) | ((d << 16) & 0xff000000u);
+    }
+    for (size_t i = n4 * 4 + tid; i < n; i += kThreads) plane[i] = (uint8_t)(g[i] >> 8);
+  } else {
+    const uint32_t* r4 = reinterpret_cast<const uint32_t*>(F.raw);
+    uint32_t* p4 = reinterpret_cast<uint32_t*>(plane);
+    const size_t n4 = (reinterpret_cast<uintptr_t>(F.raw) & 3) ? 0 : n / 4;
+    for (size_t i = tid; i < n4; i += kThreads) p4[i] = r4[i];
+    for (size_t i = n4 * 4 + tid; i < n; i += kThreads) plane[i] = F.raw[i];
+  }
+  __syncthreads();
+
+  // ---- 2. unfilter in place
+  if (F.filter == 1) {  // horizontal
+    // column-0 prefix sums c[y] (mod 256) into rowbuf
+    const int per = (H + kThreads - 1) / kThreads, y0 = tid * per, y1 = min(H, y0 + per);
+    int s = 0;
+    for (int y = y0; y < y1; ++y) s += plane[(size_t)y * W];
+    int run = block_excl_scan(s, wsum, &total);
+    for (int y = y0; y < y1; ++y) {
+      run += plane[(size_t)y * W];
+      rowbuf[y] = (uint8_t)run;
+    }
+    __syncthreads();
+    for (int y = wave; y < H; y += kWaves) scan_row(plane + (size_t)y * W, W, y == 0 ? 0u : rowbuf[y - 1]);
+  } else if (F.filter == 2) {  // vertical
+    if (wave == 0) scan_row(plane, W, 0u);
+    __syncthreads();
+    for (int x = tid; x < W; x += kThreads) {
+      uint32_t acc = plane[x];
+      int y = 1;
+      for (; y + 8 <= H; y += 8) {  // eight rows of loads in flight per step
+        uint8_t v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = plane[(size_t)(y + k) * W + x];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          acc += v[k];
+          plane[(size_t)(y + k) * W + x] = (uint8_t)acc;
+        }
+      }
+      for (; y < H; ++y) {
+        acc += plane[(size_t)y * W + x];
+        plane[(size_t)y * W + x] = (uint8_t)acc;
+      }
+    }
+  } else if (F.filter == 3) {  // gradient
+    if (wave == 0) scan_row(plane, W, 0u);
+    __syncthreads();
+    for (int x = tid; x < W; x += kThreads) rowbuf[x] = plane[x];
+    __syncthreads();
+    for (int yb = 1; yb < H; yb += kThreads) {
+      const int rows = min(kThreads, H - yb);
+      const int y = yb + tid;
+      const bool row_ok = tid < rows;
+      uint8_t* prow = plane + (size_t)min(y, H - 1) * W;
+      // inputs eight steps ahead (a shift register of loaded bytes)
+      constexpr int kAhead = 8;
+      uint32_t q[kAhead];
+#pragma unroll
+      for (int k = 0; k < kAhead; ++k) {
+        const int x = k - tid;
+        q[k] = (row_ok && x >= 0 && x < W) ? prow[x] : 0u;
+      }
+      uint32_t L = 0, TL = 0;
+      const int steps = W + rows - 1;
+      for (int s = 0; s < steps; ++s) {
+        const int x = s - tid;
+        const bool ok = row_ok && x >= 0 && x < W;
+        // T = out[y-1][x]: the thread above's output of step s-1 (DPP within the wave;
+        // across waves through `edge`; the band's top row from rowbuf)
+        uint32_t up = 0;
+        if (wave > 0) up = edge[(s + 1) & 1][wave - 1];
+        else if (s < W) up = rowbuf[s];
+        uint32_t T = shr1(up, L) & 0xff;
+        const uint32_t v = q[0];
+#pragma unroll
+        for (int k = 0; k + 1 < kAhead; ++k) q[k] = q[k + 1];
+        {
+          const int xa = x + kAhead;
+          q[kAhead - 1] = (row_ok && xa >= 0 && xa < W) ? prow[xa] : 0u;
+        }
+        uint32_t l = L, tl = TL;
+        if (x == 0) l = tl = T;  // leftmost: predicted from above
+        const int g = (int)l + (int)T - (int)tl;
+        const uint32_t o = (v + (uint32_t)min(max(g, 0), 255)) & 0xff;
+        if (ok) {
+          prow[x] = (uint8_t)o;
+          L = o;
+          if (tid == rows - 1) rowbuf[x] = (uint8_t)o;  // the next band's top row
+        }
+        TL = T;
+        if (lane == 63) edge[s & 1][wave] = L;
+        __syncthreads();
+      }
+      __syncthreads();
+    }
+  }
+  __syncthreads();
+
+  // ---- 3. plane -> A bytes
+  for (int y = wave; y < H; y += kWaves) {
+    uint32_t* dst = reinterpret_cast<uint32_t*>(F.rgba + (size_t)y * F.rgba_stride);
+    const uint8_t* src = plane + (size_t)y * W;
+    for (int x = lane; x < W; x += 64) dst[x] = (dst[x] & 0x00ffffffu) | ((uint32_t)src[x] << 24);
+  }
+}
+
+}  // namespace
+
+hipError_t launch_alpha(const AlphaDesc* d_frames, int n_frames, hipStream_t stream) {
+  if (n_frames <= 0) return hipSuccess;
+  hipLaunchKernelGGL(alpha_kernel, dim3(n_frames), dim3(kThreads), 0, stream, d_frames);
+  return hipGetLastError();
+}
+
+}  // namespace wg

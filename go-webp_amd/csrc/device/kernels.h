@@ -28,4 +28,8 @@ constexpr int kVP8LVariants = 5;
 int vp8l_variant(const int* types, const int* bits, const int* tiles, int n_stages);  // stages in application order
 hipError_t launch_vp8l_transforms(const LLDesc* d_frames, const int* group_count, int* d_err, hipStream_t stream);
 
+// K4: ALPH planes (unfilter) -> A bytes of the RGBA output, one 1024-thread workgroup per
+// plane; runs after K2 and K3.
+hipError_t launch_alpha(const AlphaDesc* d_frames, int n_frames, hipStream_t stream);
+
 }  // namespace wg

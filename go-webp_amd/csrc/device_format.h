@@ -81,4 +81,15 @@ struct LLDesc {
 };
 static_assert(sizeof(LLDesc) == 192, "LLDesc must be 192 bytes");
 
+// One ALPH plane for K4 (alpha.hip).  Exactly one of green / raw is set.
+struct AlphaDesc {
+  const uint8_t* green;  // K3's RGBA output of the lossless alpha stream: byte 1 of each pixel
+  const uint8_t* raw;    // method 0: the filtered bytes, width*height
+  uint8_t* plane;        // width*height scratch: filtered -> unfiltered alpha
+  uint8_t* rgba;         // the frame's RGBA output; K4 writes its A bytes
+  int32_t width, height, rgba_stride, filter;  // filter: 0 none, 1 horizontal, 2 vertical, 3 gradient
+  int32_t valid, pad0, pad1, pad2;
+};
+static_assert(sizeof(AlphaDesc) == 64, "AlphaDesc must be 64 bytes");
+
 }  // namespace wg

@@ -169,3 +169,20 @@ int parse_container(const uint8_t* data, size_t data_size, Container* c, wg_feat
 }
 
 }  // namespace wg
+
+namespace wg {
+
+// ALPHInit's header checks (alpha_dec.go:57-101): ALPHA_HEADER_LEN = 1, method 0/1,
+// any of the four filters, pre-processing 0/1, reserved bits 0; raw alpha must hold
+// width * height bytes.
+bool parse_alpha_header(const uint8_t* data, size_t size, int width, int height, AlphaHeader* out) {
+  if (data == nullptr || size <= 1) return false;
+  out->method = data[0] & 3;
+  out->filter = (data[0] >> 2) & 3;
+  out->pre_processing = (data[0] >> 4) & 3;
+  if (out->method > 1 || out->pre_processing > 1 || (data[0] >> 6) != 0) return false;
+  if (out->method == 0 && size - 1 < (size_t)width * (size_t)height) return false;
+  return true;
+}
+
+}  // namespace wg

@@ -57,4 +57,14 @@ struct VP8LFrame {
 // Entropy-decode a VP8L bitstream (the VP8L chunk payload).
 int vp8l_parse(const uint8_t* data, size_t size, VP8LFrame* out);
 
+// ALPH chunk (alpha_dec.go:47-105): header byte = method (bits 0-1: 0 raw, 1 lossless),
+// filter (2-3: none, horizontal, vertical, gradient), pre-processing (4-5), reserved (6-7).
+struct AlphaHeader {
+  int method = 0, filter = 0, pre_processing = 0;
+};
+// Validates the header as ALPHInit does; false -> WebPDecode's OUT_OF_MEMORY.
+bool parse_alpha_header(const uint8_t* data, size_t size, int width, int height, AlphaHeader* out);
+// The lossless alpha stream (headerless VP8L, green channel = alpha).
+int vp8l_parse_alpha(const uint8_t* data, size_t size, int width, int height, VP8LFrame* out);
+
 }  // namespace wg

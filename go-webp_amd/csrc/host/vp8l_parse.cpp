@@ -264,6 +264,8 @@ struct Decoder {
     return dist >= 1 ? dist : 1;
   }
 
+  bool in_main_pixels = false;  // the level-0 pixel loop has started (alpha error mapping)
+
   // One entropy-coded image (main image when `level0`, else a side image).
   bool decode_stream(int xsize, int ysize, bool level0, VP8LFrame* f, std::vector<uint32_t>* out) {
     if (level0) {
@@ -333,6 +335,7 @@ struct Decoder {
       for (int j = 0; j < 5; ++j)
         if (!read_code(alphabet[j], &groups[(size_t)g].code[j])) return false;
     // pixels
+    if (level0) in_main_pixels = true;
     const size_t total = (size_t)xsize * ysize;
     out->assign(total, 0u);
     uint32_t* data = out->data();
@@ -410,6 +413,24 @@ int vp8l_parse(const uint8_t* data, size_t size, VP8LFrame* out) {
   out->transforms.clear();
   out->coded_width = out->width;
   if (!d.decode_stream(out->width, out->height, true, out, &out->argb)) return d.status;
+  return WG_STATUS_OK;
+}
+
+// The ALPH chunk's lossless stream: a VP8L image stream without the 5-byte header, sized
+// by the frame (VP8LDecodeAlphaHeader / VP8LDecodeAlphaImageStream, vp8l_dec.c.go:1493-1556).
+// Status as WebPDecode reports it: a failure while reading the stream's transforms and
+// codes leaves the alpha decoder without a VP8L decoder, which VP8DecompressAlphaRows
+// reports as OUT_OF_MEMORY (alpha_dec.go:177-182); a failure in the pixel data is
+// "Could not decode alpha data" = BITSTREAM_ERROR.
+int vp8l_parse_alpha(const uint8_t* data, size_t size, int width, int height, VP8LFrame* out) {
+  out->width = width;
+  out->height = height;
+  out->has_alpha = 0;
+  out->transforms.clear();
+  out->coded_width = width;
+  Decoder d(data, size);
+  if (!d.decode_stream(width, height, true, out, &out->argb))
+    return d.in_main_pixels ? WG_STATUS_BITSTREAM_ERROR : WG_STATUS_OUT_OF_MEMORY;
   return WG_STATUS_OK;
 }
 

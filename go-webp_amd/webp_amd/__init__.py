@@ -63,6 +63,12 @@ class VP8Info(C.Structure):
                 ("frame_offset", C.c_int32)]
 
 
+class AlphaInfo(C.Structure):
+    """wg_alpha_info: the ALPH chunk of a lossy frame."""
+    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("method", C.c_int32), ("filter", C.c_int32),
+                ("pre_processing", C.c_int32), ("reserved", C.c_int32)]
+
+
 class VP8LInfo(C.Structure):
     """wg_vp8l_info: a lossless frame after the host entropy stage."""
     _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("has_alpha", C.c_int32),
@@ -103,6 +109,7 @@ _SIGS = {
                                            C.c_int, _P]),
     "wg_vp8_parse": (C.c_int, [_P, C.c_size_t, C.c_int, C.POINTER(VP8Info), _P]),
     "wg_vp8l_parse": (C.c_int, [_P, C.c_size_t, C.POINTER(VP8LInfo), _P, _P]),
+    "wg_alpha_parse": (C.c_int, [_P, C.c_size_t, _P, _P, _P, _P, _P]),
 }
 EXPORTED = tuple(_SIGS)
 
@@ -209,6 +216,32 @@ def vp8l_parse(data):
     return info, argb, tdata
 
 
+def alpha_parse(data):
+    """Host stage of the ALPH chunk of a lossy file: (AlphaInfo, payload) with payload the
+    (height, width) filtered bytes for method 0, or (VP8LInfo, argb, tdata) of the alpha
+    stream (as vp8l_parse returns them) for method 1."""
+    b = _buf(data)
+    info = AlphaInfo()
+    ll = VP8LInfo()
+    L = lib()
+    st = L.wg_alpha_parse(b, len(b), C.byref(info), None, C.byref(ll), None, None)
+    if st != Status.OK:
+        raise WebPError(st, "wg_alpha_parse")
+    if info.method == 0:
+        filt = np.zeros((info.height, info.width), np.uint8)
+        st = L.wg_alpha_parse(b, len(b), C.byref(info), filt.ctypes.data, None, None, None)
+        if st != Status.OK:
+            raise WebPError(st, "wg_alpha_parse")
+        return info, filt
+    argb = np.zeros((ll.height, ll.coded_width), np.uint32)
+    tdata = [np.zeros(max(1, ll.transform_size[i]), np.uint32) for i in range(ll.num_transforms)]
+    ptrs = (C.c_void_p * 4)(*([t.ctypes.data for t in tdata] + [None] * (4 - len(tdata))))
+    st = L.wg_alpha_parse(b, len(b), C.byref(info), None, C.byref(ll), argb.ctypes.data, ptrs)
+    if st != Status.OK:
+        raise WebPError(st, "wg_alpha_parse")
+    return info, (ll, argb, tdata)
+
+
 def _ptr_arrays(datas):
     bufs = [_buf(d) for d in datas]
     n = len(bufs)
@@ -239,18 +272,18 @@ class Batch:
             raise WebPError(st, "wg_batch_run")
 
     def kernel_ms(self):
-        """(K1, K2, K3) per-launch ms averaged over the runs since the last call."""
-        ms = (C.c_float * 3)()
-        st = lib().wg_batch_kernel_ms(self._h, ms, 3)
+        """(K1, K2, K3, K4) per-launch ms averaged over the runs since the last call."""
+        ms = (C.c_float * 4)()
+        st = lib().wg_batch_kernel_ms(self._h, ms, 4)
         if st != Status.OK:
             raise WebPError(st, "wg_batch_kernel_ms")
-        return float(ms[0]), float(ms[1]), float(ms[2])
+        return tuple(float(v) for v in ms)
 
     def kernel_bytes(self):
-        """Algorithmic HBM bytes per launch of (K1, K2, K3)."""
-        b = (C.c_double * 3)()
-        lib().wg_batch_kernel_bytes(self._h, b, 3)
-        return float(b[0]), float(b[1]), float(b[2])
+        """Algorithmic HBM bytes per launch of (K1, K2, K3, K4)."""
+        b = (C.c_double * 4)()
+        lib().wg_batch_kernel_bytes(self._h, b, 4)
+        return tuple(float(v) for v in b)
 
     @property
     def pixels(self):

@@ -98,17 +98,18 @@ wg_batch* wg_batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t*
 void wg_batch_destroy(wg_batch* b);
 
 /* Run the device DSP path for the whole batch on `stream` (NULL = ctx stream):
- * lossy frames: K1 reconstruct+deblock wavefront, K2 YUV420->RGBA; lossless frames:
- * K3 inverse transforms + RGBA.  Kernel durations of the last run
+ * lossy frames: K1 reconstruct+deblock wavefront, K2 YUV420->RGBA, K4 ALPH plane -> A;
+ * lossless frames (and lossless ALPH streams): K3 inverse transforms + RGBA.  Kernel durations of the last run
  * (HIP events on that stream) are available from wg_batch_kernel_ms(). */
 int wg_batch_run(wg_batch* b, void* stream);
 
 /* Per-launch kernel durations averaged over the runs since the last query:
  * ms[0] = VP8 reconstruct+filter (K1), ms[1] = YUV->RGBA (K2), ms[2] = VP8L inverse
- * transforms (K3); a kernel with no frames in the batch reports 0.  n_ms >= 1. */
+ * transforms (K3, lossless frames and lossless ALPH streams), ms[3] = ALPH unfilter + A
+ * channel (K4); a kernel with no frames in the batch reports 0.  n_ms >= 1. */
 int wg_batch_kernel_ms(const wg_batch* b, float* ms, int n_ms);
 
-/* Algorithmic HBM bytes per launch of K1, K2, K3. */
+/* Algorithmic HBM bytes per launch of K1, K2, K3, K4. */
 int wg_batch_kernel_bytes(const wg_batch* b, double* bytes, int n_bytes);
 
 int wg_batch_size(const wg_batch* b);
@@ -179,6 +180,26 @@ typedef struct {
  * NULL to only fill `info`. */
 int wg_vp8l_parse(const uint8_t* data, size_t size, wg_vp8l_info* info, uint32_t* argb,
                   uint32_t* const* transform_data);
+
+/* ---- host stage of an ALPH plane (VP8 + alpha) ----------------------------------------- */
+/* The ALPH chunk of a lossy frame (reference ALPHInit / VP8LDecodeAlphaHeader,
+ * pkg/libwebp/decoder/alpha_dec.go:47-105, pkg/vp8/vp8l_dec.c.go:1493-1556). */
+typedef struct {
+  int32_t width, height;        /* the frame's size = the plane's size                       */
+  int32_t method;               /* 0 raw bytes, 1 lossless (VP8L stream, alpha = green)      */
+  int32_t filter;               /* 0 none, 1 horizontal, 2 vertical, 3 gradient             */
+  int32_t pre_processing;       /* 1: level-quantized (dequantized only with dithering > 0) */
+  int32_t reserved;
+} wg_alpha_info;
+
+/* Parse the ALPH chunk of `data` (a whole WebP file).  method 0: the width*height filtered
+ * bytes go to `filtered`; method 1: the alpha stream's entropy stage goes to ll_info / argb /
+ * transform_data exactly as wg_vp8l_parse fills them.  Any output pointer may be NULL.
+ * Status as WebPDecode would report the plane: an invalid header or stream header is
+ * OUT_OF_MEMORY (libwebp's ALPHInit failure path), a bad pixel stream BITSTREAM_ERROR; a frame
+ * without ALPH is UNSUPPORTED_FEATURE. */
+int wg_alpha_parse(const uint8_t* data, size_t size, wg_alpha_info* info, uint8_t* filtered,
+                   wg_vp8l_info* ll_info, uint32_t* argb, uint32_t* const* transform_data);
 
 #ifdef __cplusplus
 }  /* extern "C" */

@@ -22,7 +22,8 @@ frames (SURVEY.md §8(d), Appendix B generators) are stored as ``.webp`` plus
 SHA-256 of their decodes in ``manifest.json``.  Every decode is also checked
 against libwebp's SIMD path (must be byte-identical) before it is written.
 
-Usage:  python tests/golden/make_golden.py   (rewrites tests/golden/{lossy,lossless,bench}/)
+Usage:  python tests/golden/make_golden.py [lossy|lossless|alpha|bench ...]
+        (rewrites tests/golden/<section>/; default all sections)
 """
 import ctypes as C
 import glob
@@ -63,7 +64,8 @@ def _plain_c(on):
 
 # ----------------------------------------------------------------------------- encode
 def encode(img, quality=75.0, lossless=0, method=4, segments=4, sns=50, filter_strength=60,
-           sharpness=0, filter_type=1, autofilter=0, partitions=0, low_memory=0, exact=0):
+           sharpness=0, filter_type=1, autofilter=0, partitions=0, low_memory=0, exact=0,
+           alpha_compression=1, alpha_filtering=1, alpha_quality=100):
     """img: HxWx3 or HxWx4 uint8.  Returns the encoded RIFF bytes."""
     h, w, ch = img.shape
     cfg = (C.c_int32 * 64)()
@@ -78,6 +80,9 @@ def encode(img, quality=75.0, lossless=0, method=4, segments=4, sns=50, filter_s
     cfg[9] = sharpness
     cfg[10] = filter_type
     cfg[11] = autofilter
+    cfg[12] = alpha_compression  # 0 raw, 1 lossless
+    cfg[13] = alpha_filtering    # 0 none, 1 fast, 2 best
+    cfg[14] = alpha_quality      # < 100: level pre-processing
     cfg[18] = partitions
     cfg[22] = low_memory
     cfg[24] = exact
@@ -262,6 +267,97 @@ def with_alpha(img, seed):
     return np.concatenate([img, a.astype(np.uint8)[..., None]], -1)
 
 
+def alpha_pattern(H, W, seed, kind):
+    """RGB content plus an alpha plane shaped so one unfilter wins: 'h' rows of ramps with
+    random row offsets, 'v' the transpose, 'g' a plane plus a mild texture, 'lv' four levels."""
+    rng = np.random.default_rng(seed)
+    img = synth(H, W, seed, 6)
+    yy, xx = np.mgrid[0:H, 0:W]
+    if kind == "h":
+        a = xx * 3 + rng.integers(0, 256, (H, 1))
+    elif kind == "v":
+        a = yy * 3 + rng.integers(0, 256, (1, W))
+    elif kind == "g":
+        a = xx * 5 + yy * 7 + (rng.integers(0, 3, (H, W)))
+    elif kind == "lv":
+        a = ((xx // 7 + yy // 5) % 4) * 85
+    else:
+        a = rng.integers(0, 256, (H, W))
+    return np.concatenate([img, (a % 256).astype(np.uint8)[..., None]], -1)
+
+
+def alpha_header(data):
+    """ALPH chunk header byte of a VP8X file -> (method, filter, pre_processing)."""
+    p = 12
+    while p + 8 <= len(data):
+        tag, size = data[p:p + 4], int.from_bytes(data[p + 4:p + 8], "little")
+        if tag == b"ALPH":
+            b0 = data[p + 8]
+            return dict(method=b0 & 3, filter=(b0 >> 2) & 3, pre=(b0 >> 4) & 3)
+        p += 8 + size + (size & 1)
+    return None
+
+
+def set_alpha_filter(data, filt):
+    """Rewrite the ALPH header's filter bits.  libwebp never filters raw (method 0) alpha
+    ("filtering will make no impact on compressed size"), but its decoder unfilters any
+    method; the payload bytes are then read as filtered data and libwebp's decode of the
+    edited file is the expected output."""
+    b = bytearray(data)
+    p = 12
+    while p + 8 <= len(b):
+        tag, size = bytes(b[p:p + 4]), int.from_bytes(b[p + 4:p + 8], "little")
+        if tag == b"ALPH":
+            b[p + 8] = (b[p + 8] & ~0x0c) | (filt << 2)
+            return bytes(b)
+        p += 8 + size + (size & 1)
+    raise ValueError("no ALPH chunk")
+
+
+def riff_chunks(data):
+    """[(tag, payload)] of a RIFF/WEBP file."""
+    out, p = [], 12
+    while p + 8 <= len(data):
+        tag, size = data[p:p + 4], int.from_bytes(data[p + 4:p + 8], "little")
+        out.append((tag, data[p + 8:p + 8 + size]))
+        p += 8 + size + (size & 1)
+    return out
+
+
+def riff_build(chunks):
+    body = b"WEBP"
+    for tag, payload in chunks:
+        body += tag + len(payload).to_bytes(4, "little") + payload + (b"\0" if len(payload) & 1 else b"")
+    return b"RIFF" + len(body).to_bytes(4, "little") + body
+
+
+def edit_alph(data, fn):
+    return riff_build([(t, fn(pl) if t == b"ALPH" else pl) for t, pl in riff_chunks(data)])
+
+
+def decode_status(data):
+    """WebPDecode's status for RGBA output (plain-C kernels)."""
+    cfg = (C.c_uint8 * 512)()
+    assert LIB.WebPInitDecoderConfigInternal(cfg, ABI)
+    C.cast(cfg, C.POINTER(C.c_int32))[40 // 4] = MODE_RGBA
+    st = LIB.WebPDecode(data, C.c_size_t(len(data)), cfg)
+    LIB.WebPFreeDecBuffer(C.byref(cfg, 40))
+    return st
+
+
+# corrupted ALPH chunks: (name, source fixture, edit of the chunk payload)
+ALPHA_ERROR_CASES = [
+    ("e_reserved_bits", "a_raw_none_40x30", lambda pl: bytes([pl[0] | 0x40]) + pl[1:]),
+    ("e_method2", "a_raw_none_40x30", lambda pl: bytes([(pl[0] & ~3) | 2]) + pl[1:]),
+    ("e_preproc2", "a_ll_none_33x65", lambda pl: bytes([(pl[0] & ~0x30) | 0x20]) + pl[1:]),
+    ("e_raw_short", "a_raw_h_71x33", lambda pl: pl[:-1]),
+    ("e_header_only", "a_ll_h_130x70", lambda pl: pl[:1]),
+    ("e_ll_stream_2b", "a_ll_h_130x70", lambda pl: pl[:3]),
+    ("e_ll_stream_half", "a_ll_g_120x1100", lambda pl: pl[:len(pl) // 2]),
+    ("e_ll_stream_zeros", "a_ll_v_97x81", lambda pl: pl[:1] + bytes(len(pl) - 1)),
+]
+
+
 # ----------------------------------------------------------------------------- cases
 LOSSY_CASES = [
     # name, image-fn, encoder kwargs
@@ -302,6 +398,27 @@ LOSSLESS_CASES = [
     ("ll_smooth_100x60_q0", lambda: smooth(60, 100, 10), {"quality": 0, "method": 1}),
 ]
 
+ALPHA_CASES = [
+    # name, image-fn, encoder kwargs, expected (method, filter)
+    ("a_raw_none_40x30", lambda: alpha_pattern(30, 40, 31, "n"),
+     {"alpha_compression": 0, "alpha_filtering": 0}, (0, 0)),
+    # set_filter: the ALPH filter bits rewritten after encoding (set_alpha_filter)
+    ("a_raw_h_71x33", lambda: alpha_pattern(33, 71, 32, "n"), {"alpha_compression": 0, "set_filter": 1}, (0, 1)),
+    ("a_raw_v_50x47", lambda: alpha_pattern(47, 50, 33, "n"), {"alpha_compression": 0, "set_filter": 2}, (0, 2)),
+    ("a_raw_g_64x64", lambda: alpha_pattern(64, 64, 34, "n"), {"alpha_compression": 0, "set_filter": 3}, (0, 3)),
+    ("a_raw_g_40x1030", lambda: alpha_pattern(1030, 40, 42, "n"), {"alpha_compression": 0, "set_filter": 3},
+     (0, 3)),
+    ("a_ll_none_33x65", lambda: alpha_pattern(65, 33, 35, "h"), {"alpha_filtering": 0}, (1, 0)),
+    ("a_ll_h_130x70", lambda: alpha_pattern(70, 130, 36, "h"), {"alpha_filtering": 0, "set_filter": 1}, (1, 1)),
+    ("a_ll_v_97x81", lambda: alpha_pattern(81, 97, 37, "v"), {"alpha_filtering": 0, "set_filter": 2}, (1, 2)),
+    ("a_ll_g_120x1100", lambda: alpha_pattern(1100, 120, 38, "g"), {"alpha_filtering": 0, "set_filter": 3}, (1, 3)),
+    ("a_ll_best_h_96x64", lambda: alpha_pattern(64, 96, 43, "h"), {"alpha_filtering": 2}, None),
+    ("a_ll_best_g_96x64", lambda: alpha_pattern(64, 96, 44, "g"), {"alpha_filtering": 2}, None),
+    ("a_ll_levels_90x60", lambda: alpha_pattern(60, 90, 39, "lv"), {"alpha_filtering": 0}, (1, 0)),
+    ("a_ll_q50_80x80", lambda: alpha_pattern(80, 80, 40, "g"), {"alpha_filtering": 1, "alpha_quality": 50}, None),
+    ("a_ll_1x1", lambda: alpha_pattern(1, 1, 41, "n"), {}, None),
+]
+
 BENCH_CASES = [
     # name, H, W, seeds, kwargs, generator  
     ("c1_512", 512, 512, [0], {}, "synth6"),
@@ -315,12 +432,21 @@ def sha(a):
     return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
 
 
-def main():
+def main(argv):
+    """argv: sections to (re)generate among lossy, lossless, alpha, bench (default: all);
+    the manifest entries of the other sections are kept."""
+    sections = set(argv) or {"lossy", "lossless", "alpha", "bench"}
     os.makedirs(os.path.join(HERE, "lossy"), exist_ok=True)
     os.makedirs(os.path.join(HERE, "lossless"), exist_ok=True)
     os.makedirs(os.path.join(HERE, "bench"), exist_ok=True)
-    manifest = {"libwebp": "1.6.0 (Pillow 12.2.0 bundle, plain-C DSP)", "lossy": {}, "lossless": {}, "bench": {}}
-    for name, fn, kw in LOSSY_CASES:
+    mpath = os.path.join(HERE, "manifest.json")
+    manifest = json.load(open(mpath)) if os.path.exists(mpath) else {}
+    manifest["libwebp"] = "1.6.0 (Pillow 12.2.0 bundle, plain-C DSP)"
+    for sec in sections:
+        manifest[sec] = {}
+    if "alpha" in sections:
+        manifest["alpha_errors"] = {}
+    for name, fn, kw in LOSSY_CASES if "lossy" in sections else []:
         img = fn()
         data = encode(img, **kw)
         r = decode_all(data, lossy=True)
@@ -331,7 +457,7 @@ def main():
         manifest["lossy"][name] = dict(bytes=len(data), width=img.shape[1], height=img.shape[0],
                                        header=hdr, encoder=kw)
         print(name, len(data), hdr, flush=True)
-    for name, fn, kw in LOSSLESS_CASES:
+    for name, fn, kw in LOSSLESS_CASES if "lossless" in sections else []:
         img = fn()
         data = encode(img, lossless=1, **kw)
         r = decode_all(data, lossy=False)
@@ -340,7 +466,38 @@ def main():
         np.savez_compressed(os.path.join(HERE, "lossless", name + ".npz"), **r)
         manifest["lossless"][name] = dict(bytes=len(data), width=img.shape[1], height=img.shape[0], encoder=kw)
         print(name, len(data), flush=True)
-    for name, H, W, seeds, kw, gen in BENCH_CASES:
+    os.makedirs(os.path.join(HERE, "alpha"), exist_ok=True)
+    for name, fn, kw, want in ALPHA_CASES if "alpha" in sections else []:
+        img = fn()
+        kw = dict(kw)
+        filt = kw.pop("set_filter", None)
+        data = encode(img, **kw)
+        if filt is not None:
+            data = set_alpha_filter(data, filt)
+            kw["set_filter"] = filt
+        hdr = alpha_header(data)
+        assert hdr is not None, name
+        if want is not None:
+            assert (hdr["method"], hdr["filter"]) == want, (name, hdr)
+        r = decode_all(data, lossy=False)
+        with open(os.path.join(HERE, "alpha", name + ".webp"), "wb") as f:
+            f.write(data)
+        np.savez_compressed(os.path.join(HERE, "alpha", name + ".npz"), **r)
+        manifest["alpha"][name] = dict(bytes=len(data), width=img.shape[1], height=img.shape[0], alph=hdr,
+                                       encoder=kw)
+        print(name, len(data), hdr, flush=True)
+    for name, src, fn in ALPHA_ERROR_CASES if "alpha" in sections else []:
+        data = edit_alph(open(os.path.join(HERE, "alpha", src + ".webp"), "rb").read(), fn)
+        st = decode_status(data)
+        _plain_c(False)
+        assert decode_status(data) == st, name
+        _plain_c(True)
+        with open(os.path.join(HERE, "alpha", name + ".webp"), "wb") as f:
+            f.write(data)
+        manifest["alpha_errors"] = manifest.get("alpha_errors", {})
+        manifest["alpha_errors"][name] = dict(source=src, status=st, bytes=len(data))
+        print(name, "status", st, flush=True)
+    for name, H, W, seeds, kw, gen in BENCH_CASES if "bench" in sections else []:
         for s in seeds:
             img = synth(H, W, s, 6) if gen == "synth6" else corr_luma(H, W, s)
             lossless = kw.get("lossless", 0)
@@ -360,4 +517,4 @@ def main():
 
 
 if __name__ == "__main__":
-    sys.exit(main())
+    sys.exit(main(sys.argv[1:]))

@@ -32,6 +32,7 @@ def oracle():
         L.oracle_transform_block.argtypes = [P, P, C.c_int]
         L.oracle_transform_block.restype = None
         L.oracle_vp8l_decode.argtypes = [P, P, P, P]
+        L.oracle_alpha_unfilter.argtypes = [C.c_int, C.c_int, C.c_int, P, P]
         _lib = L
     return _lib
 
@@ -94,3 +95,32 @@ def load_lossy(name):
 
 def bench_files(prefix):
     return sorted(glob.glob(os.path.join(GOLDEN, "bench", prefix + "_s*.webp")))
+
+
+def oracle_alpha_plane(data):
+    """CPU alpha plane of a lossy+ALPH file: host stage (webp_amd.alpha_parse), then for a
+    lossless stream the oracle's inverse transforms (alpha = green), then the oracle's
+    unfilter.  -> (AlphaInfo, (height, width) uint8)."""
+    import webp_amd
+
+    info, payload = webp_amd.alpha_parse(data)
+    if info.method == 0:
+        filtered = payload
+    else:
+        ll, argb, tdata = payload
+        filtered = np.ascontiguousarray(oracle_vp8l_decode(ll, argb, tdata)[..., 1])
+    out = np.empty((info.height, info.width), np.uint8)
+    assert oracle().oracle_alpha_unfilter(info.filter, info.width, info.height, filtered.ctypes.data,
+                                          out.ctypes.data) == 0
+    return info, out
+
+
+def alpha_names():
+    return sorted(manifest().get("alpha", {}))
+
+
+def load_alpha(name):
+    """(bytes, golden dict with 'rgba') of an ALPH fixture."""
+    d = os.path.join(GOLDEN, "alpha")
+    data = open(os.path.join(d, name + ".webp"), "rb").read()
+    return data, dict(np.load(os.path.join(d, name + ".npz")))

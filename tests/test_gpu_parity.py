@@ -115,11 +115,12 @@ def test_bad_frames_do_not_poison_batch(ctx):
     np.testing.assert_array_equal(outs[4], g["rgba"])
 
 
-def test_unsupported_formats_report_status(ctx):
-    """VP8+ALPH is a later SURVEY §8(f) row: reported, never silently wrong."""
-    al, _ = load_lossy("alpha_64x48")
-    _, status = ctx.decode_batch([al])
-    assert (status == webp_amd.Status.UNSUPPORTED_FEATURE).all()
+def test_lossy_alpha_frame_in_the_lossy_set(ctx):
+    """VP8+ALPH: the lossy set's alpha frame decodes to libwebp's RGBA."""
+    al, g = load_lossy("alpha_64x48")
+    outs, status = ctx.decode_batch([al])
+    assert (status == 0).all()
+    np.testing.assert_array_equal(outs[0], g["rgba"])
 
 
 def test_yuv_to_rgba_device_stage_vs_oracle():

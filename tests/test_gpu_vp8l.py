@@ -44,7 +44,7 @@ def test_c5_bench_frame_sha256(ctx):
     b.run()
     assert hashlib.sha256(b.rgba(2).tobytes()).hexdigest() == want  # idempotent re-run
     ms = b.kernel_ms()
-    assert ms[0] == 0 and ms[1] == 0 and ms[2] > 0
+    assert ms[0] == 0 and ms[1] == 0 and ms[2] > 0 and ms[3] == 0
     b.close()
 
 
