@@ -16,16 +16,24 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = {"vp8_recon_filter_kernel": "vp8_recon_filter_kernel", "yuv_to_rgba_kernel": "yuv_to_rgba_kernel"}
+KERNELS = {k: k for k in ("vp8_recon_filter_kernel", "yuv_to_rgba_kernel", "vp8l_transforms_kernel", "alpha_kernel")}
 
 
 def per_kernel(d):
-    acc = collections.defaultdict(list)
+    """Averages over the kernel's launches at its largest grid (the workload's batch; the
+    bench also runs small sanity batches)."""
+    rows = collections.defaultdict(list)
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             for key in KERNELS:
                 if key in r["Kernel_Name"]:
-                    acc[(key, r["Counter_Name"])].append(float(r["Counter_Value"]))
+                    rows[key].append((int(r["Grid_Size"]), r["Counter_Name"], float(r["Counter_Value"])))
+    acc = collections.defaultdict(list)
+    for key, rs in rows.items():
+        top = max(g for g, _, _ in rs)
+        for g, name, v in rs:
+            if g == top:
+                acc[(key, name)].append(v)
     out = {}
     for key in KERNELS:
         fetch = acc.get((key, "FETCH_SIZE"))
