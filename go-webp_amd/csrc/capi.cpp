@@ -23,6 +23,7 @@
 using wg::FrameDesc;
 using wg::LLDesc;
 using wg::AlphaDesc;
+using wg::AnimFrameDesc;
 using wg::MbRec;
 
 struct wg_ctx {
@@ -674,6 +675,126 @@ int wg_decode_rgba_into(const uint8_t* data, size_t size, uint8_t* rgba, size_t 
   int32_t fs[1] = {0};
   st = wg_decode_rgba_batch(ctx, d, s, 1, o, str, fs, flags);
   return st != WG_STATUS_OK ? st : fs[0];
+}
+
+int wg_anim_demux(const uint8_t* data, size_t size, wg_anim_info* info, wg_anim_frame* frames, int max_frames) {
+  if (data == nullptr || info == nullptr) return WG_STATUS_INVALID_PARAM;
+  wg::AnimInfo ai;
+  std::vector<wg::AnimFrame> fr;
+  std::memset(info, 0, sizeof(*info));
+  const int st = wg::anim_demux(data, size, &ai, &fr);
+  if (st != WG_STATUS_OK) return st;
+  info->canvas_width = (uint32_t)ai.canvas_width;
+  info->canvas_height = (uint32_t)ai.canvas_height;
+  info->loop_count = (uint32_t)ai.loop_count;
+  info->bgcolor = ai.bgcolor;
+  info->frame_count = (uint32_t)ai.frame_count;
+  for (int i = 0; frames && i < std::min(max_frames, ai.frame_count); ++i) {
+    const wg::AnimFrame& f = fr[(size_t)i];
+    wg_anim_frame& o = frames[i];
+    o.x_offset = f.x_offset;
+    o.y_offset = f.y_offset;
+    o.width = f.width;
+    o.height = f.height;
+    o.duration = f.duration;
+    o.dispose_background = f.dispose_bg;
+    o.no_blend = f.no_blend;
+    o.has_alpha = f.has_alpha;
+    o.fragment_offset = f.off;
+    o.fragment_size = f.size;
+  }
+  return WG_STATUS_OK;
+}
+
+int wg_anim_decode(wg_ctx* ctx, const uint8_t* data, size_t size, uint8_t* canvases, int32_t* timestamps,
+                   int32_t flags) {
+  if (!ctx || !data || !canvases || !timestamps) return WG_STATUS_INVALID_PARAM;
+  wg::AnimInfo ai;
+  std::vector<wg::AnimFrame> fr;
+  int st = wg::anim_demux(data, size, &ai, &fr);
+  if (st != WG_STATUS_OK) return st;
+  const int n = ai.frame_count;
+  // every frame's fragment decodes as one batch (K1..K4)
+  std::vector<const uint8_t*> ptrs((size_t)n);
+  std::vector<size_t> sizes((size_t)n);
+  std::vector<int32_t> status((size_t)n, 0);
+  for (int i = 0; i < n; ++i) {
+    ptrs[(size_t)i] = data + fr[(size_t)i].off;
+    sizes[(size_t)i] = fr[(size_t)i].size;
+  }
+  wg_batch* b = wg_batch_create(ctx, ptrs.data(), sizes.data(), n, flags, status.data());
+  if (!b) {
+    for (int i = 0; i < n; ++i)
+      if (status[(size_t)i] != WG_STATUS_OK) return status[(size_t)i];
+    return WG_STATUS_OUT_OF_MEMORY;
+  }
+  for (int i = 0; i < n; ++i) {
+    if (status[(size_t)i] != WG_STATUS_OK) {
+      wg_batch_destroy(b);
+      return status[(size_t)i];
+    }
+    if (b->desc[(size_t)i].width != fr[(size_t)i].width || b->desc[(size_t)i].height != fr[(size_t)i].height) {
+      wg_batch_destroy(b);
+      return WG_STATUS_BITSTREAM_ERROR;
+    }
+  }
+  st = wg_batch_run(b, nullptr);
+  // frame descriptors: IsKeyFrame (anim_decode.go:183-197) and the blend / dispose flags
+  std::vector<AnimFrameDesc> fd((size_t)n);
+  int32_t t = 0;
+  bool prev_key = false;
+  auto full = [&](const wg::AnimFrame& f) { return f.width == ai.canvas_width && f.height == ai.canvas_height; };
+  for (int i = 0; i < n; ++i) {
+    const wg::AnimFrame& f = fr[(size_t)i];
+    bool key;
+    if (i == 0) key = true;
+    else if ((!f.has_alpha || f.no_blend) && full(f)) key = true;
+    else key = fr[(size_t)i - 1].dispose_bg && (full(fr[(size_t)i - 1]) || prev_key);
+    AnimFrameDesc& d = fd[(size_t)i];
+    d.rgba = b->desc[(size_t)i].rgba;
+    d.x = f.x_offset;
+    d.y = f.y_offset;
+    d.width = f.width;
+    d.height = f.height;
+    d.key = key;
+    d.blend = i > 0 && !f.no_blend && !key;
+    d.dispose_bg = f.dispose_bg;
+    if (i > 0) {
+      const wg::AnimFrame& p = fr[(size_t)i - 1];
+      d.prev_dispose_bg = p.dispose_bg;
+      d.px = p.x_offset;
+      d.py = p.y_offset;
+      d.pw = p.width;
+      d.ph = p.height;
+    }
+    prev_key = key;
+    t += f.duration;
+    timestamps[i] = t;
+  }
+  const size_t canvas_bytes = (size_t)ai.canvas_width * ai.canvas_height * 4;
+  AnimFrameDesc* d_fd = nullptr;
+  uint8_t* d_canvases = nullptr;
+  {
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    hipSetDevice(ctx->device);
+    hipError_t e = st == WG_STATUS_OK ? hipSuccess : hipErrorUnknown;
+    if (e == hipSuccess) e = hipMalloc(&d_fd, sizeof(AnimFrameDesc) * (size_t)n);
+    if (e == hipSuccess) e = hipMalloc(&d_canvases, canvas_bytes * (size_t)n);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(d_fd, fd.data(), sizeof(AnimFrameDesc) * (size_t)n, hipMemcpyHostToDevice, ctx->stream);
+    if (e == hipSuccess)
+      e = wg::launch_anim_compose(d_fd, n, d_canvases, ai.canvas_width, ai.canvas_height, ctx->stream);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(canvases, d_canvases, canvas_bytes * (size_t)n, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    int err = 0;
+    if (e == hipSuccess) e = hipMemcpy(&err, b->d_err, sizeof(int), hipMemcpyDeviceToHost);
+    if (st == WG_STATUS_OK && (e != hipSuccess || err)) st = WG_STATUS_USER_ABORT;
+    if (d_fd) hipFree(d_fd);
+    if (d_canvases) hipFree(d_canvases);
+  }
+  wg_batch_destroy(b);
+  return st;
 }
 
 int wg_yuv420_to_rgba_device(const uint8_t* y, const uint8_t* u, const uint8_t* v, int y_stride, int uv_stride,

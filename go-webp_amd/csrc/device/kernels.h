@@ -32,4 +32,9 @@ hipError_t launch_vp8l_transforms(const LLDesc* d_frames, const int* group_count
 // plane; runs after K2 and K3.
 hipError_t launch_alpha(const AlphaDesc* d_frames, int n_frames, hipStream_t stream);
 
+// K5: animation canvases (frames in display order, already decoded) -> n_frames canvases of
+// canvas_w x canvas_h RGBA.
+hipError_t launch_anim_compose(const AnimFrameDesc* d_frames, int n_frames, uint8_t* d_canvases, int canvas_w,
+                               int canvas_h, hipStream_t stream);
+
 }  // namespace wg

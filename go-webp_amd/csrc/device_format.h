@@ -92,4 +92,16 @@ struct AlphaDesc {
 };
 static_assert(sizeof(AlphaDesc) == 64, "AlphaDesc must be 64 bytes");
 
+// One frame of an animation for K5 (anim.hip), in display order.
+struct AnimFrameDesc {
+  const uint8_t* rgba;     // the frame's decoded RGBA (width x height, stride 4*width)
+  int32_t x, y, width, height;
+  int32_t key;             // IsKeyFrame: start from a transparent canvas
+  int32_t blend;           // frame > 1, blend method BLEND and not a key frame
+  int32_t prev_dispose_bg; // the previous frame disposes to background: no blend inside its rectangle
+  int32_t dispose_bg;      // this frame disposes to background
+  int32_t px, py, pw, ph;  // the previous frame's rectangle
+};
+static_assert(sizeof(AnimFrameDesc) == 56, "AnimFrameDesc must be 56 bytes");
+
 }  // namespace wg

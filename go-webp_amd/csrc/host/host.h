@@ -57,6 +57,19 @@ struct VP8LFrame {
 // Entropy-decode a VP8L bitstream (the VP8L chunk payload).
 int vp8l_parse(const uint8_t* data, size_t size, VP8LFrame* out);
 
+// Animation demux (demux/demux.go): canvas + frames in display order.  A still image is a
+// one-frame animation.  Status: OK, NOT_ENOUGH_DATA (truncated), BITSTREAM_ERROR (invalid).
+struct AnimInfo {
+  int canvas_width = 0, canvas_height = 0, loop_count = 0, frame_count = 0;
+  uint32_t bgcolor = 0;
+};
+struct AnimFrame {
+  int x_offset = 0, y_offset = 0, width = 0, height = 0, duration = 0;
+  int dispose_bg = 0, no_blend = 0, has_alpha = 0;
+  size_t off = 0, size = 0;  // the frame's fragment (ALPH + image chunk, or the whole bitstream)
+};
+int anim_demux(const uint8_t* data, size_t size, AnimInfo* info, std::vector<AnimFrame>* frames);
+
 // ALPH chunk (alpha_dec.go:47-105): header byte = method (bits 0-1: 0 raw, 1 lossless),
 // filter (2-3: none, horizontal, vertical, gradient), pre-processing (4-5), reserved (6-7).
 struct AlphaHeader {

@@ -63,6 +63,19 @@ class VP8Info(C.Structure):
                 ("frame_offset", C.c_int32)]
 
 
+class AnimInfo(C.Structure):
+    """wg_anim_info = WebPAnimInfo."""
+    _fields_ = [("canvas_width", C.c_uint32), ("canvas_height", C.c_uint32), ("loop_count", C.c_uint32),
+                ("bgcolor", C.c_uint32), ("frame_count", C.c_uint32), ("pad", C.c_uint32 * 4)]
+
+
+class AnimFrame(C.Structure):
+    """wg_anim_frame: one frame as the demux iterator describes it."""
+    _fields_ = [("x_offset", C.c_int32), ("y_offset", C.c_int32), ("width", C.c_int32), ("height", C.c_int32),
+                ("duration", C.c_int32), ("dispose_background", C.c_int32), ("no_blend", C.c_int32),
+                ("has_alpha", C.c_int32), ("fragment_offset", C.c_uint64), ("fragment_size", C.c_uint64)]
+
+
 class AlphaInfo(C.Structure):
     """wg_alpha_info: the ALPH chunk of a lossy frame."""
     _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("method", C.c_int32), ("filter", C.c_int32),
@@ -110,6 +123,8 @@ _SIGS = {
     "wg_vp8_parse": (C.c_int, [_P, C.c_size_t, C.c_int, C.POINTER(VP8Info), _P]),
     "wg_vp8l_parse": (C.c_int, [_P, C.c_size_t, C.POINTER(VP8LInfo), _P, _P]),
     "wg_alpha_parse": (C.c_int, [_P, C.c_size_t, _P, _P, _P, _P, _P]),
+    "wg_anim_demux": (C.c_int, [_P, C.c_size_t, _P, _P, C.c_int]),
+    "wg_anim_decode": (C.c_int, [_P, _P, C.c_size_t, _P, _P, C.c_int32]),
 }
 EXPORTED = tuple(_SIGS)
 
@@ -242,6 +257,22 @@ def alpha_parse(data):
     return info, (ll, argb, tdata)
 
 
+def anim_demux(data):
+    """Host demux (WebPDemux + frame iterator): (AnimInfo, [AnimFrame]); a still image is one
+    frame.  frame.fragment_offset / fragment_size delimit its standalone bitstream."""
+    b = _buf(data)
+    info = AnimInfo()
+    L = lib()
+    st = L.wg_anim_demux(b, len(b), C.byref(info), None, 0)
+    if st != Status.OK:
+        raise WebPError(st, "wg_anim_demux")
+    frames = (AnimFrame * max(1, info.frame_count))()
+    st = L.wg_anim_demux(b, len(b), C.byref(info), frames, info.frame_count)
+    if st != Status.OK:
+        raise WebPError(st, "wg_anim_demux")
+    return info, list(frames)[:info.frame_count]
+
+
 def _ptr_arrays(datas):
     bufs = [_buf(d) for d in datas]
     n = len(bufs)
@@ -339,6 +370,18 @@ class Context:
 
     def batch(self, datas, flags=0):
         return Batch(self, datas, flags)
+
+    def decode_anim(self, data, flags=0):
+        """Whole animation -> (canvases (frames, H, W, 4) uint8 RGBA, timestamps int32 ms), as
+        the WebPAnimDecoderGetNext loop returns them."""
+        info, _ = anim_demux(data)
+        b = _buf(data)
+        canv = np.empty((info.frame_count, info.canvas_height, info.canvas_width, 4), np.uint8)
+        ts = np.empty(info.frame_count, np.int32)
+        st = lib().wg_anim_decode(self._h, b, len(b), canv.ctypes.data, ts.ctypes.data, flags)
+        if st != Status.OK:
+            raise WebPError(st, "wg_anim_decode")
+        return canv, ts
 
     def decode_batch(self, datas, flags=0, out=None):
         """Decode a list of WebP files; returns (list of RGBA arrays or None, status array).

@@ -201,6 +201,38 @@ typedef struct {
 int wg_alpha_parse(const uint8_t* data, size_t size, wg_alpha_info* info, uint8_t* filtered,
                    wg_vp8l_info* ll_info, uint32_t* argb, uint32_t* const* transform_data);
 
+/* ---- animation (ANIM / ANMF) --------------------------------------------------------- */
+/* WebPAnimInfo (reference pkg/libwebp/webp/demux.go:124-131). */
+typedef struct {
+  uint32_t canvas_width, canvas_height, loop_count, bgcolor, frame_count;
+  uint32_t pad[4];
+} wg_anim_info;
+
+/* One frame as WebPDemuxGetFrame's iterator describes it (demux.go SynthesizeFrame): its
+ * rectangle on the canvas (size from the frame's bitstream), duration, disposal / blending and
+ * its fragment -- the bytes from its ALPH chunk (if any) to the end of its image chunk, which
+ * decode as a standalone input. */
+typedef struct {
+  int32_t x_offset, y_offset, width, height, duration;
+  int32_t dispose_background;   /* WEBP_MUX_DISPOSE_BACKGROUND                              */
+  int32_t no_blend;             /* WEBP_MUX_NO_BLEND                                        */
+  int32_t has_alpha;
+  uint64_t fragment_offset, fragment_size;
+} wg_anim_frame;
+
+/* Host-only demux (WebPDemux + WebPDemuxGetFrame): a still image is a one-frame animation.
+ * Fills info and up to max_frames frames (frames may be NULL).  BITSTREAM_ERROR for an invalid
+ * container, NOT_ENOUGH_DATA for truncated data. */
+int wg_anim_demux(const uint8_t* data, size_t size, wg_anim_info* info, wg_anim_frame* frames, int max_frames);
+
+/* Decode every frame of an animation and composite the canvases on the device (replaces the
+ * WebPAnimDecoderNew + WebPAnimDecoderGetNext loop, anim_decode.go:66-433; MODE_RGBA).
+ * canvases: frame_count * canvas_height * canvas_width * 4 bytes (stride 4 * canvas_width);
+ * timestamps: frame_count ints (ms, end of each frame, as GetNext reports).  The frames decode
+ * as one batch (K1..K4), then K5 composites.  Returns the first failing frame's status. */
+int wg_anim_decode(wg_ctx* ctx, const uint8_t* data, size_t size, uint8_t* canvases, int32_t* timestamps,
+                   int32_t flags);
+
 #ifdef __cplusplus
 }  /* extern "C" */
 #endif

@@ -22,7 +22,7 @@ frames (SURVEY.md §8(d), Appendix B generators) are stored as ``.webp`` plus
 SHA-256 of their decodes in ``manifest.json``.  Every decode is also checked
 against libwebp's SIMD path (must be byte-identical) before it is written.
 
-Usage:  python tests/golden/make_golden.py [lossy|lossless|alpha|bench ...]
+Usage:  python tests/golden/make_golden.py [lossy|lossless|alpha|anim|bench ...]
         (rewrites tests/golden/<section>/; default all sections)
 """
 import ctypes as C
@@ -358,6 +358,211 @@ ALPHA_ERROR_CASES = [
 ]
 
 
+# ----------------------------------------------------------------------------- animation
+DEMUX_ABI = 0x0107  # WEBP_DEMUX_ABI_VERSION of 1.6.0
+MUX_ABI = 0x0109    # WEBP_MUX_ABI_VERSION of 1.6.0
+
+
+def _load_anim_libs():
+    mux = C.CDLL(glob.glob(PIL_LIBS + "libwebpmux-*.so*")[0])
+    dmx = C.CDLL(glob.glob(PIL_LIBS + "libwebpdemux-*.so*")[0])
+    mux.WebPAnimEncoderNewInternal.restype = C.c_void_p
+    mux.WebPAnimEncoderNewInternal.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_int]
+    mux.WebPAnimEncoderAdd.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
+    mux.WebPAnimEncoderAssemble.argtypes = [C.c_void_p, C.c_void_p]
+    mux.WebPAnimEncoderDelete.argtypes = [C.c_void_p]
+    dmx.WebPAnimDecoderNewInternal.restype = C.c_void_p
+    dmx.WebPAnimDecoderNewInternal.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+    dmx.WebPAnimDecoderGetInfo.argtypes = [C.c_void_p, C.c_void_p]
+    dmx.WebPAnimDecoderHasMoreFrames.argtypes = [C.c_void_p]
+    dmx.WebPAnimDecoderGetNext.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    dmx.WebPAnimDecoderDelete.argtypes = [C.c_void_p]
+    return mux, dmx
+
+
+class WebPData(C.Structure):
+    _fields_ = [("bytes", C.c_void_p), ("size", C.c_size_t)]
+
+
+def _picture(img):
+    h, w, ch = img.shape
+    pic = (C.c_uint8 * 512)()
+    assert LIB.WebPPictureInitInternal(pic, ABI)
+    pi = C.cast(pic, C.POINTER(C.c_int32))
+    pi[0] = 1
+    pi[2] = w
+    pi[3] = h
+    buf = np.ascontiguousarray(img)
+    ok = (LIB.WebPPictureImportRGBA if ch == 4 else LIB.WebPPictureImportRGB)(pic, buf.ctypes.data_as(C.c_void_p),
+                                                                             w * ch)
+    assert ok
+    return pic
+
+
+def _config(lossless, quality=75.0):
+    cfg = (C.c_int32 * 64)()
+    assert LIB.WebPConfigInitInternal(cfg, 0, C.c_float(quality), ABI)
+    cfg[0] = lossless
+    C.cast(cfg, C.POINTER(C.c_float))[1] = quality
+    assert LIB.WebPValidateConfig(cfg)
+    return cfg
+
+
+def anim_encode(frames, durations, lossless_flags, allow_mixed=1, kmax=0, loop=0, bgcolor=0xffffffff):
+    """WebPAnimEncoder over full-canvas frames (it picks sub-rectangles, blend and dispose)."""
+    mux, _ = _load_anim_libs()
+    h, w = frames[0].shape[:2]
+    opt = (C.c_int32 * 16)()
+    assert mux.WebPAnimEncoderOptionsInitInternal(opt, MUX_ABI)
+    opt[0] = C.c_int32(bgcolor - (1 << 32) if bgcolor >= 1 << 31 else bgcolor).value  # anim_params.bgcolor
+    opt[1] = loop                     # anim_params.loop_count
+    opt[3] = 0 if kmax == 0 else max(1, kmax - 1)  # kmin
+    opt[4] = kmax                     # kmax
+    opt[5] = allow_mixed
+    enc = mux.WebPAnimEncoderNewInternal(w, h, opt, MUX_ABI)
+    assert enc
+    t = 0
+    for img, d, ll in zip(frames, durations, lossless_flags):
+        pic = _picture(img)
+        assert mux.WebPAnimEncoderAdd(enc, pic, t, _config(ll)), "AnimEncoderAdd"
+        LIB.WebPPictureFree(pic)
+        t += d
+    assert mux.WebPAnimEncoderAdd(enc, None, t, None)
+    data = WebPData()
+    assert mux.WebPAnimEncoderAssemble(enc, C.byref(data))
+    out = C.string_at(data.bytes, data.size)
+    LIB.WebPFree(C.c_void_p(data.bytes))
+    mux.WebPAnimEncoderDelete(enc)
+    return out
+
+
+def image_chunks(data):
+    """The ALPH / VP8 / VP8L chunks (header + padded payload) of a still image file."""
+    return b"".join(t + len(pl).to_bytes(4, "little") + pl + (b"\0" if len(pl) & 1 else b"")
+                    for t, pl in riff_chunks(data) if t in (b"ALPH", b"VP8 ", b"VP8L"))
+
+
+def anim_build(canvas_w, canvas_h, frames, loop=0, bgcolor=0xffffffff):
+    """Hand-built animation: frames = [(encoded still, x, y, duration, dispose_bg, no_blend)]."""
+    has_alpha = any(b"ALPH" in f[0] or b"VP8L" in f[0] for f in frames)
+    vp8x = bytes([0x02 | (0x10 if has_alpha else 0), 0, 0, 0]) + (canvas_w - 1).to_bytes(3, "little") + \
+        (canvas_h - 1).to_bytes(3, "little")
+    chunks = [(b"VP8X", vp8x), (b"ANIM", bgcolor.to_bytes(4, "little") + loop.to_bytes(2, "little"))]
+    for data, x, y, dur, dispose_bg, no_blend in frames:
+        assert x % 2 == 0 and y % 2 == 0
+        fw, fh = None, None
+        for t, pl in riff_chunks(data):
+            if t == b"VP8X":
+                fw, fh = 1 + int.from_bytes(pl[4:7], "little"), 1 + int.from_bytes(pl[7:10], "little")
+        if fw is None:
+            t, pl = riff_chunks(data)[0]
+            if t == b"VP8 ":
+                fw, fh = int.from_bytes(pl[6:8], "little") & 0x3fff, int.from_bytes(pl[8:10], "little") & 0x3fff
+            else:
+                v = int.from_bytes(pl[1:5], "little")
+                fw, fh = (v & 0x3fff) + 1, ((v >> 14) & 0x3fff) + 1
+        hdr = (x // 2).to_bytes(3, "little") + (y // 2).to_bytes(3, "little") + (fw - 1).to_bytes(3, "little") + \
+            (fh - 1).to_bytes(3, "little") + dur.to_bytes(3, "little") + bytes([(1 if dispose_bg else 0) |
+                                                                                 (2 if no_blend else 0)])
+        chunks.append((b"ANMF", hdr + image_chunks(data)))
+    return riff_build(chunks)
+
+
+def anim_decode(data):
+    """WebPAnimDecoder (MODE_RGBA): (info dict, canvases (F, H, W, 4), timestamps)."""
+    _, dmx = _load_anim_libs()
+    opt = (C.c_int32 * 9)()
+    assert dmx.WebPAnimDecoderOptionsInitInternal(opt, DEMUX_ABI)
+    opt[0] = MODE_RGBA
+    wd = WebPData(C.cast(C.c_char_p(data), C.c_void_p).value, len(data))
+    dec = dmx.WebPAnimDecoderNewInternal(C.byref(wd), opt, DEMUX_ABI)
+    assert dec, "WebPAnimDecoderNew failed"
+    info = (C.c_uint32 * 9)()
+    assert dmx.WebPAnimDecoderGetInfo(dec, info)
+    w, h = info[0], info[1]
+    frames, ts = [], []
+    while dmx.WebPAnimDecoderHasMoreFrames(dec):
+        buf, t = C.c_void_p(), C.c_int()
+        assert dmx.WebPAnimDecoderGetNext(dec, C.byref(buf), C.byref(t))
+        frames.append(np.frombuffer(C.string_at(buf, w * h * 4), np.uint8).reshape(h, w, 4).copy())
+        ts.append(t.value)
+    dmx.WebPAnimDecoderDelete(dec)
+    return (dict(canvas_width=w, canvas_height=h, loop_count=info[2], bgcolor=info[3], frame_count=info[4]),
+            np.stack(frames), np.array(ts, np.int32))
+
+
+def moving_scene(H, W, n, seed, alpha=False):
+    """n full-canvas frames: a textured background with a square moving across it; with
+    alpha, the background is partly transparent and the square semi-transparent."""
+    rng = np.random.default_rng(seed)
+    base = synth(H, W, seed, 4)
+    out = []
+    for i in range(n):
+        img = base.copy()
+        s = max(4, min(H, W) // 4)
+        y0, x0 = (i * 5) % (H - s), (i * 9) % (W - s)
+        img[y0:y0 + s, x0:x0 + s] = (40 * i % 256, 200, 90)
+        if alpha:
+            a = np.full((H, W, 1), 255, np.uint8)
+            a[: H // 3, :] = 0
+            a[y0:y0 + s, x0:x0 + s] = 128 + 20 * i % 100
+            a[H // 2:, : W // 3] = rng.integers(0, 256, (H - H // 2, W // 3, 1))
+            img = np.concatenate([img, a], -1)
+        out.append(img)
+    return out
+
+
+def sprite(h, w, seed, alpha_kind):
+    rng = np.random.default_rng(seed)
+    img = synth(h, w, seed, 10)
+    a = {"opaque": np.full((h, w), 255), "half": np.full((h, w), 128), "mixed": rng.integers(0, 256, (h, w)),
+         "holes": np.where((np.arange(w)[None, :] // 3 + np.arange(h)[:, None] // 3) % 2 == 0, 255, 0)}[alpha_kind]
+    return np.concatenate([img, a.astype(np.uint8)[..., None]], -1)
+
+
+def _manual_anims():
+    lossy_full = encode(synth(48, 64, 50, 6))
+    ll_sprite = encode(sprite(20, 30, 51, "mixed"), lossless=1, exact=1)
+    lossy_alpha_sprite = encode(sprite(16, 16, 52, "half"))
+    ll_holes = encode(sprite(30, 40, 53, "holes"), lossless=1, exact=1)
+    ll_full_alpha = encode(sprite(48, 64, 54, "mixed"), lossless=1, exact=1)
+    lossy_sprite = encode(synth(12, 18, 55, 6))
+    return {
+        # blend over dispose-none, blend over dispose-background (blend only outside the previous
+        # rectangle), an opaque sub-frame, a full no-blend frame, dispose of a full frame
+        "anim_manual_blend_dispose": anim_build(64, 48, [
+            (lossy_full, 0, 0, 100, False, False),
+            (ll_sprite, 10, 8, 50, False, False),
+            (lossy_alpha_sprite, 20, 10, 70, True, False),
+            (ll_holes, 0, 0, 40, False, False),
+            (lossy_sprite, 40, 30, 30, True, True),
+            (ll_full_alpha, 0, 0, 60, True, True),
+            (ll_sprite, 34, 28, 20, False, False),
+        ], loop=3, bgcolor=0xff336699),
+        # key-frame rules: a no-blend full frame with alpha, a frame after a full dispose-background
+        "anim_manual_keyframes": anim_build(64, 48, [
+            (ll_sprite, 4, 4, 10, True, False),
+            (ll_full_alpha, 0, 0, 10, False, True),
+            (lossy_alpha_sprite, 2, 2, 10, False, False),
+            (ll_full_alpha, 0, 0, 10, True, False),
+            (ll_holes, 12, 6, 10, False, False),
+        ]),
+        "anim_manual_single": anim_build(30, 20, [(ll_sprite, 0, 0, 0, False, False)], loop=1),
+    }
+
+
+ANIM_CASES = [
+    # name, builder
+    ("anim_enc_mixed_96x80", lambda: anim_encode(moving_scene(80, 96, 8, 60), [40] * 8, [0, 1, 0, 0, 1, 0, 0, 1])),
+    ("anim_enc_alpha_lossless_72x56", lambda: anim_encode(moving_scene(56, 72, 6, 61, alpha=True),
+                                                         [30, 60, 30, 60, 30, 60], [1] * 6)),
+    ("anim_enc_alpha_lossy_80x64", lambda: anim_encode(moving_scene(64, 80, 6, 62, alpha=True), [25] * 6, [0] * 6,
+                                                      allow_mixed=0)),
+    ("anim_enc_keyframes_64x64", lambda: anim_encode(moving_scene(64, 64, 9, 63, alpha=True), [20] * 9,
+                                                    [0, 1] * 4 + [0], kmax=3)),
+]
+
+
 # ----------------------------------------------------------------------------- cases
 LOSSY_CASES = [
     # name, image-fn, encoder kwargs
@@ -435,7 +640,7 @@ def sha(a):
 def main(argv):
     """argv: sections to (re)generate among lossy, lossless, alpha, bench (default: all);
     the manifest entries of the other sections are kept."""
-    sections = set(argv) or {"lossy", "lossless", "alpha", "bench"}
+    sections = set(argv) or {"lossy", "lossless", "alpha", "anim", "bench"}
     os.makedirs(os.path.join(HERE, "lossy"), exist_ok=True)
     os.makedirs(os.path.join(HERE, "lossless"), exist_ok=True)
     os.makedirs(os.path.join(HERE, "bench"), exist_ok=True)
@@ -497,6 +702,29 @@ def main(argv):
         manifest["alpha_errors"] = manifest.get("alpha_errors", {})
         manifest["alpha_errors"][name] = dict(source=src, status=st, bytes=len(data))
         print(name, "status", st, flush=True)
+    if "anim" in sections:
+        os.makedirs(os.path.join(HERE, "anim"), exist_ok=True)
+        builders = list(ANIM_CASES) + [(k, (lambda v=v: v)) for k, v in _manual_anims().items()]
+        for name, build in builders:
+            data = build()
+            info, canv, ts = anim_decode(data)
+            _plain_c(False)
+            _, canv_simd, ts_simd = anim_decode(data)
+            _plain_c(True)
+            assert np.array_equal(canv, canv_simd) and np.array_equal(ts, ts_simd), name
+            with open(os.path.join(HERE, "anim", name + ".webp"), "wb") as f:
+                f.write(data)
+            np.savez_compressed(os.path.join(HERE, "anim", name + ".npz"), canvases=canv, timestamps=ts)
+            flags = []
+            for t, pl in riff_chunks(data):
+                if t == b"ANMF":
+                    flags.append(dict(x=2 * int.from_bytes(pl[0:3], "little"), y=2 * int.from_bytes(pl[3:6], "little"),
+                                      w=1 + int.from_bytes(pl[6:9], "little"), h=1 + int.from_bytes(pl[9:12], "little"),
+                                      duration=int.from_bytes(pl[12:15], "little"), dispose_bg=pl[15] & 1,
+                                      no_blend=(pl[15] >> 1) & 1, alpha=b"ALPH" in pl or b"VP8L" in pl))
+            manifest["anim"][name] = dict(bytes=len(data), info=info, frames=flags)
+            print(name, len(data), info, [(f["x"], f["y"], f["w"], f["h"], f["dispose_bg"], f["no_blend"])
+                                          for f in flags], flush=True)
     for name, H, W, seeds, kw, gen in BENCH_CASES if "bench" in sections else []:
         for s in seeds:
             img = synth(H, W, s, 6) if gen == "synth6" else corr_luma(H, W, s)

@@ -33,6 +33,7 @@ def oracle():
         L.oracle_transform_block.restype = None
         L.oracle_vp8l_decode.argtypes = [P, P, P, P]
         L.oracle_alpha_unfilter.argtypes = [C.c_int, C.c_int, C.c_int, P, P]
+        L.oracle_anim_compose.argtypes = [P, C.c_int, C.c_int, C.c_int, P, P]
         _lib = L
     return _lib
 
@@ -122,5 +123,58 @@ def alpha_names():
 def load_alpha(name):
     """(bytes, golden dict with 'rgba') of an ALPH fixture."""
     d = os.path.join(GOLDEN, "alpha")
+    data = open(os.path.join(d, name + ".webp"), "rb").read()
+    return data, dict(np.load(os.path.join(d, name + ".npz")))
+
+
+def oracle_still_rgba(data):
+    """CPU RGBA of a still bitstream (whole file or an animation frame's fragment) with the
+    oracles: lossless -> vp8l oracle; lossy -> lossy oracle, A from the ALPH oracle if present."""
+    import webp_amd
+
+    if webp_amd.features(data).format == 2:
+        info, argb, tdata = webp_amd.vp8l_parse(data)
+        return oracle_vp8l_decode(info, argb, tdata)
+    info, mbs = webp_amd.vp8_parse(data)
+    rgba = oracle_decode(info, mbs)["rgba"]
+    try:
+        rgba[..., 3] = oracle_alpha_plane(data)[1]
+    except webp_amd.WebPError as e:
+        if e.status != webp_amd.Status.UNSUPPORTED_FEATURE:
+            raise
+    return rgba
+
+
+class _OFrame(C.Structure):
+    _fields_ = [("rgba", C.c_void_p), ("x", C.c_int), ("y", C.c_int), ("width", C.c_int), ("height", C.c_int),
+                ("duration", C.c_int), ("dispose_bg", C.c_int), ("no_blend", C.c_int), ("has_alpha", C.c_int)]
+
+
+def oracle_anim(data):
+    """CPU animation decode: host demux, oracle decode of every fragment, oracle compositing.
+    -> (canvases (F, H, W, 4), timestamps)."""
+    import webp_amd
+
+    info, frames = webp_amd.anim_demux(data)
+    stills = [np.ascontiguousarray(oracle_still_rgba(data[f.fragment_offset:f.fragment_offset + f.fragment_size]))
+              for f in frames]
+    of = (_OFrame * len(frames))()
+    for o, f, r in zip(of, frames, stills):
+        assert r.shape[:2] == (f.height, f.width)
+        o.rgba, o.x, o.y, o.width, o.height = r.ctypes.data, f.x_offset, f.y_offset, f.width, f.height
+        o.duration, o.dispose_bg, o.no_blend, o.has_alpha = f.duration, f.dispose_background, f.no_blend, f.has_alpha
+    canv = np.empty((len(frames), info.canvas_height, info.canvas_width, 4), np.uint8)
+    ts = np.empty(len(frames), np.int32)
+    assert oracle().oracle_anim_compose(of, len(frames), info.canvas_width, info.canvas_height, canv.ctypes.data,
+                                        ts.ctypes.data) == 0
+    return canv, ts
+
+
+def anim_names():
+    return sorted(manifest().get("anim", {}))
+
+
+def load_anim(name):
+    d = os.path.join(GOLDEN, "anim")
     data = open(os.path.join(d, name + ".webp"), "rb").read()
     return data, dict(np.load(os.path.join(d, name + ".npz")))
