@@ -56,6 +56,12 @@ struct FrameParse {
   const uint8_t* alpha_raw = nullptr;  // into the caller's input (valid during batch creation)
   size_t off_araw = 0, off_acoded = 0, off_atdata[4] = {0, 0, 0, 0};  // input buffer
   size_t off_ascratch = 0, off_argba = 0, off_aplane = 0;            // plane buffer
+  // output (cropping, f4): out_w x out_h, taken at (win_x, win_y) of the frame's RGBA buffer
+  // (rgba_w x rgba_h: the window itself for lossy frames, the whole frame for lossless)
+  int out_w = 0, out_h = 0, win_x = 0, win_y = 0, rgba_w = 0, rgba_h = 0;
+  bool cropped = false;
+  size_t off_yc = 0, off_uc = 0, off_vc = 0;  // cropped lossy planes (plane buffer)
+  int yc_stride = 0, uvc_stride = 0;
 };
 
 struct Timing {
@@ -141,6 +147,11 @@ struct wg_batch {
   LLDesc* d_lldesc = nullptr;
   AlphaDesc* d_adesc = nullptr;
   int n_lossy = 0, n_lossless = 0, n_alpha = 0, n_k3 = 0;
+  wg_decoder_options opt{};          // output colorspace, cropping, flip (f4)
+  bool any_crop = false;             // K2 reads compact cropped planes through desc2
+  std::vector<FrameDesc> desc2;
+  FrameDesc* d_desc2 = nullptr;
+  int max_out_w = 1, max_out_h = 1;
   int ll_groups[wg::kVP8LVariants] = {0, 0, 0, 0, 0};  // K3 frames per kernel variant
   int* d_err = nullptr;
   uint8_t* d_in = nullptr;
@@ -157,6 +168,14 @@ struct wg_batch {
 
 namespace {
 void fill_vp8l_info(const wg::VP8LFrame& f, wg_vp8l_info* info, uint32_t* argb, uint32_t* const* transform_data);
+// The single-frame entry points share one lazily created context on device 0.
+wg_ctx* default_ctx() {
+  static std::mutex mu;
+  static wg_ctx* ctx = nullptr;
+  std::lock_guard<std::mutex> lock(mu);
+  if (!ctx) ctx = wg_ctx_create(0, 1);
+  return ctx;
+}
 }  // namespace
 
 extern "C" {
@@ -286,6 +305,7 @@ void wg_batch_destroy(wg_batch* b) {
   if (b->d_desc) hipFree(b->d_desc);
   if (b->d_lldesc) hipFree(b->d_lldesc);
   if (b->d_adesc) hipFree(b->d_adesc);
+  if (b->d_desc2) hipFree(b->d_desc2);
   if (b->d_err) hipFree(b->d_err);
   if (b->d_in) hipFree(b->d_in);
   if (b->d_planes) hipFree(b->d_planes);
@@ -295,14 +315,75 @@ void wg_batch_destroy(wg_batch* b) {
 
 wg_batch* wg_batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t* sizes, int n, int32_t flags,
                           int32_t* status) {
-  if (!ctx || !data || !sizes || n <= 0) return nullptr;
+  wg_decoder_options o{};
+  o.colorspace = 1;  // MODE_RGBA
+  o.bypass_filtering = !!(flags & WG_FLAG_BYPASS_FILTERING);
+  o.no_fancy_upsampling = !!(flags & WG_FLAG_NO_FANCY_UPSAMPLING);
+  return wg_batch_create_ex(ctx, data, sizes, n, &o, status);
+}
+
+int wg_output_bpp(int colorspace) { return wg::output_bpp(colorspace); }
+
+wg_batch* wg_batch_create_ex(wg_ctx* ctx, const uint8_t* const* data, const size_t* sizes, int n,
+                             const wg_decoder_options* opt, int32_t* status) {
+  if (!ctx || !data || !sizes || n <= 0 || !opt) return nullptr;
   std::lock_guard<std::mutex> lock(ctx->mu);
   if (hipSetDevice(ctx->device) != hipSuccess) return nullptr;
   wg_batch* b = new wg_batch();
   b->ctx = ctx;
   b->n = n;
+  b->opt = *opt;
+  const int32_t flags = (opt->bypass_filtering ? WG_FLAG_BYPASS_FILTERING : 0) |
+                        (opt->no_fancy_upsampling ? WG_FLAG_NO_FANCY_UPSAMPLING : 0);
   b->flags = flags;
   parse_all(data, sizes, n, flags, ctx->host_threads, b->fp);
+  // output options (WebPIoInitFromOptions / WebPAllocateDecBuffer, webp.go): colorspace,
+  // scaling (disabled in the reference, io_dec.c.go:540-541), cropping (left/top snapped to
+  // even, WebPCheckCropDimensions -> INVALID_PARAM)
+  const int mode_status = wg::output_bpp(opt->colorspace) ? WG_STATUS_OK
+                          : (opt->colorspace == 11 || opt->colorspace == 12) ? WG_STATUS_UNSUPPORTED_FEATURE
+                                                                              : WG_STATUS_INVALID_PARAM;
+  for (int i = 0; i < n; ++i) {
+    FrameParse& f = b->fp[i];
+    if (f.status != WG_STATUS_OK) continue;
+    if (mode_status != WG_STATUS_OK) {
+      f.status = mode_status;
+      continue;
+    }
+    if (opt->use_scaling) {
+      f.status = WG_STATUS_UNSUPPORTED_FEATURE;
+      continue;
+    }
+    f.out_w = f.width;
+    f.out_h = f.height;
+    if (opt->use_cropping) {
+      // WebPAllocateDecBuffer checks the window with its origin snapped to even
+      // (buffer_dec.c.go:201-209); the decoder's window (WebPIoInitFromOptions, webp.go:922-945)
+      // snaps only for YUV sources: lossy frames use the snapped origin, lossless the exact one
+      const int cw = opt->crop_width, ch = opt->crop_height;
+      auto inside = [&](int x, int y) {
+        return x >= 0 && y >= 0 && cw > 0 && ch > 0 && x < f.width && y < f.height && cw <= f.width - x &&
+               ch <= f.height - y;
+      };
+      const int x = f.lossless ? opt->crop_left : (opt->crop_left & ~1);
+      const int y = f.lossless ? opt->crop_top : (opt->crop_top & ~1);
+      if (!inside(opt->crop_left & ~1, opt->crop_top & ~1) || !inside(x, y)) {
+        f.status = WG_STATUS_INVALID_PARAM;
+        continue;
+      }
+      f.cropped = x != 0 || y != 0 || cw != f.width || ch != f.height;
+      f.out_w = cw;
+      f.out_h = ch;
+      if (!f.lossless) {
+        f.win_x = f.win_y = 0;  // K2 writes the window itself
+      } else {
+        f.win_x = x;
+        f.win_y = y;
+      }
+    }
+    f.rgba_w = f.lossless ? f.width : f.out_w;
+    f.rgba_h = f.lossless ? f.height : f.out_h;
+  }
   // layout
   size_t in_b = 0, pl_b = 0, rg_b = 0;
   double k1 = 0, k2 = 0, k3 = 0, k4 = 0;
@@ -331,11 +412,13 @@ wg_batch* wg_batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t*
     if (status) status[i] = f.status;
     if (f.status != WG_STATUS_OK) continue;
     f.off_rgba = rg_b;
-    rg_b = align_up(rg_b + (size_t)f.width * f.height * 4);
+    rg_b = align_up(rg_b + (size_t)f.rgba_w * f.rgba_h * 4);
     b->max_w = std::max(b->max_w, f.width);
     b->max_h = std::max(b->max_h, f.height);
+    b->max_out_w = std::max(b->max_out_w, f.out_w);
+    b->max_out_h = std::max(b->max_out_h, f.out_h);
     b->n_valid++;
-    b->pixels += (int64_t)f.width * f.height;
+    b->pixels += (int64_t)f.out_w * f.out_h;
     const double px = (double)f.width * f.height;
     if (f.lossless) {
       b->n_lossless++;
@@ -359,11 +442,24 @@ wg_batch* wg_batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t*
     f.off_v = pl_b;
     pl_b = align_up(pl_b + nmb * 64);
     b->max_mb_w = std::max(b->max_mb_w, inf.mb_w);
+    if (f.cropped) {  // K2 reads the crop window from compact planes (copied after K1)
+      b->any_crop = true;
+      f.yc_stride = (f.out_w + 15) & ~15;
+      f.uvc_stride = ((((f.out_w + 1) >> 1) + 7) & ~7);
+      f.off_yc = pl_b;
+      pl_b = align_up(pl_b + (size_t)f.yc_stride * f.out_h);
+      f.off_uc = pl_b;
+      pl_b = align_up(pl_b + (size_t)f.uvc_stride * ((f.out_h + 1) >> 1));
+      f.off_vc = pl_b;
+      pl_b = align_up(pl_b + (size_t)f.uvc_stride * ((f.out_h + 1) >> 1));
+    }
     // algorithmic bytes: K1 reads records + coefficients, writes MB-padded
     // planes; K2 reads cropped planes, writes RGBA.
     const double uvpx = 2.0 * ((inf.width + 1) / 2) * (double)((inf.height + 1) / 2);
     k1 += (double)nmb * sizeof(MbRec) + inf.mb_h * 4.0 + f.sf.blocks.size() * 2.0 + nmb * 384.0;
-    k2 += px + uvpx + 4.0 * px;
+    const double opx = (double)f.out_w * f.out_h;
+    k2 += opx + 2.0 * ((f.out_w + 1) / 2) * (double)((f.out_h + 1) / 2) + 4.0 * opx;
+    (void)uvpx;
     if (f.alpha) {
       // K4 reads the filtered alpha (raw bytes, or K3's RGBA of the alpha stream) and
       // rewrites the RGBA A bytes (dword read-modify-write)
@@ -456,7 +552,7 @@ wg_batch* wg_batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t*
     d.rgba = b->d_rgba + f.off_rgba;
     d.width = f.width;
     d.height = f.height;
-    d.rgba_stride = 4 * f.width;
+    d.rgba_stride = 4 * f.rgba_w;
     if (f.lossless) {  // K1/K2 skip it (valid = 0); K3 gets an LLDesc
       b->lldesc.push_back(make_ll(f.lf, f.width, f.height, f.off_coded, f.off_tdata, f.off_scratch, d.rgba,
                                   d.rgba_stride));
@@ -497,6 +593,10 @@ wg_batch* wg_batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t*
       a.rgba_stride = d.rgba_stride;
       a.filter = f.ah.filter;
       a.valid = 1;
+      a.win_x = f.cropped ? (b->opt.crop_left & ~1) : 0;
+      a.win_y = f.cropped ? (b->opt.crop_top & ~1) : 0;
+      a.win_w = f.out_w;
+      a.win_h = f.out_h;
       b->adesc.push_back(a);
       f.alpha_raw = nullptr;
     }
@@ -505,7 +605,28 @@ wg_batch* wg_batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t*
     std::vector<int16_t>().swap(f.sf.blocks);
     std::vector<uint32_t>().swap(f.sf.row_block0);
   }
+  if (b->any_crop) {  // K2's view: cropped lossy frames read their compact planes
+    b->desc2 = b->desc;
+    for (int i = 0; i < n; ++i) {
+      FrameParse& f = b->fp[i];
+      FrameDesc& d2 = b->desc2[i];
+      if (f.status != WG_STATUS_OK || f.lossless || !f.cropped) continue;
+      d2.y = b->d_planes + f.off_yc;
+      d2.u = b->d_planes + f.off_uc;
+      d2.v = b->d_planes + f.off_vc;
+      d2.y_stride = f.yc_stride;
+      d2.uv_stride = f.uvc_stride;
+      d2.width = f.out_w;
+      d2.height = f.out_h;
+    }
+  }
   hipError_t e = hipMemcpyAsync(b->d_in, h_in, b->in_bytes, hipMemcpyHostToDevice, ctx->stream);
+  if (e == hipSuccess && b->any_crop) {
+    e = hipMalloc(&b->d_desc2, sizeof(FrameDesc) * (size_t)n);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(b->d_desc2, b->desc2.data(), sizeof(FrameDesc) * (size_t)n, hipMemcpyHostToDevice,
+                         ctx->stream);
+  }
   if (e == hipSuccess)
     e = hipMemcpyAsync(b->d_desc, b->desc.data(), sizeof(FrameDesc) * (size_t)n, hipMemcpyHostToDevice,
                        ctx->stream);
@@ -544,8 +665,29 @@ int wg_batch_run(wg_batch* b, void* stream) {
   }
   hipEventRecord(t.ev[1], s);
   if (b->n_lossy > 0) {
-    hipError_t e = wg::launch_yuv_to_rgba(b->d_desc, nullptr, b->n, b->max_w, b->max_h,
-                                          (b->flags & WG_FLAG_NO_FANCY_UPSAMPLING) ? 0 : 1, s);
+    if (b->any_crop) {
+      // the crop windows of the reconstructed planes (even left/top, so chroma is aligned):
+      // upsampled as standalone images, as EmitFancyRGB / EmitSampledRGB see them
+      for (int i = 0; i < b->n; ++i) {
+        const FrameParse& f = b->fp[i];
+        if (f.status != WG_STATUS_OK || f.lossless || !f.cropped) continue;
+        const FrameDesc& d = b->desc[i];
+        const FrameDesc& d2 = b->desc2[i];
+        const int x = b->opt.crop_left & ~1, y = b->opt.crop_top & ~1;
+        const int uw = (f.out_w + 1) >> 1, uh = (f.out_h + 1) >> 1;
+        hipError_t e = hipMemcpy2DAsync(d2.y, d2.y_stride, d.y + (size_t)y * d.y_stride + x, d.y_stride, f.out_w,
+                                        f.out_h, hipMemcpyDeviceToDevice, s);
+        if (e == hipSuccess)
+          e = hipMemcpy2DAsync(d2.u, d2.uv_stride, d.u + (size_t)(y >> 1) * d.uv_stride + (x >> 1), d.uv_stride, uw,
+                               uh, hipMemcpyDeviceToDevice, s);
+        if (e == hipSuccess)
+          e = hipMemcpy2DAsync(d2.v, d2.uv_stride, d.v + (size_t)(y >> 1) * d.uv_stride + (x >> 1), d.uv_stride, uw,
+                               uh, hipMemcpyDeviceToDevice, s);
+        if (e != hipSuccess) return WG_STATUS_USER_ABORT;
+      }
+    }
+    hipError_t e = wg::launch_yuv_to_rgba(b->any_crop ? b->d_desc2 : b->d_desc, nullptr, b->n, b->max_out_w,
+                                          b->max_out_h, (b->flags & WG_FLAG_NO_FANCY_UPSAMPLING) ? 0 : 1, s);
     if (e != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
   }
   hipEventRecord(t.ev[2], s);
@@ -598,24 +740,71 @@ int64_t wg_batch_pixels(const wg_batch* b) { return b ? b->pixels : 0; }
 int wg_batch_frame_dims(const wg_batch* b, int i, int32_t* width, int32_t* height) {
   if (!b || i < 0 || i >= b->n) return WG_STATUS_INVALID_PARAM;
   if (b->fp[i].status != WG_STATUS_OK) return b->fp[i].status;
-  if (width) *width = b->desc[i].width;
-  if (height) *height = b->desc[i].height;
+  if (width) *width = b->fp[i].out_w;
+  if (height) *height = b->fp[i].out_h;
   return WG_STATUS_OK;
 }
 
-int wg_batch_download_rgba(wg_batch* b, int i, uint8_t* rgba, int stride) {
-  if (!b || i < 0 || i >= b->n || !rgba) return WG_STATUS_INVALID_PARAM;
-  if (b->fp[i].status != WG_STATUS_OK) return b->fp[i].status;
-  const FrameDesc& d = b->desc[i];
-  if (stride < 4 * d.width) return WG_STATUS_INVALID_PARAM;
+int wg_batch_frame_status(const wg_batch* b, int i) {
+  if (!b || i < 0 || i >= b->n) return WG_STATUS_INVALID_PARAM;
+  return b->fp[i].status;
+}
+
+namespace {
+// Wait for the batch's work and check the kernels' error word.
+int batch_sync(wg_batch* b) {
   hipSetDevice(b->ctx->device);
   hipError_t e = hipStreamSynchronize(b->ctx->stream);
   if (e == hipSuccess) e = hipDeviceSynchronize();
   int err = 0;
   if (e == hipSuccess) e = hipMemcpy(&err, b->d_err, sizeof(int), hipMemcpyDeviceToHost);
-  if (e == hipSuccess && err) return WG_STATUS_USER_ABORT;
-  if (e == hipSuccess)
-    e = hipMemcpy2D(rgba, stride, d.rgba, d.rgba_stride, 4 * (size_t)d.width, d.height, hipMemcpyDeviceToHost);
+  return (e != hipSuccess || err) ? WG_STATUS_USER_ABORT : WG_STATUS_OK;
+}
+const uint8_t* window_ptr(const wg_batch* b, int i) {
+  const FrameParse& f = b->fp[i];
+  const FrameDesc& d = b->desc[i];
+  return d.rgba + (size_t)f.win_y * d.rgba_stride + 4 * (size_t)f.win_x;
+}
+}  // namespace
+
+int wg_batch_download_rgba(wg_batch* b, int i, uint8_t* rgba, int stride) {
+  if (!b || i < 0 || i >= b->n || !rgba) return WG_STATUS_INVALID_PARAM;
+  if (b->fp[i].status != WG_STATUS_OK) return b->fp[i].status;
+  const FrameParse& f = b->fp[i];
+  if (stride < 4 * f.out_w) return WG_STATUS_INVALID_PARAM;
+  int st = batch_sync(b);
+  if (st != WG_STATUS_OK) return st;
+  const hipError_t e = hipMemcpy2D(rgba, stride, window_ptr(b, i), b->desc[i].rgba_stride, 4 * (size_t)f.out_w,
+                                   f.out_h, hipMemcpyDeviceToHost);
+  return e == hipSuccess ? WG_STATUS_OK : WG_STATUS_USER_ABORT;
+}
+
+int wg_batch_download(wg_batch* b, int i, uint8_t* out, int stride) {
+  if (!b || i < 0 || i >= b->n || !out) return WG_STATUS_INVALID_PARAM;
+  if (b->fp[i].status != WG_STATUS_OK) return b->fp[i].status;
+  const FrameParse& f = b->fp[i];
+  const int bpp = wg::output_bpp(b->opt.colorspace);
+  if (stride < bpp * f.out_w) return WG_STATUS_INVALID_PARAM;
+  if (b->opt.colorspace == 1 && !b->opt.flip) return wg_batch_download_rgba(b, i, out, stride);
+  int st = batch_sync(b);
+  if (st != WG_STATUS_OK) return st;
+  // K6 into a device staging buffer, then one 2D copy
+  const size_t row = (size_t)bpp * f.out_w;
+  uint8_t* d_out = nullptr;
+  wg::EmitDesc* d_ed = nullptr;
+  wg::EmitDesc ed{window_ptr(b, i), nullptr, b->desc[i].rgba_stride, (int32_t)row, f.out_w, f.out_h,
+                  b->opt.colorspace, b->opt.flip ? 1 : 0, 1, 0};
+  hipError_t e = hipMalloc(&d_out, row * f.out_h);
+  if (e == hipSuccess) e = hipMalloc(&d_ed, sizeof(ed));
+  if (e == hipSuccess) {
+    ed.dst = d_out;
+    e = hipMemcpyAsync(d_ed, &ed, sizeof(ed), hipMemcpyHostToDevice, b->ctx->stream);
+  }
+  if (e == hipSuccess) e = wg::launch_emit(d_ed, 1, f.out_w * f.out_h, b->ctx->stream);
+  if (e == hipSuccess) e = hipMemcpy2DAsync(out, stride, d_out, row, row, f.out_h, hipMemcpyDeviceToHost, b->ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(b->ctx->stream);
+  if (d_out) hipFree(d_out);
+  if (d_ed) hipFree(d_ed);
   return e == hipSuccess ? WG_STATUS_OK : WG_STATUS_USER_ABORT;
 }
 
@@ -654,19 +843,103 @@ int wg_decode_rgba_batch(wg_ctx* ctx, const uint8_t* const* data, const size_t* 
   return st;
 }
 
+int wg_decode_batch(wg_ctx* ctx, const uint8_t* const* data, const size_t* sizes, int n, const wg_decoder_options* opt,
+                    uint8_t* const* out, const int32_t* strides, int32_t* status) {
+  if (!ctx || !data || !sizes || !out || !strides || !status || !opt || n <= 0) return WG_STATUS_INVALID_PARAM;
+  wg_batch* b = wg_batch_create_ex(ctx, data, sizes, n, opt, status);
+  if (!b) return WG_STATUS_OUT_OF_MEMORY;
+  int st = wg_batch_run(b, nullptr);
+  const int bpp = wg::output_bpp(opt->colorspace);
+  if (st == WG_STATUS_OK && !(opt->colorspace == 1 && !opt->flip)) {
+    // K6 over every frame in one launch into one staging buffer
+    std::vector<wg::EmitDesc> ed((size_t)n, wg::EmitDesc{});
+    std::vector<size_t> offs((size_t)n, 0);
+    size_t total = 0;
+    int maxpx = 1;
+    for (int i = 0; i < n; ++i) {
+      const FrameParse& f = b->fp[i];
+      if (f.status != WG_STATUS_OK) continue;
+      offs[(size_t)i] = total;
+      total = align_up(total + (size_t)bpp * f.out_w * f.out_h);
+      maxpx = std::max(maxpx, f.out_w * f.out_h);
+    }
+    uint8_t* d_out = nullptr;
+    wg::EmitDesc* d_ed = nullptr;
+    hipError_t e = hipMalloc(&d_out, std::max<size_t>(total, kAlign));
+    if (e == hipSuccess) e = hipMalloc(&d_ed, sizeof(wg::EmitDesc) * (size_t)n);
+    for (int i = 0; e == hipSuccess && i < n; ++i) {
+      const FrameParse& f = b->fp[i];
+      if (f.status != WG_STATUS_OK) continue;
+      ed[(size_t)i] = wg::EmitDesc{window_ptr(b, i), d_out + offs[(size_t)i], b->desc[i].rgba_stride,
+                                   bpp * f.out_w, f.out_w, f.out_h, opt->colorspace, opt->flip ? 1 : 0, 1, 0};
+    }
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(d_ed, ed.data(), sizeof(wg::EmitDesc) * (size_t)n, hipMemcpyHostToDevice, ctx->stream);
+    if (e == hipSuccess) e = wg::launch_emit(d_ed, n, maxpx, ctx->stream);
+    if (e == hipSuccess) st = batch_sync(b);
+    else st = WG_STATUS_USER_ABORT;
+    for (int i = 0; st == WG_STATUS_OK && i < n; ++i) {
+      const FrameParse& f = b->fp[i];
+      if (status[i] != WG_STATUS_OK) continue;
+      if (out[i] == nullptr || strides[i] < bpp * f.out_w) {
+        status[i] = WG_STATUS_INVALID_PARAM;
+        continue;
+      }
+      const size_t row = (size_t)bpp * f.out_w;
+      if (hipMemcpy2D(out[i], strides[i], d_out + offs[(size_t)i], row, row, f.out_h, hipMemcpyDeviceToHost) !=
+          hipSuccess)
+        status[i] = WG_STATUS_USER_ABORT;
+    }
+    if (d_out) hipFree(d_out);
+    if (d_ed) hipFree(d_ed);
+  } else if (st == WG_STATUS_OK) {
+    if (hipStreamSynchronize(ctx->stream) != hipSuccess) st = WG_STATUS_USER_ABORT;
+    for (int i = 0; st == WG_STATUS_OK && i < n; ++i) {
+      if (status[i] != WG_STATUS_OK) continue;
+      if (out[i] == nullptr || strides[i] < 4 * b->fp[i].out_w) {
+        status[i] = WG_STATUS_INVALID_PARAM;
+        continue;
+      }
+      status[i] = wg_batch_download_rgba(b, i, out[i], strides[i]);
+    }
+  }
+  wg_batch_destroy(b);
+  return st;
+}
+
+int wg_decode_into(const uint8_t* data, size_t size, const wg_decoder_options* opt, uint8_t* out, size_t cap,
+                   int stride) {
+  if (!data || !out || !opt) return WG_STATUS_INVALID_PARAM;
+  wg_features f{};
+  int st = wg_get_features(data, size, &f);
+  if (st != WG_STATUS_OK) return st;
+  const int bpp = wg::output_bpp(opt->colorspace);
+  int w = f.width, h = f.height;
+  if (opt->use_cropping) {
+    w = opt->crop_width;
+    h = opt->crop_height;
+  }
+  if (bpp && w > 0 && h > 0 && (stride < bpp * w || (size_t)stride * (h - 1) + (size_t)bpp * w > cap))
+    return WG_STATUS_INVALID_PARAM;
+  wg_ctx* ctx = default_ctx();
+  if (!ctx) return WG_STATUS_UNSUPPORTED_FEATURE;  // no GPU: no CPU fallback by design
+  const uint8_t* d[1] = {data};
+  const size_t s[1] = {size};
+  uint8_t* o[1] = {out};
+  const int32_t str[1] = {stride};
+  int32_t fs[1] = {0};
+  st = wg_decode_batch(ctx, d, s, 1, opt, o, str, fs);
+  return st != WG_STATUS_OK ? st : fs[0];
+}
+
 int wg_decode_rgba_into(const uint8_t* data, size_t size, uint8_t* rgba, size_t cap, int stride, int flags) {
-  static std::mutex mu;
-  static wg_ctx* ctx = nullptr;
   if (!data || !rgba) return WG_STATUS_INVALID_PARAM;
   wg_features f{};
   int st = wg_get_features(data, size, &f);
   if (st != WG_STATUS_OK) return st;
   if (stride < 4 * f.width || (size_t)stride * (f.height - 1) + 4 * (size_t)f.width > cap)
     return WG_STATUS_INVALID_PARAM;
-  {
-    std::lock_guard<std::mutex> lock(mu);
-    if (!ctx) ctx = wg_ctx_create(0, 1);
-  }
+  wg_ctx* ctx = default_ctx();
   if (!ctx) return WG_STATUS_UNSUPPORTED_FEATURE;  // no GPU: no CPU fallback by design
   const uint8_t* d[1] = {data};
   const size_t s[1] = {size};

@@ -21,7 +21,8 @@
 //        gradient    row 0 as horizontal, then out = in + clip(L + T - TL): a wavefront
 //                    over 1024-row bands (thread = row, one column per step, T from the
 //                    thread above via DPP / LDS, the band's top row from LDS);
-//   3. write the plane into the A bytes (dword read-modify-write, coalesced).
+//   3. write the plane (its output window when cropping) into the A bytes (dword
+//      read-modify-write, coalesced).
 // The plane traffic is small next to K1/K2 (1 B/px vs 5.5 B/px); the gradient wavefront is
 // latency-bound (one barrier per column step) and is the slow case.
 #include <hip/hip_runtime.h>
@@ -200,11 +201,11 @@ __global__ void __launch_bounds__(kThreads) alpha_kernel(const AlphaDesc* __rest
   }
   __syncthreads();
 
-  // ---- 3. plane -> A bytes
-  for (int y = wave; y < H; y += kWaves) {
+  // ---- 3. plane window -> A bytes (the RGBA holds the window: the whole plane unless cropping)
+  for (int y = wave; y < F.win_h; y += kWaves) {
     uint32_t* dst = reinterpret_cast<uint32_t*>(F.rgba + (size_t)y * F.rgba_stride);
-    const uint8_t* src = plane + (size_t)y * W;
-    for (int x = lane; x < W; x += 64) dst[x] = (dst[x] & 0x00ffffffu) | ((uint32_t)src[x] << 24);
+    const uint8_t* src = plane + (size_t)(y + F.win_y) * W + F.win_x;
+    for (int x = lane; x < F.win_w; x += 64) dst[x] = (dst[x] & 0x00ffffffu) | ((uint32_t)src[x] << 24);
   }
 }
 

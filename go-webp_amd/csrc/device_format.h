@@ -87,10 +87,20 @@ struct AlphaDesc {
   const uint8_t* raw;    // method 0: the filtered bytes, width*height
   uint8_t* plane;        // width*height scratch: filtered -> unfiltered alpha
   uint8_t* rgba;         // the frame's RGBA output; K4 writes its A bytes
-  int32_t width, height, rgba_stride, filter;  // filter: 0 none, 1 horizontal, 2 vertical, 3 gradient
-  int32_t valid, pad0, pad1, pad2;
+  int32_t width, height, rgba_stride, filter;  // plane size; filter: 0 none, 1 horizontal, 2 vertical, 3 gradient
+  int32_t valid, win_x, win_y, win_w;           // the output window of the plane (cropping)
+  int32_t win_h, pad0, pad1, pad2;
 };
-static_assert(sizeof(AlphaDesc) == 64, "AlphaDesc must be 64 bytes");
+static_assert(sizeof(AlphaDesc) == 80, "AlphaDesc must be 80 bytes");
+
+// One frame's output conversion for K6 (emit.hip): RGBA window -> WEBP_CSP_MODE bytes.
+struct EmitDesc {
+  const uint8_t* src;  // RGBA, first pixel of the window
+  uint8_t* dst;        // output rows (stride dst_stride), row 0 at the top
+  int32_t src_stride, dst_stride, width, height;
+  int32_t mode, flip, valid, pad0;
+};
+static_assert(sizeof(EmitDesc) == 48, "EmitDesc must be 48 bytes");
 
 // One frame of an animation for K5 (anim.hip), in display order.
 struct AnimFrameDesc {

@@ -63,6 +63,28 @@ class VP8Info(C.Structure):
                 ("frame_offset", C.c_int32)]
 
 
+class DecoderOptions(C.Structure):
+    """wg_decoder_options (WebPDecoderConfig output colorspace + options subset)."""
+    _fields_ = [("colorspace", C.c_int32), ("bypass_filtering", C.c_int32), ("no_fancy_upsampling", C.c_int32),
+                ("use_cropping", C.c_int32), ("crop_left", C.c_int32), ("crop_top", C.c_int32),
+                ("crop_width", C.c_int32), ("crop_height", C.c_int32), ("use_scaling", C.c_int32),
+                ("scaled_width", C.c_int32), ("scaled_height", C.c_int32), ("flip", C.c_int32),
+                ("reserved", C.c_int32 * 4)]
+
+
+def options(colorspace=1, crop=None, flip=0, no_fancy=0, bypass=0, scale=None):
+    """DecoderOptions from keywords; crop = (left, top, width, height), scale = (w, h)."""
+    o = DecoderOptions()
+    o.colorspace, o.flip, o.no_fancy_upsampling, o.bypass_filtering = colorspace, flip, no_fancy, bypass
+    if crop is not None:
+        o.use_cropping = 1
+        o.crop_left, o.crop_top, o.crop_width, o.crop_height = crop
+    if scale is not None:
+        o.use_scaling = 1
+        o.scaled_width, o.scaled_height = scale
+    return o
+
+
 class AnimInfo(C.Structure):
     """wg_anim_info = WebPAnimInfo."""
     _fields_ = [("canvas_width", C.c_uint32), ("canvas_height", C.c_uint32), ("loop_count", C.c_uint32),
@@ -124,6 +146,12 @@ _SIGS = {
     "wg_vp8l_parse": (C.c_int, [_P, C.c_size_t, C.POINTER(VP8LInfo), _P, _P]),
     "wg_alpha_parse": (C.c_int, [_P, C.c_size_t, _P, _P, _P, _P, _P]),
     "wg_anim_demux": (C.c_int, [_P, C.c_size_t, _P, _P, C.c_int]),
+    "wg_output_bpp": (C.c_int, [C.c_int]),
+    "wg_decode_into": (C.c_int, [_P, C.c_size_t, _P, _P, C.c_size_t, C.c_int]),
+    "wg_decode_batch": (C.c_int, [_P, _P, _P, C.c_int, _P, _P, _P, _P]),
+    "wg_batch_create_ex": (_P, [_P, _P, _P, C.c_int, _P, _P]),
+    "wg_batch_download": (C.c_int, [_P, C.c_int, _P, C.c_int]),
+    "wg_batch_frame_status": (C.c_int, [_P, C.c_int]),
     "wg_anim_decode": (C.c_int, [_P, _P, C.c_size_t, _P, _P, C.c_int32]),
 }
 EXPORTED = tuple(_SIGS)
@@ -177,6 +205,24 @@ def features(data):
     if st != Status.OK:
         raise WebPError(st, "wg_get_features")
     return f
+
+
+def output_bpp(colorspace):
+    return lib().wg_output_bpp(colorspace)
+
+
+def decode_into(data, opts):
+    """Mirror of WebPDecode with output options: one frame -> (h, w * bpp) uint8 rows in the
+    options' colorspace / crop window / orientation."""
+    b = _buf(data)
+    f = features(b)
+    bpp = output_bpp(opts.colorspace) or 4
+    w, h = (opts.crop_width, opts.crop_height) if opts.use_cropping else (f.width, f.height)
+    out = np.empty((max(h, 1), max(w, 1) * bpp), np.uint8)
+    st = lib().wg_decode_into(b, len(b), C.byref(opts), out.ctypes.data, out.nbytes, out.shape[1])
+    if st != Status.OK:
+        raise WebPError(st, "wg_decode_into")
+    return out
 
 
 def decode_config(data):
@@ -370,6 +416,27 @@ class Context:
 
     def batch(self, datas, flags=0):
         return Batch(self, datas, flags)
+
+    def decode_batch_opts(self, datas, opts):
+        """wg_decode_batch: frames -> ([(h, w * bpp) uint8 rows or None], status)."""
+        bufs, ptrs, sizes = _ptr_arrays(datas)
+        n = len(bufs)
+        bpp = output_bpp(opts.colorspace) or 4
+        outs = []
+        for b in bufs:
+            try:
+                f = features(b)
+                w, h = (opts.crop_width, opts.crop_height) if opts.use_cropping else (f.width, f.height)
+            except WebPError:
+                w = h = 1
+            outs.append(np.zeros((max(h, 1), max(w, 1) * bpp), np.uint8))
+        optr = (C.c_void_p * n)(*[o.ctypes.data for o in outs])
+        strides = (C.c_int32 * n)(*[o.shape[1] for o in outs])
+        status = np.zeros(n, np.int32)
+        st = lib().wg_decode_batch(self._h, ptrs, sizes, n, C.byref(opts), optr, strides, status.ctypes.data)
+        if st != Status.OK:
+            raise WebPError(st, "wg_decode_batch")
+        return [o if s == 0 else None for o, s in zip(outs, status)], status
 
     def decode_anim(self, data, flags=0):
         """Whole animation -> (canvases (frames, H, W, 4) uint8 RGBA, timestamps int32 ms), as

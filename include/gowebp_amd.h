@@ -72,6 +72,31 @@ int wg_get_features(const uint8_t* data, size_t size, wg_features* out);
 int wg_decode_rgba_into(const uint8_t* data, size_t size, uint8_t* rgba, size_t cap,
                         int stride, int flags);
 
+/* ---- output options (WebPDecoderConfig subset, pkg/libwebp/webp/decode.go:59-83) --------- */
+/* colorspace = WEBP_CSP_MODE of the RGB family: 0 RGB, 1 RGBA, 2 BGR, 3 BGRA, 4 ARGB,
+ * 5 RGBA_4444, 6 RGB_565, 7 rgbA, 8 bgrA, 9 Argb, 10 rgbA_4444 (lower case = premultiplied);
+ * the YUV modes 11/12 are UNSUPPORTED_FEATURE here (wg_batch_download_yuv gives the planes).
+ * Cropping as WebPIoInitFromOptions: left/top snapped to even, the window must lie inside the
+ * frame (else INVALID_PARAM).  Scaling is disabled in the reference (io_dec.c.go:540-541):
+ * use_scaling -> UNSUPPORTED_FEATURE.  flip emits rows bottom-up. */
+typedef struct {
+  int32_t colorspace;
+  int32_t bypass_filtering, no_fancy_upsampling;
+  int32_t use_cropping, crop_left, crop_top, crop_width, crop_height;
+  int32_t use_scaling, scaled_width, scaled_height;
+  int32_t flip;
+  int32_t reserved[4];
+} wg_decoder_options;
+
+/* Bytes per pixel of a colorspace (3, 4 or 2); 0 if not an RGB-family mode. */
+int wg_output_bpp(int colorspace);
+
+/* Replaces WebPDecode with config.output in external memory (webp.go:870-909): one frame on
+ * the GPU (device 0 context) in the options' colorspace / crop window / orientation, rows of
+ * `stride` bytes. */
+int wg_decode_into(const uint8_t* data, size_t size, const wg_decoder_options* opt, uint8_t* out,
+                   size_t cap, int stride);
+
 /* ---- batched decode: one context per device ------------------------------------------ */
 typedef struct wg_ctx wg_ctx;
 
@@ -87,6 +112,11 @@ int wg_decode_rgba_batch(wg_ctx* ctx, const uint8_t* const* data, const size_t* 
                          uint8_t* const* rgba, const int32_t* strides, int32_t* status,
                          int32_t flags);
 
+/* As wg_decode_rgba_batch with full output options (colorspace, cropping, flip). */
+int wg_decode_batch(wg_ctx* ctx, const uint8_t* const* data, const size_t* sizes, int n,
+                    const wg_decoder_options* opt, uint8_t* const* out, const int32_t* strides,
+                    int32_t* status);
+
 /* ---- device-resident batch (benchmarks, tests) -------------------------------------- */
 typedef struct wg_batch wg_batch;
 
@@ -95,6 +125,9 @@ typedef struct wg_batch wg_batch;
  * device path (inputs resident in HBM).  NULL on failure (status[] says why per frame). */
 wg_batch* wg_batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t* sizes, int n,
                           int32_t flags, int32_t* status);
+/* As wg_batch_create with output options; flags-only creation = colorspace RGBA, no crop. */
+wg_batch* wg_batch_create_ex(wg_ctx* ctx, const uint8_t* const* data, const size_t* sizes, int n,
+                             const wg_decoder_options* opt, int32_t* status);
 void wg_batch_destroy(wg_batch* b);
 
 /* Run the device DSP path for the whole batch on `stream` (NULL = ctx stream):
@@ -113,12 +146,15 @@ int wg_batch_kernel_ms(const wg_batch* b, float* ms, int n_ms);
 int wg_batch_kernel_bytes(const wg_batch* b, double* bytes, int n_bytes);
 
 int wg_batch_size(const wg_batch* b);
-int wg_batch_frame_dims(const wg_batch* b, int i, int32_t* width, int32_t* height);
+int wg_batch_frame_dims(const wg_batch* b, int i, int32_t* width, int32_t* height); /* output size */
+int wg_batch_frame_status(const wg_batch* b, int i);
 int64_t wg_batch_pixels(const wg_batch* b);
 
-/* Copy results of frame i back to host: RGBA (stride >= 4*width) and/or the cropped
- * Y/U/V planes (strides width, (width+1)/2). */
+/* Copy results of frame i back to host: RGBA of the output window (stride >= 4*width; no flip,
+ * whatever the batch's colorspace), the batch's colorspace / flip via K6 (wg_batch_download,
+ * stride >= bpp*width), and/or the full frame's Y/U/V planes (strides width, (width+1)/2). */
 int wg_batch_download_rgba(wg_batch* b, int i, uint8_t* rgba, int stride);
+int wg_batch_download(wg_batch* b, int i, uint8_t* out, int stride);
 int wg_batch_download_yuv(wg_batch* b, int i, uint8_t* y, uint8_t* u, uint8_t* v); /* lossy only */
 
 /* ---- stage entry point: YUV420 -> RGBA on device pointers ---------------------------- */

@@ -22,7 +22,7 @@ frames (SURVEY.md §8(d), Appendix B generators) are stored as ``.webp`` plus
 SHA-256 of their decodes in ``manifest.json``.  Every decode is also checked
 against libwebp's SIMD path (must be byte-identical) before it is written.
 
-Usage:  python tests/golden/make_golden.py [lossy|lossless|alpha|anim|bench ...]
+Usage:  python tests/golden/make_golden.py [lossy|lossless|alpha|modes|anim|bench ...]
         (rewrites tests/golden/<section>/; default all sections)
 """
 import ctypes as C
@@ -358,6 +358,68 @@ ALPHA_ERROR_CASES = [
 ]
 
 
+# ----------------------------------------------------------------------------- output modes
+# WEBP_CSP_MODE (pkg/libwebp/webp/decode.go enums): bytes per pixel of each RGB-family mode
+MODE_BPP = {0: 3, 1: 4, 2: 3, 3: 4, 4: 4, 5: 2, 6: 2, 7: 4, 8: 4, 9: 4, 10: 2}
+
+
+def decode_mode(data, mode, crop=None, flip=0, no_fancy=0, bypass=0):
+    """WebPDecode with config.output.colorspace = mode (+ cropping / flip options) -> (status,
+    (h, w * bpp) uint8 rows)."""
+    cfg = (C.c_uint8 * 512)()
+    assert LIB.WebPInitDecoderConfigInternal(cfg, ABI)
+    ci = C.cast(cfg, C.POINTER(C.c_int32))
+    ci[40 // 4] = mode
+    ci[160 // 4] = bypass
+    ci[164 // 4] = no_fancy
+    if crop is not None:
+        ci[168 // 4] = 1
+        ci[172 // 4], ci[176 // 4], ci[180 // 4], ci[184 // 4] = crop
+    ci[208 // 4] = flip
+    st = LIB.WebPDecode(data, C.c_size_t(len(data)), cfg)
+    if st != 0:
+        return st, None
+    w, h = ci[44 // 4], ci[48 // 4]
+    cp = C.cast(cfg, C.POINTER(C.c_void_p))
+    stride = ci[64 // 4]
+    bpp = MODE_BPP[mode]
+    base = cp[56 // 8]  # with flip, DecodeInto restores pointer and stride: rows are stored flipped
+    rows = [np.frombuffer(C.string_at(base + r * stride, w * bpp), np.uint8) for r in range(h)]
+    LIB.WebPFreeDecBuffer(C.byref(cfg, 40))
+    return 0, np.stack(rows)
+
+
+MODE_SOURCES = [("lossy", "synth_17x9"), ("lossy", "synth_80x96"), ("alpha", "a_raw_g_64x64"),
+                ("lossy", "alpha_64x48"), ("lossless", "ll_alpha_48x48"), ("lossless", "ll_pal4_63x41")]
+# (crop_left, crop_top, crop_width, crop_height); odd left/top are snapped to even by libwebp
+MODE_CROPS = {"none": None, "c1": (3, 5, 20, 11), "c2": (0, 0, 9, 1), "c3": (6, 2, 1, 7), "c4": (5, 3, 12, 6)}
+
+
+def mode_cases(data, w, h, lossy):
+    """Outputs of every mode x crop (+ flip / no-fancy on two crops, no-fancy for lossy only);
+    the 'full' crop (= no crop) and the out-of-bounds one only record a status."""
+    out, statuses = {}, {}
+    crops = dict(MODE_CROPS)
+    crops["full"] = (0, 0, w, h)
+    crops["oob"] = (w - 4, 0, 8, 2)  # past the right edge: INVALID_PARAM
+    for cname, crop in crops.items():
+        for mode in MODE_BPP:
+            for flip in (0, 1):
+                for nf in (0, 1):
+                    if (flip or nf) and cname not in ("none", "c1") or (nf and not lossy):
+                        continue
+                    key = f"m{mode}_{cname}_f{flip}_nf{nf}"
+                    st, arr = decode_mode(data, mode, crop, flip, nf)
+                    _plain_c(False)
+                    st2, arr2 = decode_mode(data, mode, crop, flip, nf)
+                    _plain_c(True)
+                    assert st == st2 and (arr is None or np.array_equal(arr, arr2)), key
+                    statuses[key] = st
+                    if arr is not None and cname != "full":
+                        out[key] = arr
+    return out, statuses
+
+
 # ----------------------------------------------------------------------------- animation
 DEMUX_ABI = 0x0107  # WEBP_DEMUX_ABI_VERSION of 1.6.0
 MUX_ABI = 0x0109    # WEBP_MUX_ABI_VERSION of 1.6.0
@@ -640,7 +702,7 @@ def sha(a):
 def main(argv):
     """argv: sections to (re)generate among lossy, lossless, alpha, bench (default: all);
     the manifest entries of the other sections are kept."""
-    sections = set(argv) or {"lossy", "lossless", "alpha", "anim", "bench"}
+    sections = set(argv) or {"lossy", "lossless", "alpha", "modes", "anim", "bench"}
     os.makedirs(os.path.join(HERE, "lossy"), exist_ok=True)
     os.makedirs(os.path.join(HERE, "lossless"), exist_ok=True)
     os.makedirs(os.path.join(HERE, "bench"), exist_ok=True)
@@ -702,6 +764,18 @@ def main(argv):
         manifest["alpha_errors"] = manifest.get("alpha_errors", {})
         manifest["alpha_errors"][name] = dict(source=src, status=st, bytes=len(data))
         print(name, "status", st, flush=True)
+    if "modes" in sections:
+        os.makedirs(os.path.join(HERE, "modes"), exist_ok=True)
+        for kind, src in MODE_SOURCES:
+            data = open(os.path.join(HERE, kind, src + ".webp"), "rb").read()
+            w, h = _decode_cfg(data, MODE_RGBA).shape[1::-1]
+            arrs, statuses = mode_cases(data, w, h, kind != "lossless")
+            np.savez_compressed(os.path.join(HERE, "modes", src + ".npz"), **arrs)
+            manifest["modes"][src] = dict(source=f"{kind}/{src}.webp", width=w, height=h,
+                                          crops={k: v for k, v in MODE_CROPS.items()} | {"full": [0, 0, w, h],
+                                                                                       "oob": [w - 4, 0, 8, 2]},
+                                          status=statuses)
+            print(src, len(arrs), "outputs", sum(1 for v in statuses.values() if v), "errors", flush=True)
     if "anim" in sections:
         os.makedirs(os.path.join(HERE, "anim"), exist_ok=True)
         builders = list(ANIM_CASES) + [(k, (lambda v=v: v)) for k, v in _manual_anims().items()]

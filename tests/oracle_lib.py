@@ -34,6 +34,7 @@ def oracle():
         L.oracle_vp8l_decode.argtypes = [P, P, P, P]
         L.oracle_alpha_unfilter.argtypes = [C.c_int, C.c_int, C.c_int, P, P]
         L.oracle_anim_compose.argtypes = [P, C.c_int, C.c_int, C.c_int, P, P]
+        L.oracle_emit.argtypes = [P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, C.c_int]
         _lib = L
     return _lib
 
@@ -178,3 +179,63 @@ def load_anim(name):
     d = os.path.join(GOLDEN, "anim")
     data = open(os.path.join(d, name + ".webp"), "rb").read()
     return data, dict(np.load(os.path.join(d, name + ".npz")))
+
+
+MODE_BPP = {0: 3, 1: 4, 2: 3, 3: 4, 4: 4, 5: 2, 6: 2, 7: 4, 8: 4, 9: 4, 10: 2}
+
+
+def oracle_output(data, mode=1, crop=None, flip=0, no_fancy=0, bypass=0):
+    """CPU WebPDecode with output options, from the oracles: the RGBA of the output window
+    (lossless: a window of the full decode; lossy: the cropped planes upsampled as a standalone
+    image, A from the ALPH oracle's window), then the oracle's mode packing / premultiply / flip.
+    -> (h, w * bpp) uint8, or None when libwebp reports INVALID_PARAM for the crop."""
+    import webp_amd
+
+    f = webp_amd.features(data)
+    W, H = f.width, f.height
+    x, y, cw, ch = 0, 0, W, H
+    if crop is not None:
+        # WebPAllocateDecBuffer checks the window with the origin snapped to even; the io window
+        # (WebPIoInitFromOptions) snaps only for YUV sources (lossy), lossless keeps odd origins
+        ok = lambda a, b: a >= 0 and b >= 0 and cw > 0 and ch > 0 and a + cw <= W and b + ch <= H  # noqa: E731
+        cw, ch = crop[2], crop[3]
+        x, y = (crop[0], crop[1]) if f.format == 2 else (crop[0] & ~1, crop[1] & ~1)
+        if not (ok(crop[0] & ~1, crop[1] & ~1) and ok(x, y)):
+            return None
+    if f.format == 2:
+        info, argb, tdata = webp_amd.vp8l_parse(data)
+        rgba = oracle_vp8l_decode(info, argb, tdata)[y:y + ch, x:x + cw]
+    else:
+        info, mbs = webp_amd.vp8_parse(data, flags=1 if bypass else 0)
+        planes = oracle_decode(info, mbs)
+        uh, uw = (ch + 1) // 2, (cw + 1) // 2
+        rgba = oracle_yuv_to_rgba(np.ascontiguousarray(planes["y"][y:y + ch, x:x + cw]),
+                                  np.ascontiguousarray(planes["u"][y // 2:y // 2 + uh, x // 2:x // 2 + uw]),
+                                  np.ascontiguousarray(planes["v"][y // 2:y // 2 + uh, x // 2:x // 2 + uw]),
+                                  fancy=not no_fancy)
+        try:
+            rgba[..., 3] = oracle_alpha_plane(data)[1][y:y + ch, x:x + cw]
+        except webp_amd.WebPError as e:
+            if e.status != webp_amd.Status.UNSUPPORTED_FEATURE:
+                raise
+    rgba = np.ascontiguousarray(rgba)
+    out = np.empty((ch, cw * MODE_BPP[mode]), np.uint8)
+    assert oracle().oracle_emit(rgba.ctypes.data, cw, ch, cw * 4, mode, flip, out.ctypes.data, out.shape[1]) == 0
+    return out
+
+
+def mode_sources():
+    return sorted(manifest().get("modes", {}))
+
+
+def load_modes(src):
+    ent = manifest()["modes"][src]
+    data = open(os.path.join(GOLDEN, ent["source"]), "rb").read()
+    return data, dict(np.load(os.path.join(GOLDEN, "modes", src + ".npz"))), ent
+
+
+def parse_mode_key(key):
+    """'m{mode}_{crop}_f{flip}_nf{nf}' -> (mode, crop name, flip, nf)."""
+    m, rest = key.split("_", 1)
+    crop, fl, nf = rest.rsplit("_", 2)
+    return int(m[1:]), crop, int(fl[1:]), int(nf[2:])
