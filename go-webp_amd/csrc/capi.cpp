@@ -46,6 +46,8 @@ struct FrameParse {
   size_t off_recs = 0, off_rows = 0, off_blocks = 0;  // within the input buffer (lossy)
   size_t off_coded = 0, off_tdata[4] = {0, 0, 0, 0};  // within the input buffer (lossless)
   size_t off_y = 0, off_u = 0, off_v = 0;            // within the plane buffer
+  size_t off_cols = 0;                                // K1 global column store (wide frames)
+  bool wide = false;                                  // mb_w > vp8_recon_max_mb_w()
   size_t off_scratch = 0;                             // lossless two-pass scratch (plane buffer)
   size_t off_rgba = 0;                                // within the RGBA buffer
   int width = 0, height = 0;
@@ -90,7 +92,6 @@ int parse_one(const uint8_t* data, size_t size, int flags, FrameParse* fp) {
   }
   st = wg::vp8_parse(data, size, flags, nullptr, nullptr, &fp->sf);
   if (st != WG_STATUS_OK) return st;
-  if (fp->sf.info.mb_w > wg::vp8_recon_max_mb_w()) return WG_STATUS_UNSUPPORTED_FEATURE;
   fp->width = fp->sf.info.width;
   fp->height = fp->sf.info.height;
   if (c.alpha_size > 0) {  // ALPH (VP8DecompressAlphaRows, alpha_dec.go:164-213)
@@ -158,7 +159,8 @@ struct wg_batch {
   uint8_t* d_planes = nullptr;
   uint8_t* d_rgba = nullptr;
   size_t in_bytes = 0, plane_bytes = 0, rgba_bytes = 0;
-  int max_mb_w = 1, max_w = 1, max_h = 1;
+  int max_mb_w = 1, max_w = 1, max_h = 1;  // max_mb_w over the frames whose K1 column store is in LDS
+  int n_wide = 0;                          // lossy frames wider than that (global column store)
   int n_valid = 0;
   int64_t pixels = 0;
   double kbytes[4] = {0, 0, 0, 0};
@@ -441,7 +443,14 @@ wg_batch* wg_batch_create_ex(wg_ctx* ctx, const uint8_t* const* data, const size
     pl_b = align_up(pl_b + nmb * 64);
     f.off_v = pl_b;
     pl_b = align_up(pl_b + nmb * 64);
-    b->max_mb_w = std::max(b->max_mb_w, inf.mb_w);
+    f.wide = inf.mb_w > wg::vp8_recon_max_mb_w();
+    if (f.wide) {
+      b->n_wide++;
+      f.off_cols = pl_b;
+      pl_b = align_up(pl_b + (size_t)inf.mb_w * 160);
+    } else {
+      b->max_mb_w = std::max(b->max_mb_w, inf.mb_w);
+    }
     if (f.cropped) {  // K2 reads the crop window from compact planes (copied after K1)
       b->any_crop = true;
       f.yc_stride = (f.out_w + 15) & ~15;
@@ -567,6 +576,7 @@ wg_batch* wg_batch_create_ex(wg_ctx* ctx, const uint8_t* const* data, const size
     d.blocks = reinterpret_cast<const int16_t*>(b->d_in + f.off_blocks);
     d.blocks_bytes = (int32_t)(f.sf.blocks.size() * 2);
     d.y = b->d_planes + f.off_y;
+    d.cols = f.wide ? b->d_planes + f.off_cols : nullptr;
     d.u = b->d_planes + f.off_u;
     d.v = b->d_planes + f.off_v;
     d.mb_w = inf.mb_w;
@@ -660,7 +670,8 @@ int wg_batch_run(wg_batch* b, void* stream) {
   Timing& t = b->timings[b->n_runs_pending++];
   hipEventRecord(t.ev[0], s);
   if (b->n_lossy > 0) {
-    hipError_t e = wg::launch_vp8_recon_filter(b->d_desc, b->n, b->max_mb_w, b->d_err, s);
+    hipError_t e = wg::launch_vp8_recon_filter(b->d_desc, b->n, b->max_mb_w, b->n_lossy > b->n_wide,
+                                               b->n_wide > 0, b->d_err, s);
     if (e != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
   }
   hipEventRecord(t.ev[1], s);

@@ -36,6 +36,7 @@
 // exactly once, when final.  MB records and coefficients are software-pipelined:
 // record x+2 and coefficients x+1 are in flight while MB x is processed.
 #include <hip/hip_runtime.h>
+#include <type_traits>
 #include <stdint.h>
 #include <stdlib.h>
 
@@ -110,6 +111,9 @@ __device__ __forceinline__ uint32_t pack4(int a, int b, int c, int d) {
 __device__ __forceinline__ int byte_of(uint32_t w, int i) { return (w >> (8 * i)) & 0xff; }
 __device__ __forceinline__ uint32_t ld32(const uint8_t* p) { return *reinterpret_cast<const uint32_t*>(p); }
 __device__ __forceinline__ void st32(uint8_t* p, uint32_t v) { *reinterpret_cast<uint32_t*>(p) = v; }
+// the column store of wide frames (global memory, see vp8_recon_filter_kernel)
+__device__ __forceinline__ uint32_t ld32(gptr<const uint8_t> p) { return *(gptr<const uint32_t>)p; }
+__device__ __forceinline__ void st32(gptr<uint8_t> p, uint32_t v) { *(gptr<uint32_t>)p = v; }
 
 // 32-bit wrapping MUL1/MUL2 (dsp.h.go WEBP_TRANSFORM_AC3_MUL1/2).  |a| < 2^23 for any
 // int16 input, so the 24-bit multiplier gives the exact low 32 bits of a*c.
@@ -373,6 +377,14 @@ __device__ __forceinline__ Coefs load_coefs(__amdgpu_buffer_rsrc_t blks, uint32_
 
 }  // namespace
 
+// kGlobalCols: the per-MB-column store (kColBytes per column) lives in LDS when the frame's
+// columns fit next to the workspaces (mb_w <= vp8_recon_max_mb_w(), 9600 px), else in a
+// per-frame global buffer (FrameDesc::cols, wide frames up to VP8's 16383 px).  Each variant
+// skips the other's frames.  The hand-offs through the store keep their ordering: within a
+// wave (row 2k -> 2k+1) by the fences of lds_sync, across waves by the release/acquire
+// progress counters -- at workgroup scope the AMDGPU memory model orders global accesses
+// of one CU the same way (its L1 is shared by the workgroup), no extra s_waitcnt needed.
+template <bool kGlobalCols>
 __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc* __restrict__ frames, int* err,
                                                                 int lead_arg) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -381,7 +393,7 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
   // vmcnt(0) drained the record/coefficient prefetch every MB.
   __shared__ uint32_t progress[kWaves];
   const FrameDesc* F = frames + blockIdx.x;
-  if (!F->valid) return;
+  if (!F->valid || (F->cols != nullptr) != kGlobalCols) return;
   const int mb_w = F->mb_w, mb_h = F->mb_h;
   const int ftype = F->filter_type;
   const int ys = F->y_stride, uvs = F->uv_stride;
@@ -408,7 +420,10 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
   const int h = lane >> 5;  // half-wave: 0 = row 2k, 1 = row 2k+1
   const int l = lane & 31;
   uint32_t* tab = reinterpret_cast<uint32_t*>(lds + kProgBytes);
-  uint8_t* cols = lds + kHdrBytes + 2 * kWaves * kSlotBytes;
+  using ColPtr = std::conditional_t<kGlobalCols, gptr<uint8_t>, uint8_t*>;
+  ColPtr cols;
+  if constexpr (kGlobalCols) cols = as_global(F->cols);
+  else cols = lds + kHdrBytes + 2 * kWaves * kSlotBytes;
   // per MB column c: cols + c*kColBytes: [0..15] ytop Y, [16..23] U, [24..31] V, [32..159] fbot
   if (threadIdx.x < kWaves) progress[threadIdx.x] = 0;
   for (int t = threadIdx.x; t < 160; t += blockDim.x) tab[t] = kPred4Table[t];
@@ -478,7 +493,7 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
       }
       const uint32_t fl = rc.flags;
       const bool i4 = (fl >> kI4Shift) & 1;
-      uint8_t* col = cols + x * kColBytes;
+      const ColPtr col = cols + x * kColBytes;
 
       K1_SECT(1);
       // ---- ReconstructRow prologue at the row's first MB (frame_dec.c.go:79-98)
@@ -669,7 +684,7 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
           } else {
             const int kk = l - 16, p = kk >> 3, rr = (kk >> 1) & 3, d = kk & 1;
             const uint8_t* src = fw + (p ? kFwV : kFwU) + (rr + 8) * FWC;
-            uint8_t* cb0 = col + 96 + 32 * p + 8 * rr;
+            const ColPtr cb0 = col + 96 + 32 * p + 8 * rr;
             if (d == 0) {
               if (x > 0) st32(cb0 - kColBytes + 4, ld32(src));
               if (last_x) st32(cb0 + 4, ld32(src + 8));
@@ -776,23 +791,41 @@ size_t vp8_recon_lds_bytes(int mb_w) {
 
 int vp8_recon_max_mb_w() { return (int)((163840 - kHdrBytes - 2 * kWaves * kSlotBytes) / kColBytes); }
 
-hipError_t launch_vp8_recon_filter(const FrameDesc* d_frames, int n_frames, int max_mb_w, int* d_err,
-                                   hipStream_t stream) {
+hipError_t launch_vp8_recon_filter(const FrameDesc* d_frames, int n_frames, int max_mb_w, bool lds_frames,
+                                   bool wide_frames, int* d_err, hipStream_t stream) {
   // WG_K1_LEAD overrides the inter-pair lead (tuning experiments only).
   static const int lead = [] {
     const char* e = getenv("WG_K1_LEAD");
     return e ? atoi(e) : 0;
   }();
-  const size_t lds = vp8_recon_lds_bytes(max_mb_w);
-  static size_t configured = 0;
-  if (lds > 65536 && lds > configured) {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&vp8_recon_filter_kernel),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (lds_frames) {
+    const size_t lds = vp8_recon_lds_bytes(max_mb_w);
+    static size_t configured = 0;
+    if (lds > 65536 && lds > configured) {
+      const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&vp8_recon_filter_kernel<false>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (e != hipSuccess) return e;
+      configured = lds;
+    }
+    hipLaunchKernelGGL(vp8_recon_filter_kernel<false>, dim3(n_frames), dim3(1024), lds, stream, d_frames, d_err,
+                       lead);
+    const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    configured = lds;
   }
-  hipLaunchKernelGGL(vp8_recon_filter_kernel, dim3(n_frames), dim3(1024), lds, stream, d_frames, d_err, lead);
-  return hipGetLastError();
+  if (wide_frames) {
+    const size_t lds = vp8_recon_lds_bytes(0);
+    static bool configured = false;
+    if (lds > 65536 && !configured) {
+      const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&vp8_recon_filter_kernel<true>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (e != hipSuccess) return e;
+      configured = true;
+    }
+    hipLaunchKernelGGL(vp8_recon_filter_kernel<true>, dim3(n_frames), dim3(1024), lds, stream, d_frames, d_err,
+                       lead);
+    return hipGetLastError();
+  }
+  return hipSuccess;
 }
 
 }  // namespace wg

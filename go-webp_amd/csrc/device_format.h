@@ -51,7 +51,7 @@ struct FrameDesc {
   uint8_t* u;
   uint8_t* v;
   uint8_t* rgba;
-  uint64_t pad0;
+  uint8_t* cols;  // K1 column store in global memory (wide frames only, mb_w * 160 B), else null
   int32_t width, height, mb_w, mb_h;
   int32_t y_stride, uv_stride, rgba_stride, filter_type;
   int32_t flags, valid, blocks_bytes, pad2;  // blocks_bytes: size of `blocks` (K1 bounds)

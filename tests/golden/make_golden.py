@@ -650,6 +650,9 @@ LOSSY_CASES = [
     ("noise_130x70_q5", lambda: noise(70, 130, 19, 30), {"quality": 5, "filter_strength": 100}),
     ("synth_256x256_sns100", lambda: synth(256, 256, 20, 20), {"sns": 100, "filter_strength": 40}),
     ("alpha_64x48", lambda: with_alpha(synth(48, 64, 21, 6), 21), {}),
+    # wider than K1's LDS column store (mb_w > 600): the global-store variant
+    ("wide_9617x40", lambda: synth(40, 9617, 22, 6), {"quality": 60}),
+    ("wide_16383x17_simple", lambda: smooth(17, 16383, 23), {"filter_type": 0, "quality": 50}),
 ]
 
 LOSSLESS_CASES = [

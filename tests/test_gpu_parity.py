@@ -141,3 +141,28 @@ def test_yuv_to_rgba_device_stage_vs_oracle():
             torch.cuda.synchronize()
             ref = oracle_yuv_to_rgba(Y[:, :w], U[:, :uw], V[:, :uw], fancy=fancy)
             np.testing.assert_array_equal(out.cpu().numpy(), ref, err_msg=f"{h}x{w} fancy={fancy}")
+
+
+def test_wide_frames_global_column_store(ctx):
+    """Frames wider than K1's LDS column store (mb_w > 600, up to VP8's 16383 px) take the
+    global-store K1 variant: alone, interleaved with narrow frames (both variants launched on
+    one batch), and cropped (K2 over the compact window).  libwebp + oracle parity."""
+    assert webp_amd.vp8_parse(load_lossy("wide_9617x40")[0])[0].mb_w > 600
+    wide = ["wide_9617x40", "wide_16383x17_simple"]
+    for names in (wide, ["wide_9617x40", "synth_80x96", "wide_16383x17_simple", "synth_17x9"]):
+        imgs, status = ctx.decode_batch([load_lossy(n)[0] for n in names])
+        assert (status == 0).all(), status
+        for n, img in zip(names, imgs):
+            np.testing.assert_array_equal(img, load_lossy(n)[1]["rgba"], err_msg=n)
+    d, g = load_lossy("wide_16383x17_simple")
+    for flags, key in ((webp_amd.FLAG_BYPASS_FILTERING, "rgba_nofilter"), (webp_amd.FLAG_NO_FANCY_UPSAMPLING,
+                                                                            "rgba_point")):
+        imgs, status = ctx.decode_batch([d], flags)
+        assert status[0] == 0
+        np.testing.assert_array_equal(imgs[0], g[key], err_msg=key)
+    from oracle_lib import oracle_output
+
+    crop = (9000, 3, 7001, 13)
+    outs, status = ctx.decode_batch_opts([d, load_lossy("wide_9617x40")[0]], webp_amd.options(1, crop))
+    assert status[0] == 0 and status[1] != 0  # the window exceeds the 9617-px frame
+    np.testing.assert_array_equal(outs[0], oracle_output(d, 1, crop))
