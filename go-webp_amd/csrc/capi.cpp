@@ -514,12 +514,23 @@ wg_batch* wg_batch_create_ex(wg_ctx* ctx, const uint8_t* const* data, const size
   uint8_t* h_in = nullptr;
   if (hipHostMalloc(reinterpret_cast<void**>(&h_in), b->in_bytes, hipHostMallocDefault) != hipSuccess)
     return fail(WG_STATUS_OUT_OF_MEMORY);
+  // Staging copies are collected first and run on the host threads afterwards (the
+  // parsed data they read is released only after that).
+  struct CopyJob {
+    uint8_t* dst;
+    const void* src;
+    size_t n;
+  };
+  std::vector<CopyJob> jobs;
+  auto stage = [&](size_t off, const void* src, size_t nbytes) {
+    if (nbytes) jobs.push_back(CopyJob{h_in + off, src, nbytes});
+  };
   // the LLDesc of one lossless stream (transforms in application order = reverse of read
   // order); its coded image and transform data go to the staging buffer
   auto make_ll = [&](wg::VP8LFrame& lf, int w, int h, size_t off_coded, const size_t* off_tdata,
                      size_t off_scratch, uint8_t* rgba, int stride) {
     LLDesc l{};
-    std::memcpy(h_in + off_coded, lf.argb.data(), lf.argb.size() * 4);
+    stage(off_coded, lf.argb.data(), lf.argb.size() * 4);
     l.coded = reinterpret_cast<const uint32_t*>(b->d_in + off_coded);
     l.coded_bytes = (int32_t)(lf.argb.size() * 4);
     l.scratch = ll_two_pass(lf) ? reinterpret_cast<uint32_t*>(b->d_planes + off_scratch) : nullptr;
@@ -534,7 +545,7 @@ wg_batch* wg_batch_create_ex(wg_ctx* ctx, const uint8_t* const* data, const size
     for (int t = 0; t < l.n_stages; ++t) {
       const wg::VP8LTransform& tr = lf.transforms[(size_t)(l.n_stages - 1 - t)];
       const size_t off = off_tdata[l.n_stages - 1 - t];
-      if (!tr.data.empty()) std::memcpy(h_in + off, tr.data.data(), tr.data.size() * 4);
+      stage(off, tr.data.data(), tr.data.size() * 4);
       wg::LLStage& st = l.stages[t];
       st.type = tr.type;
       st.bits = tr.bits;
@@ -549,8 +560,6 @@ wg_batch* wg_batch_create_ex(wg_ctx* ctx, const uint8_t* const* data, const size
     }
     l.valid = 1;
     l.pad1[0] = (uint64_t)wg::vp8l_variant(types, bits, tiles, l.n_stages);  // sort key
-    wg::VP8LFrame().transforms.swap(lf.transforms);
-    std::vector<uint32_t>().swap(lf.argb);
     return l;
   };
   b->desc.assign(n, FrameDesc{});
@@ -568,9 +577,9 @@ wg_batch* wg_batch_create_ex(wg_ctx* ctx, const uint8_t* const* data, const size
       continue;
     }
     const wg_vp8_info& inf = f.sf.info;
-    std::memcpy(h_in + f.off_recs, f.sf.mbs.data(), f.sf.mbs.size() * sizeof(MbRec));
-    std::memcpy(h_in + f.off_rows, f.sf.row_block0.data(), f.sf.row_block0.size() * 4);
-    if (!f.sf.blocks.empty()) std::memcpy(h_in + f.off_blocks, f.sf.blocks.data(), f.sf.blocks.size() * 2);
+    stage(f.off_recs, f.sf.mbs.data(), f.sf.mbs.size() * sizeof(MbRec));
+    stage(f.off_rows, f.sf.row_block0.data(), f.sf.row_block0.size() * 4);
+    stage(f.off_blocks, f.sf.blocks.data(), f.sf.blocks.size() * 2);
     d.mbs = reinterpret_cast<const MbRec*>(b->d_in + f.off_recs);
     d.row_block0 = reinterpret_cast<const uint32_t*>(b->d_in + f.off_rows);
     d.blocks = reinterpret_cast<const int16_t*>(b->d_in + f.off_blocks);
@@ -593,7 +602,7 @@ wg_batch* wg_batch_create_ex(wg_ctx* ctx, const uint8_t* const* data, const size
                                     b->d_planes + f.off_argba, 4 * f.width));
         a.green = b->d_planes + f.off_argba;
       } else {
-        std::memcpy(h_in + f.off_araw, f.alpha_raw, (size_t)f.width * f.height);
+        stage(f.off_araw, f.alpha_raw, (size_t)f.width * f.height);
         a.raw = b->d_in + f.off_araw;
       }
       a.plane = b->d_planes + f.off_aplane;
@@ -608,12 +617,36 @@ wg_batch* wg_batch_create_ex(wg_ctx* ctx, const uint8_t* const* data, const size
       a.win_w = f.out_w;
       a.win_h = f.out_h;
       b->adesc.push_back(a);
-      f.alpha_raw = nullptr;
     }
-    // release host-side copies of the parsed data: the device owns them now
+  }
+  // run the staging copies on the host threads (large ones split into 4 MB pieces)
+  {
+    constexpr size_t kPiece = size_t(4) << 20;
+    std::vector<CopyJob> pieces;
+    for (const CopyJob& j : jobs)
+      for (size_t o = 0; o < j.n; o += kPiece)
+        pieces.push_back(CopyJob{j.dst + o, static_cast<const uint8_t*>(j.src) + o, std::min(kPiece, j.n - o)});
+    std::atomic<size_t> next{0};
+    auto work = [&]() {
+      for (size_t k; (k = next.fetch_add(1)) < pieces.size();) std::memcpy(pieces[k].dst, pieces[k].src, pieces[k].n);
+    };
+    const int t = (int)std::max<size_t>(1, std::min<size_t>((size_t)ctx->host_threads, pieces.size()));
+    std::vector<std::thread> pool;
+    for (int k = 1; k < t; ++k) pool.emplace_back(work);
+    work();
+    for (auto& th : pool) th.join();
+  }
+  // release host-side copies of the parsed data: the device owns them now
+  for (int i = 0; i < n; ++i) {
+    FrameParse& f = b->fp[i];
     std::vector<MbRec>().swap(f.sf.mbs);
-    std::vector<int16_t>().swap(f.sf.blocks);
+    f.sf.blocks.release();
     std::vector<uint32_t>().swap(f.sf.row_block0);
+    wg::VP8LFrame().transforms.swap(f.lf.transforms);
+    std::vector<uint32_t>().swap(f.lf.argb);
+    wg::VP8LFrame().transforms.swap(f.af.transforms);
+    std::vector<uint32_t>().swap(f.af.argb);
+    f.alpha_raw = nullptr;
   }
   if (b->any_crop) {  // K2's view: cropped lossy frames read their compact planes
     b->desc2 = b->desc;

@@ -4,6 +4,8 @@
 #pragma once
 #include <cstddef>
 #include <cstdint>
+#include <cstring>
+#include <memory>
 #include <vector>
 
 #include "../../../include/gowebp_amd.h"
@@ -24,12 +26,39 @@ struct Container {
 
 int parse_container(const uint8_t* data, size_t size, Container* c, wg_features* feat);
 
+// Growable buffer of trivially copyable T without zero-filling on growth (the entropy
+// stage writes every element it keeps).
+template <class T>
+struct PodBuf {
+  std::unique_ptr<T[]> p;
+  size_t n = 0, cap = 0;
+  T* data() { return p.get(); }
+  const T* data() const { return p.get(); }
+  size_t size() const { return n; }
+  bool empty() const { return n == 0; }
+  void clear() { n = 0; }
+  void release() {
+    p.reset();
+    n = cap = 0;
+  }
+  T* reserve_more(size_t k) {  // room for k more elements; returns the end
+    if (n + k > cap) {
+      const size_t nc = n + k > 2 * cap ? n + k : 2 * cap;
+      T* q = new T[nc];
+      if (n) std::memcpy(q, p.get(), n * sizeof(T));
+      p.reset(q);
+      cap = nc;
+    }
+    return p.get() + n;
+  }
+};
+
 // Parsed lossy frame in the device layout.
 struct SparseFrame {
   wg_vp8_info info{};
   std::vector<MbRec> mbs;              // mb_w * mb_h, raster order
   std::vector<uint32_t> row_block0;    // first coefficient block of each MB row
-  std::vector<int16_t> blocks;         // 16 int16 per non-zero 4x4 block, column-major
+  PodBuf<int16_t> blocks;              // 16 int16 per non-zero 4x4 block, column-major
 };
 
 // Entropy-decode one lossy frame.  `dense` (mb_w*mb_h) and/or `sparse` may be null.

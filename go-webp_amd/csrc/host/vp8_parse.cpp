@@ -229,8 +229,12 @@ int get_large_value(BoolReader* br, const uint8_t* p) {  // vp8_dec.go:489-519
 }
 
 // GetCoeffs (vp8_dec.go:522-547).  `prob[n]` = band probas of coefficient n.
-int get_coeffs(BoolReader* br, const BandProbas* const* prob, int ctx, const int* dq, int n,
-               int16_t* out) {
+// kZigzag composed with the raster -> column-major transpose of the device block layout
+// (device_format.h): the sparse path writes coefficients where the kernel reads them.
+constexpr uint8_t kZigzagColMajor[16] = {0, 4, 1, 2, 5, 8, 12, 9, 6, 3, 7, 10, 13, 14, 11, 15};
+
+template <bool kColMajor>
+int get_coeffs_t(BoolReader* br, const BandProbas* const* prob, int ctx, const int* dq, int n, int16_t* out) {
   const uint8_t* p = prob[n]->p[ctx];
   for (; n < 16; ++n) {
     if (!br->get_bit(p[0])) return n;  // previous coeff was last non-zero coeff
@@ -247,9 +251,13 @@ int get_coeffs(BoolReader* br, const BandProbas* const* prob, int ctx, const int
       v = get_large_value(br, p);
       p = p_ctx->p[2];
     }
-    out[kZigzag[n]] = (int16_t)(br->get_signed(v) * dq[n > 0]);  // int16_t store wraps
+    out[kColMajor ? kZigzagColMajor[n] : kZigzag[n]] = (int16_t)(br->get_signed(v) * dq[n > 0]);  // wraps
   }
   return 16;
+}
+
+int get_coeffs(BoolReader* br, const BandProbas* const* prob, int ctx, const int* dq, int n, int16_t* out) {
+  return get_coeffs_t<false>(br, prob, ctx, dq, n, out);
 }
 
 inline uint32_t nz_code_bits(uint32_t nz_coeffs, int nz, int dc_nz) {  // vp8_dec.go:588-598
@@ -408,6 +416,98 @@ int parse_residuals(Decoder* d, MBCtx* mb, MBCtx* left_mb, BoolReader* token_br,
   return !(non_zero_y | non_zero_uv);
 }
 
+// ParseResiduals for the sparse device layout: the same token walk and contexts as
+// parse_residuals, but each 4x4 block is decoded straight into the next free slot of
+// `out` (column-major, kZigzagColMajor) and kept only if some coefficient is non-zero
+// (no 384-coefficient MB buffer, no copy).  Returns the kept-block mask (bit b = block b,
+// blocks 0..15 Y raster, 16..19 U, 20..23 V) and sets *n_kept and block->non_zero_*.
+uint32_t parse_residuals_sparse(Decoder* d, MBCtx* mb, MBCtx* left_mb, BoolReader* token_br, MBOut* block,
+                                const BandProbas* const (*bands)[17], int16_t* out, int* n_kept) {
+  const int seg = block->segment;
+  uint32_t non_zero_y = 0, non_zero_uv = 0, mask = 0;
+  int nb = 0;
+  int16_t dcs[16];
+  const BandProbas* const* ac_proba;
+  int first;
+  auto keep = [&](int16_t* ob, int b) {
+    uint64_t w[4];
+    std::memcpy(w, ob, 32);
+    if (w[0] | w[1] | w[2] | w[3]) {
+      mask |= 1u << b;
+      ++nb;
+    }
+  };
+  if (!block->is_i4x4) {  // parse DC
+    int16_t dc[16] = {0};
+    const int ctx = mb->nz_dc + left_mb->nz_dc;
+    const int nz = get_coeffs_t<false>(token_br, bands[1], ctx, d->dq_y2[seg], 0, dc);
+    mb->nz_dc = left_mb->nz_dc = (nz > 0);
+    if (nz > 1) {
+      int16_t tmp[256];
+      transform_wht(dc, tmp);
+      for (int i = 0; i < 16; ++i) dcs[i] = tmp[16 * i];
+    } else {
+      const int16_t dc0 = (int16_t)((dc[0] + 3) >> 3);
+      for (int i = 0; i < 16; ++i) dcs[i] = dc0;
+    }
+    first = 1;
+    ac_proba = bands[0];
+  } else {
+    std::memset(dcs, 0, sizeof(dcs));
+    first = 0;
+    ac_proba = bands[3];
+  }
+  uint8_t tnz = mb->nz & 0x0f, lnz = left_mb->nz & 0x0f;
+  for (int y = 0; y < 4; ++y) {
+    int l = lnz & 1;
+    uint32_t nz_coeffs = 0;
+    for (int x = 0; x < 4; ++x) {
+      int16_t* ob = out + 16 * nb;
+      std::memset(ob, 0, 32);
+      ob[0] = dcs[4 * y + x];
+      const int ctx = l + (tnz & 1);
+      const int nz = get_coeffs_t<true>(token_br, ac_proba, ctx, d->dq_y1[seg], first, ob);
+      l = (nz > first);
+      tnz = (uint8_t)((tnz >> 1) | (l << 7));
+      nz_coeffs = nz_code_bits(nz_coeffs, nz, ob[0] != 0);
+      keep(ob, 4 * y + x);
+    }
+    tnz >>= 4;
+    lnz = (uint8_t)((lnz >> 1) | (l << 7));
+    non_zero_y = (non_zero_y << 8) | nz_coeffs;
+  }
+  uint32_t out_t_nz = tnz, out_l_nz = lnz >> 4;
+  for (int ch = 0; ch < 4; ch += 2) {
+    uint32_t nz_coeffs = 0;
+    tnz = (uint8_t)(mb->nz >> (4 + ch));
+    lnz = (uint8_t)(left_mb->nz >> (4 + ch));
+    for (int y = 0; y < 2; ++y) {
+      int l = lnz & 1;
+      for (int x = 0; x < 2; ++x) {
+        int16_t* ob = out + 16 * nb;
+        std::memset(ob, 0, 32);
+        const int ctx = l + (tnz & 1);
+        const int nz = get_coeffs_t<true>(token_br, bands[2], ctx, d->dq_uv[seg], 0, ob);
+        l = (nz > 0);
+        tnz = (uint8_t)((tnz >> 1) | (l << 3));
+        nz_coeffs = nz_code_bits(nz_coeffs, nz, ob[0] != 0);
+        keep(ob, 16 + 2 * ch + 2 * y + x);
+      }
+      tnz >>= 2;
+      lnz = (uint8_t)((lnz >> 1) | (l << 5));
+    }
+    non_zero_uv |= nz_coeffs << (4 * ch);
+    out_t_nz |= (uint32_t)(tnz << 4) << ch;
+    out_l_nz |= (uint32_t)(lnz & 0xf0) << ch;
+  }
+  mb->nz = (uint8_t)out_t_nz;
+  left_mb->nz = (uint8_t)out_l_nz;
+  block->non_zero_y = non_zero_y;
+  block->non_zero_uv = non_zero_uv;
+  *n_kept = nb;
+  return mask;
+}
+
 int get_headers(Decoder* d, const uint8_t* buf, size_t buf_size) {  // vp8_dec.go:362-484
   if (buf_size < 4) return WG_STATUS_NOT_ENOUGH_DATA;
   const uint32_t bits = buf[0] | (buf[1] << 8) | (buf[2] << 16);
@@ -509,14 +609,22 @@ int vp8_parse(const uint8_t* data, size_t size, int flags, wg_vp8_info* info, wg
       parse_intra_mode(d, &intra_t[4 * (size_t)mb_x], intra_l, &blk);
       MBCtx* mb = &mb_info[1 + mb_x];
       int skip = d->use_skip_proba ? blk.skip : 0;
+      uint32_t mask = 0;
+      int n_kept = 0;
       if (!skip) {
-        skip = parse_residuals(d, mb, left, token_br, &blk, bands_ptr);
+        if (dense) {
+          skip = parse_residuals(d, mb, left, token_br, &blk, bands_ptr);
+        } else {
+          int16_t* ob = sparse->blocks.reserve_more(24 * 16);
+          mask = parse_residuals_sparse(d, mb, left, token_br, &blk, bands_ptr, ob, &n_kept);
+          skip = !(blk.non_zero_y | blk.non_zero_uv);
+        }
       } else {
         left->nz = mb->nz = 0;
         if (!blk.is_i4x4) left->nz_dc = mb->nz_dc = 0;
         blk.non_zero_y = 0;
         blk.non_zero_uv = 0;
-        std::memset(blk.coeffs, 0, sizeof(blk.coeffs));
+        if (dense) std::memset(blk.coeffs, 0, sizeof(blk.coeffs));
       }
       uint8_t fi[4] = {0, 0, 0, 0};
       if (d->filter_type > 0) {
@@ -543,22 +651,21 @@ int vp8_parse(const uint8_t* data, size_t size, int flags, wg_vp8_info* info, wg
       }
       if (sparse) {
         MbRec r{0, 0, 0, 0};
-        uint32_t mask = 0;
-        if (blk.non_zero_y | blk.non_zero_uv) {
+        if (dense && (blk.non_zero_y | blk.non_zero_uv)) {  // dense + sparse: pack from the MB buffer
+          int16_t* ob = sparse->blocks.reserve_more(24 * 16);
           for (int b = 0; b < 24; ++b) {
             const int16_t* cb = blk.coeffs + 16 * b;
             uint64_t any = 0;
             for (int k = 0; k < 16; ++k) any |= (uint16_t)cb[k];
             if (!any) continue;
             mask |= 1u << b;
-            const size_t off = sparse->blocks.size();
-            sparse->blocks.resize(off + 16);
-            int16_t* ob = &sparse->blocks[off];
             for (int cc = 0; cc < 4; ++cc)
-              for (int k = 0; k < 4; ++k) ob[4 * cc + k] = cb[4 * k + cc];
-            ++nblocks;
+              for (int k = 0; k < 4; ++k) ob[16 * n_kept + 4 * cc + k] = cb[4 * k + cc];
+            ++n_kept;
           }
         }
+        sparse->blocks.n += 16 * (size_t)n_kept;
+        nblocks += n_kept;
         r.flags = mask | ((uint32_t)blk.is_i4x4 << kI4Shift) |
                   ((uint32_t)(blk.is_i4x4 ? 0 : blk.imodes[0]) << kYModeShift) |
                   ((uint32_t)blk.uvmode << kUVModeShift);

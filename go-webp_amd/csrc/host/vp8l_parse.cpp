@@ -47,7 +47,7 @@ class BitReader {
   BitReader(const uint8_t* p, size_t n) : p_(p), n_(n) {}
   uint32_t read(int nbits) {
     if (nbits == 0) return 0;
-    fill();
+    if (avail_ < nbits) fill();
     if (avail_ < nbits) {
       eos_ = true;
       avail_ = 0;
@@ -61,7 +61,7 @@ class BitReader {
   }
   // At least kMaxCodeLength bits (zero-padded past the end) for a table lookup.
   uint32_t peek15() {
-    fill();
+    if (avail_ < kMaxCodeLength) fill();
     return (uint32_t)(val_ & 0x7fff);
   }
   void skip(int nbits) {
@@ -77,7 +77,14 @@ class BitReader {
   bool eos() const { return eos_; }
 
  private:
-  void fill() {
+  void fill() {  // 32 bits at a time away from the end, then byte by byte
+    if (avail_ <= 32 && pos_ + 4 <= n_) {
+      uint32_t w;
+      std::memcpy(&w, p_ + pos_, 4);
+      val_ |= (uint64_t)w << avail_;
+      pos_ += 4;
+      avail_ += 32;
+    }
     while (avail_ <= 56 && pos_ < n_) {
       val_ |= (uint64_t)p_[pos_++] << avail_;
       avail_ += 8;
