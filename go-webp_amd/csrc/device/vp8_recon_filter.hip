@@ -73,6 +73,9 @@ constexpr uint32_t kDrop = 0x80000000u;  // buffer offset beyond any frame: stor
 #ifdef WG_K1_SECTION_TIMING
 constexpr int kSections = 14;
 __device__ unsigned long long g_k1_sections[kSections];
+// timeline: per workgroup (frame) the start time and each wave's exit time (s_memrealtime)
+constexpr int kTimelineFrames = 1024;
+__device__ unsigned long long g_k1_timeline[kTimelineFrames][1 + kWaves];
 #define K1_SECT_DECL() uint64_t sect_acc[kSections] = {}, sect_t = 0
 #define K1_SECT_START() (sect_t = __builtin_amdgcn_s_memtime())
 #define K1_SECT(id)                                       \
@@ -83,14 +86,23 @@ __device__ unsigned long long g_k1_sections[kSections];
   } while (0)
 #define K1_SECT_FLUSH()                                                        \
   do {                                                                         \
-    if (lane == 0)                                                             \
+    if (lane == 0) {                                                           \
       for (int s_ = 0; s_ < kSections; ++s_) atomicAdd(&g_k1_sections[s_], sect_acc[s_]); \
+      if (blockIdx.x < kTimelineFrames)                                        \
+        g_k1_timeline[blockIdx.x][1 + wave] = __builtin_amdgcn_s_memrealtime(); \
+    }                                                                          \
+  } while (0)
+#define K1_TIMELINE_START()                                                    \
+  do {                                                                         \
+    if (threadIdx.x == 0 && blockIdx.x < kTimelineFrames)                     \
+      g_k1_timeline[blockIdx.x][0] = __builtin_amdgcn_s_memrealtime();         \
   } while (0)
 #else
 #define K1_SECT_DECL() (void)0
 #define K1_SECT_START() (void)0
 #define K1_SECT(id) (void)0
 #define K1_SECT_FLUSH() (void)0
+#define K1_TIMELINE_START() (void)0
 #endif
 
 __device__ __forceinline__ void lds_sync() {
@@ -427,6 +439,7 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
   // per MB column c: cols + c*kColBytes: [0..15] ytop Y, [16..23] U, [24..31] V, [32..159] fbot
   if (threadIdx.x < kWaves) progress[threadIdx.x] = 0;
   for (int t = threadIdx.x; t < 160; t += blockDim.x) tab[t] = kPred4Table[t];
+  K1_TIMELINE_START();
   __syncthreads();
 
   for (int k = wave; 2 * k < mb_h; k += kWaves) {
@@ -782,6 +795,14 @@ extern "C" int wg_debug_k1_sections(unsigned long long* out, int n, int reset) {
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_k1_sections), z, sizeof(z)) != hipSuccess) return -1;
   }
   return n;
+}
+
+// per frame: start, then the exit time of each of the 16 waves (memrealtime ticks, 100 MHz)
+extern "C" int wg_debug_k1_timeline(unsigned long long* out, int n_frames) {
+  if (n_frames > kTimelineFrames) n_frames = kTimelineFrames;
+  const size_t bytes = (size_t)n_frames * (1 + kWaves) * sizeof(unsigned long long);
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_k1_timeline), bytes) != hipSuccess) return -1;
+  return n_frames;
 }
 #endif
 

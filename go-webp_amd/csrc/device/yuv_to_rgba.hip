@@ -39,26 +39,40 @@ constexpr int kWavesPerWG = 4;
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-// clamp(v, 0, 255) as an opaque v_med3_i32.  Written in asm on purpose: ROCm 7.2 fuses
-// two `clamp(x >> 6)` + byte-pack sequences into gfx950's v_ashr_pk_u8_i32 and then
-// assumes its upper 16 bits are zero, which corrupted the B byte whenever G saturated
-// low (caught by tests/test_gpu_parity.py).
-__device__ __forceinline__ uint32_t clamp_u8(int v) {
-  int r;
-  asm("v_med3_i32 %0, %1, 0, %2" : "=v"(r) : "v"(v), "s"(255));
-  return (uint32_t)r;
+// Packed 16-bit arithmetic: two pixels per VALU instruction (v_pk_mad_u16, v_pk_sub_u16
+// with clamp, v_pk_min_u16, v_pk_lshrrev_b16).  Every VP8YuvToRgba term fits 16 bits once
+// MultHi(a, c) = (a*c) >> 8 is split at the multiplier's high byte, c = 256*h + l:
+// MultHi(a, c) = h*a + ((l*a) >> 8) exactly (a <= 255, l*a < 2^16).  The signed
+// `(sum - k) >> 6` followed by Clip8 is min(sat_sub(sum, k) >> 6, 255): a negative sum
+// clips to 0 either way.  Exhaustively checked over all (y, u, v) against the reference
+// formulas (tests/test_oracle.py::test_packed_yuv_formulas).
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ u16x2 as_u16x2(uint32_t w) { return __builtin_bit_cast(u16x2, w); }
+__device__ __forceinline__ uint32_t as_u32(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+__device__ __forceinline__ u16x2 splat(unsigned short c) { return u16x2{c, c}; }
+__device__ __forceinline__ u16x2 sat_sub(u16x2 a, unsigned short c) { return __builtin_elementwise_sub_sat(a, splat(c)); }
+__device__ __forceinline__ u16x2 sat_sub(u16x2 a, u16x2 b) { return __builtin_elementwise_sub_sat(a, b); }
+__device__ __forceinline__ u16x2 min255(u16x2 a) { return __builtin_elementwise_min(a, splat(255)); }
+
+// VP8YuvToRgba (conversion.go:28-49, A = 0xff) of two pixels; y, u, v hold one 8-bit
+// sample per 16-bit half.  Returns the two RGBA dwords.
+__device__ __forceinline__ uint2 yuv_to_rgba2(u16x2 y, u16x2 u, u16x2 v) {
+  const u16x2 y1 = y * splat(74) + ((y * splat(133)) >> 8);                              // MultHi(y, 19077)
+  const u16x2 r = min255(sat_sub(y1 + v * splat(102) + ((v * splat(37)) >> 8), 14234) >> 6);  // + MultHi(v, 26149)
+  const u16x2 gu = u * splat(25) + ((u * splat(19)) >> 8);                               // MultHi(u, 6419)
+  const u16x2 gv = v * splat(52) + (v >> 5);                                             // MultHi(v, 13320)
+  const u16x2 g = min255(sat_sub(sat_sub(y1 + splat(8708), gu), gv) >> 6);
+  const u16x2 b = min255(sat_sub(y1 + u * splat(129) + ((u * splat(26)) >> 8), 17685) >> 6);  // + MultHi(u, 33050)
+  // bytes: t = R0 G0 R1 G1; px = R G B 0xff (perm selector 0x0d = 0xff)
+  const uint32_t t = __builtin_amdgcn_perm(as_u32(g), as_u32(r), 0x06020400u);
+  return make_uint2(__builtin_amdgcn_perm(as_u32(b), t, 0x0d040100u), __builtin_amdgcn_perm(as_u32(b), t, 0x0d060302u));
 }
 
-__device__ __forceinline__ uint32_t yuv_to_rgba(int y, int u, int v) {
-  // MultHi(a, c) = (a*c) >> 8; Clip8(v) = clamp(v >> 6, 0, 255) (YUV_FIX2 = 6)
-  const int y1 = __mul24(y, 19077) >> 8;
-  const int r = (y1 + (__mul24(v, 26149) >> 8) - 14234) >> 6;
-  const int g = (y1 - (__mul24(u, 6419) >> 8) - (__mul24(v, 13320) >> 8) + 8708) >> 6;
-  const int b = (y1 + (__mul24(u, 33050) >> 8) - 17685) >> 6;
-  return clamp_u8(r) | (clamp_u8(g) << 8) | (clamp_u8(b) << 16) | 0xff000000u;
+// bytes i and j of w as the two 16-bit halves
+__device__ __forceinline__ u16x2 bytes2(uint32_t w, int i, int j) {
+  return as_u16x2(__builtin_amdgcn_perm(0u, w, 0x0c000c00u | (uint32_t)i | ((uint32_t)j << 16)));
 }
-
-__device__ __forceinline__ int byte_of(uint32_t w, int i) { return (w >> (8 * i)) & 0xff; }
 
 __device__ __forceinline__ uint32_t bperm(uint32_t v, int src_lane) {
   return (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane << 2, (int)v);
@@ -134,21 +148,22 @@ __device__ __forceinline__ ChromaWin make_win(const ChromaRaw& r, int cb0, int u
   return w;
 }
 
-// 4 pixels of group k: near/far chroma windows (n, f), luma dword.
+// 4 pixels of group k: near/far chroma windows (n, f), luma dword.  Per chroma plane the
+// vertical blend a[j] = 3*n[j] + f[j] is computed as two packed pairs (a0, a2), (a1, a3);
+// pixel 2c takes (3*a[near] + a[far] + 8) >> 4 with far = c-1, pixel 2c+1 far = c+1.
+__device__ __forceinline__ void upsample4(uint32_t n, uint32_t f, u16x2& p01, u16x2& p23) {
+  const u16x2 a02 = as_u16x2(n & 0x00ff00ffu) * splat(3) + as_u16x2(f & 0x00ff00ffu);
+  const u16x2 a13 = bytes2(n, 1, 3) * splat(3) + bytes2(f, 1, 3);
+  p01 = (a13.xx * splat(3) + (a02 + splat(8))) >> 4;  // (3a1 + a0 + 8, 3a1 + a2 + 8) >> 4
+  p23 = (a02.yy * splat(3) + (a13 + splat(8))) >> 4;  // (3a2 + a1 + 8, 3a2 + a3 + 8) >> 4
+}
+
 __device__ __forceinline__ u32x4 convert_group(uint32_t nu, uint32_t fu, uint32_t nv, uint32_t fv, uint32_t yw) {
-  int a[4], b[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    a[j] = 3 * byte_of(nu, j) + byte_of(fu, j);
-    b[j] = 3 * byte_of(nv, j) + byte_of(fv, j);
-  }
-  // pixel 2c: near column c, far column c-1; pixel 2c+1: far column c+1
-  const int u0 = (3 * a[1] + a[0] + 8) >> 4, u1 = (3 * a[1] + a[2] + 8) >> 4;
-  const int u2 = (3 * a[2] + a[1] + 8) >> 4, u3 = (3 * a[2] + a[3] + 8) >> 4;
-  const int v0 = (3 * b[1] + b[0] + 8) >> 4, v1 = (3 * b[1] + b[2] + 8) >> 4;
-  const int v2 = (3 * b[2] + b[1] + 8) >> 4, v3 = (3 * b[2] + b[3] + 8) >> 4;
-  return u32x4{yuv_to_rgba(byte_of(yw, 0), u0, v0), yuv_to_rgba(byte_of(yw, 1), u1, v1),
-               yuv_to_rgba(byte_of(yw, 2), u2, v2), yuv_to_rgba(byte_of(yw, 3), u3, v3)};
+  u16x2 u01, u23, v01, v23;
+  upsample4(nu, fu, u01, u23);
+  upsample4(nv, fv, v01, v23);
+  const uint2 a = yuv_to_rgba2(bytes2(yw, 0, 1), u01, v01), b = yuv_to_rgba2(bytes2(yw, 2, 3), u23, v23);
+  return u32x4{a.x, a.y, b.x, b.y};
 }
 
 __device__ __forceinline__ void store_group(gptr<uint8_t> dst, u32x4 px, int nvalid, bool aligned) {
@@ -238,14 +253,16 @@ __global__ void __launch_bounds__(64 * kWavesPerWG) yuv_to_rgba_kernel(const Fra
         const int x = xl + 256 * k;
         const int nvalid = W - x;
         if (nvalid <= 0) continue;
-        const int u0 = byte_of(c.p[k], 0), u1 = byte_of(c.p[k], 1), v0 = byte_of(c.p[k], 2), v1 = byte_of(c.p[k], 3);
+        // pixels 0,1 take chroma column cb, pixels 2,3 column cb+1
+        const uint32_t cp = c.p[k];
+        const u16x2 u0 = bytes2(cp, 0, 0), u1 = bytes2(cp, 1, 1), v0 = bytes2(cp, 2, 2), v1 = bytes2(cp, 3, 3);
 #pragma unroll
         for (int r = 0; r < 2; ++r) {
           const int yr = 2 * p + r;
           if (yr >= H) break;
           const uint32_t yw = r ? yB[k] : yA[k];
-          const u32x4 px{yuv_to_rgba(byte_of(yw, 0), u0, v0), yuv_to_rgba(byte_of(yw, 1), u0, v0),
-                         yuv_to_rgba(byte_of(yw, 2), u1, v1), yuv_to_rgba(byte_of(yw, 3), u1, v1)};
+          const uint2 a = yuv_to_rgba2(bytes2(yw, 0, 1), u0, v0), b = yuv_to_rgba2(bytes2(yw, 2, 3), u1, v1);
+          const u32x4 px{a.x, a.y, b.x, b.y};
           store_group(out + (size_t)yr * os + 4 * x, px, nvalid, aligned);
         }
       }

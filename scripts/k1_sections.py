@@ -49,6 +49,24 @@ def main():
     print(f"workload {args.workload} batch {args.batch} runs {args.runs}: K1 {ms[0]:.3f} ms, K2 {ms[1]:.3f} ms")
     for n, v in sorted(zip(NAMES, buf), key=lambda t: -t[1]):
         print(f"  {n:10s} {100.0 * v / tot:6.2f}%  {v / args.runs / 1e6:10.1f} Mcyc/run")
+    # timeline of the last run: per frame, how long each wave sat idle after its last pair
+    L.wg_debug_k1_timeline.restype = C.c_int
+    L.wg_debug_k1_timeline.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
+    nf = min(args.batch, 1024)
+    tl = (C.c_ulonglong * (nf * 17))()
+    L.wg_debug_k1_timeline(tl, nf)
+    import numpy as np
+    t = np.frombuffer(tl, dtype=np.uint64).reshape(nf, 17).astype(np.int64)
+    start, ends = t[:, :1], t[:, 1:]
+    dur = ends.max(1) - start[:, 0]
+    idle = (ends.max(1, keepdims=True) - ends).sum(1) / (16.0 * dur)
+    srt = np.sort(ends - start, axis=1)
+    print(f"timeline (100 MHz ticks): frame span mean {dur.mean() / 100:.1f} us (min {dur.min() / 100:.1f}, "
+          f"max {dur.max() / 100:.1f}); idle wave-time after exit {100 * idle.mean():.1f}%")
+    print("  mean exit time of the k-th wave to finish, % of frame span:",
+          " ".join(f"{100 * (srt[:, k] / dur).mean():.0f}" for k in range(16)))
+    st = start[:, 0] - start.min()
+    print(f"  frame start spread {st.max() / 100:.1f} us; kernel span {(ends.max() - start.min()) / 100:.1f} us")
     b.close()
     ctx.close()
 

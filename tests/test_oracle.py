@@ -148,6 +148,41 @@ def test_upsampler_closed_form():
         assert (got[..., 3] == 255).all()
 
 
+def test_packed_yuv_formulas():
+    """K2's packed 16-bit VP8YuvToRgba (yuv_to_rgba.hip::yuv_to_rgba2) == conversion.go:28-49
+    for every (y, u, v): MultHi split at the multiplier's high byte, saturating subtract
+    before the >> 6, every intermediate within 16 bits unsigned.  And the packed vertical
+    blend + horizontal taps (upsample4) stay within 16 bits."""
+    y, u, v = (a.ravel().astype(np.int64) for a in np.meshgrid(*(np.arange(256),) * 3, indexing="ij"))
+
+    def mh(a, c):
+        return (a * c) >> 8
+
+    def c8(x):
+        return np.clip(x >> 6, 0, 255)
+    R = c8(mh(y, 19077) + mh(v, 26149) - 14234)
+    G = c8(mh(y, 19077) - mh(u, 6419) - mh(v, 13320) + 8708)
+    B = c8(mh(y, 19077) + mh(u, 33050) - 17685)
+
+    def u16(x):
+        assert x.min() >= 0 and x.max() < 65536
+        return x
+
+    def sat(a, b):
+        return np.maximum(a - b, 0)
+    y1 = u16(74 * y + (u16(133 * y) >> 8))
+    r = np.minimum(sat(u16(y1 + u16(102 * v + (u16(37 * v) >> 8))), 14234) >> 6, 255)
+    gu = u16(25 * u + (u16(19 * u) >> 8))
+    gv = u16(52 * v + (v >> 5))
+    g = np.minimum(sat(sat(u16(y1 + 8708), gu), gv) >> 6, 255)
+    b = np.minimum(sat(u16(y1 + u16(129 * u + (u16(26 * u) >> 8))), 17685) >> 6, 255)
+    np.testing.assert_array_equal(r, R)
+    np.testing.assert_array_equal(g, G)
+    np.testing.assert_array_equal(b, B)
+    a = 3 * 255 + 255
+    assert 3 * a + a + 8 < 65536
+
+
 def test_bench_c1_frame_sha256():
     """Plumbing config C1 (512x512 lossy, webp.Decode on the CPU path): parse + oracle
     reproduce libwebp's RGBA bit for bit (SHA-256 from the manifest)."""
