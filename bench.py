@@ -150,6 +150,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (host in, host out) leg")
+    ap.add_argument("--emit", choices=("fused", "separate"), default="fused",
+                    help="lossy RGBA from K1's tail (default) or a separate K2 launch")
     ap.add_argument("--host-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
     args = ap.parse_args()
 
@@ -180,6 +182,7 @@ def main():
     if not (b.status == 0).all():
         raise SystemExit(f"rank {rank}: frames failed to parse: {b.status}")
     stream = torch.cuda.current_stream().cuda_stream
+    b.set_emit(args.emit == "separate")
 
     for _ in range(args.warmup):
         b.run(stream)
@@ -194,8 +197,19 @@ def main():
     torch.cuda.synchronize()
     barrier()
     dt = time.perf_counter() - t0
-    kms = b.kernel_ms()  # per-launch averages over the timed steps (HIP events): K1..K4
+    kms = list(b.kernel_ms())  # per-launch averages over the timed steps (HIP events): K1..K4
     kby = b.kernel_bytes()
+    stage_ms = 0.0
+    if kms[0] > 0 and kms[1] == 0:
+        # the metric's YUV->RGBA stage, which K1's tail performs inside the timed steps, timed
+        # alone (K2 over the same reconstructed planes) for its own roofline figure
+        for _ in range(2):
+            b.run_emit(stream)
+        torch.cuda.synchronize()
+        b.kernel_ms()
+        for _ in range(args.steps):
+            b.run_emit(stream)
+        stage_ms = b.kernel_ms()[1]
     px_rank = b.pixels
     dt, total_px = reduce_job(dist, "cuda", dt, px_rank * args.steps)
     value = total_px / dt / 1e6
@@ -211,6 +225,10 @@ def main():
         ran = [k for k in range(len(KERNELS)) if kms[k] > 0]
         roofs = {KERNELS[k]: roof(kby[k], kms[k], KERNELS[k]) for k in ran}
         dominant = roofs[KERNELS[max(ran, key=lambda k: kms[k])]]
+        if stage_ms > 0:
+            roofs["yuv_to_rgba_kernel"] = dict(roof(kby[1], stage_ms, "yuv_to_rgba_kernel"),
+                                               note="stage timed alone over the same planes; in the "
+                                                    "timed steps K1's tail performs it (--emit fused)")
         out = {
             "metric": "decoded MPixels/sec at 1/2/4/8 GPUs; % HBM roofline (YUV->RGBA)",
             "value": round(value, 1),
@@ -230,6 +248,7 @@ def main():
                        "inputs": "resident in HBM (host entropy stage + H2D outside the timed region)"},
             "roofline": dominant,
             "kernel_ms": {KERNELS[k]: round(kms[k], 4) for k in ran},
+            "lossy_emit": args.emit if kms[0] > 0 else None,
             "host_prepare_s": round(t_prep, 3),
         }
         if "yuv_to_rgba_kernel" in roofs:

@@ -68,6 +68,7 @@ struct FrameParse {
 
 struct Timing {
   hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+  bool ran[4] = {false, false, false, false};  // K1, K2, K3, K4 launched in this run
 };
 
 // Does the lossless frame need a second pass (predictor and color indexing both present)?
@@ -150,6 +151,7 @@ struct wg_batch {
   int n_lossy = 0, n_lossless = 0, n_alpha = 0, n_k3 = 0;
   wg_decoder_options opt{};          // output colorspace, cropping, flip (f4)
   bool any_crop = false;             // K2 reads compact cropped planes through desc2
+  bool fused = false;                // lossy RGBA emitted by K1's tail (wg::kFrameEmitRgba), no K2 launch
   std::vector<FrameDesc> desc2;
   FrameDesc* d_desc2 = nullptr;
   int max_out_w = 1, max_out_h = 1;
@@ -164,6 +166,7 @@ struct wg_batch {
   int n_valid = 0;
   int64_t pixels = 0;
   double kbytes[4] = {0, 0, 0, 0};
+  double k1_fused_bytes = 0;  // K1 with its RGBA tail: inputs + RGBA (planes are an intermediate)
   std::vector<Timing> timings;  // one per run since the last query
   size_t n_runs_pending = 0;
 };
@@ -466,6 +469,8 @@ wg_batch* wg_batch_create_ex(wg_ctx* ctx, const uint8_t* const* data, const size
     // planes; K2 reads cropped planes, writes RGBA.
     const double uvpx = 2.0 * ((inf.width + 1) / 2) * (double)((inf.height + 1) / 2);
     k1 += (double)nmb * sizeof(MbRec) + inf.mb_h * 4.0 + f.sf.blocks.size() * 2.0 + nmb * 384.0;
+    b->k1_fused_bytes += (double)nmb * sizeof(MbRec) + inf.mb_h * 4.0 + f.sf.blocks.size() * 2.0 +
+                         4.0 * inf.width * (double)inf.height;
     const double opx = (double)f.out_w * f.out_h;
     k2 += opx + 2.0 * ((f.out_w + 1) / 2) * (double)((f.out_h + 1) / 2) + 4.0 * opx;
     (void)uvpx;
@@ -648,6 +653,12 @@ wg_batch* wg_batch_create_ex(wg_ctx* ctx, const uint8_t* const* data, const size
     std::vector<uint32_t>().swap(f.af.argb);
     f.alpha_raw = nullptr;
   }
+  // Full-frame RGBA (no crop window anywhere in the batch): K1 converts each frame in its
+  // own tail instead of a separate K2 launch (wg_batch_set_emit() switches back).
+  b->fused = !b->any_crop;
+  if (b->fused)
+    for (int i = 0; i < n; ++i)
+      if (b->desc[i].valid) b->desc[i].flags |= wg::kFrameEmitRgba;
   if (b->any_crop) {  // K2's view: cropped lossy frames read their compact planes
     b->desc2 = b->desc;
     for (int i = 0; i < n; ++i) {
@@ -701,6 +712,10 @@ int wg_batch_run(wg_batch* b, void* stream) {
     b->timings.push_back(t);
   }
   Timing& t = b->timings[b->n_runs_pending++];
+  t.ran[0] = b->n_lossy > 0;
+  t.ran[1] = b->n_lossy > 0 && !b->fused;
+  t.ran[2] = b->n_k3 > 0;
+  t.ran[3] = b->n_alpha > 0;
   hipEventRecord(t.ev[0], s);
   if (b->n_lossy > 0) {
     hipError_t e = wg::launch_vp8_recon_filter(b->d_desc, b->n, b->max_mb_w, b->n_lossy > b->n_wide,
@@ -708,7 +723,7 @@ int wg_batch_run(wg_batch* b, void* stream) {
     if (e != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
   }
   hipEventRecord(t.ev[1], s);
-  if (b->n_lossy > 0) {
+  if (t.ran[1]) {
     if (b->any_crop) {
       // the crop windows of the reconstructed planes (even left/top, so chroma is aligned):
       // upsampled as standalone images, as EmitFancyRGB / EmitSampledRGB see them
@@ -754,19 +769,21 @@ int wg_batch_kernel_ms(const wg_batch* bc, float* ms, int n_ms) {
   for (int k = 0; k < n_ms; ++k) ms[k] = 0.f;
   if (b->n_runs_pending == 0) return WG_STATUS_OK;
   double acc[4] = {0, 0, 0, 0};
+  int cnt[4] = {0, 0, 0, 0};
   for (size_t i = 0; i < b->n_runs_pending; ++i) {
     Timing& t = b->timings[i];
     if (hipEventSynchronize(t.ev[4]) != hipSuccess) return WG_STATUS_USER_ABORT;
     for (int k = 0; k < 4; ++k) {
+      if (!t.ran[k]) continue;
       float a = 0;
       hipEventElapsedTime(&a, t.ev[k], t.ev[k + 1]);
       acc[k] += a;
+      cnt[k]++;
     }
   }
   int err = 0;
   if (hipMemcpy(&err, b->d_err, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess || err) return WG_STATUS_USER_ABORT;
-  const bool ran[4] = {b->n_lossy > 0, b->n_lossy > 0, b->n_k3 > 0, b->n_alpha > 0};
-  for (int k = 0; k < std::min(n_ms, 4); ++k) ms[k] = ran[k] ? (float)(acc[k] / b->n_runs_pending) : 0.f;
+  for (int k = 0; k < std::min(n_ms, 4); ++k) ms[k] = cnt[k] ? (float)(acc[k] / cnt[k]) : 0.f;
   b->n_runs_pending = 0;
   return WG_STATUS_OK;
 }
@@ -774,7 +791,43 @@ int wg_batch_kernel_ms(const wg_batch* bc, float* ms, int n_ms) {
 int wg_batch_kernel_bytes(const wg_batch* b, double* bytes, int n_bytes) {
   if (!b || !bytes || n_bytes < 1) return WG_STATUS_INVALID_PARAM;
   for (int k = 0; k < n_bytes; ++k) bytes[k] = k < 4 ? b->kbytes[k] : 0.0;
+  if (b->fused) bytes[0] = b->k1_fused_bytes;
   return WG_STATUS_OK;
+}
+
+int wg_batch_set_emit(wg_batch* b, int separate) {
+  if (!b) return WG_STATUS_INVALID_PARAM;
+  if (!separate && b->any_crop) return WG_STATUS_INVALID_PARAM;  // crop windows need K2
+  if (b->fused == !separate) return WG_STATUS_OK;
+  b->fused = !separate;
+  for (FrameDesc& d : b->desc)
+    if (d.valid) d.flags = b->fused ? (d.flags | wg::kFrameEmitRgba) : (d.flags & ~wg::kFrameEmitRgba);
+  hipSetDevice(b->ctx->device);
+  hipError_t e = hipMemcpyAsync(b->d_desc, b->desc.data(), sizeof(FrameDesc) * (size_t)b->n, hipMemcpyHostToDevice,
+                                b->ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(b->ctx->stream);
+  return e == hipSuccess ? WG_STATUS_OK : WG_STATUS_USER_ABORT;
+}
+
+int wg_batch_run_emit(wg_batch* b, void* stream) {
+  if (!b) return WG_STATUS_INVALID_PARAM;
+  if (b->n_lossy == 0 || b->any_crop) return WG_STATUS_OK;
+  hipSetDevice(b->ctx->device);
+  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : b->ctx->stream;
+  if (b->n_runs_pending >= b->timings.size()) {
+    Timing t;
+    for (auto& e : t.ev)
+      if (hipEventCreate(&e) != hipSuccess) return WG_STATUS_OUT_OF_MEMORY;
+    b->timings.push_back(t);
+  }
+  Timing& t = b->timings[b->n_runs_pending++];
+  t.ran[0] = t.ran[2] = t.ran[3] = false;
+  t.ran[1] = true;
+  for (int k = 0; k < 2; ++k) hipEventRecord(t.ev[k], s);
+  hipError_t e = wg::launch_yuv_to_rgba(b->d_desc, nullptr, b->n, b->max_out_w, b->max_out_h,
+                                        (b->flags & WG_FLAG_NO_FANCY_UPSAMPLING) ? 0 : 1, s);
+  for (int k = 2; k < 5; ++k) hipEventRecord(t.ev[k], s);
+  return e == hipSuccess ? WG_STATUS_OK : WG_STATUS_UNSUPPORTED_FEATURE;
 }
 
 int wg_batch_size(const wg_batch* b) { return b ? b->n : 0; }

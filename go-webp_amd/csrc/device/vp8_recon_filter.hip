@@ -42,6 +42,7 @@
 
 #include "../device_format.h"
 #include "kernels.h"
+#include "yuv_rgba_strip.h"
 
 namespace wg {
 namespace {
@@ -387,6 +388,51 @@ __device__ __forceinline__ Coefs load_coefs(__amdgpu_buffer_rsrc_t blks, uint32_
   return c;
 }
 
+// Bounded LDS spin (workgroup-scope acquire) until *p >= need; false after 2 s.
+__device__ __forceinline__ bool wait_at_least(uint32_t* p, uint32_t need) {
+  if (__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= need) return true;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
+    __builtin_amdgcn_s_sleep(8);
+    if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) return false;
+  }
+  return true;
+}
+
+// K1's tail: the frame's YUV420 -> RGBA (K2's strip conversion, yuv_rgba_strip.h) done by
+// the waves whose reconstruction work is over, while the last MB-row pairs are still being
+// decoded (68 pairs of a 4K frame over 16 waves leave 12 waves idle for the last ~15 % of
+// the frame).  Units = (band, strip), claimed top-down from an LDS counter.  A band needs
+// luma rows <= L and chroma rows <= C final: MB row m has published luma rows <= 16m + 12
+// and chroma rows <= 8m + 4 once its pair's progress reaches mb_w (rows 13-15 / 5-7 are
+// written by the row below; the last MB row writes all).  One MB row of margin beyond that.
+template <bool kFancy>
+__device__ __forceinline__ void emit_tail(const FrameDesc& F, uint32_t* progress, uint32_t* recon_done, uint32_t* next_unit, int lane,
+                          int* err) {
+  const int W = F.width, H = F.height, uv_h = (H + 1) >> 1, mb_w = F.mb_w, mb_h = F.mb_h;
+  const int sx = strip::strips_x(W);
+  const int npairs = kFancy ? (H >> 1) + 1 : (H + 1) >> 1;
+  const int n_units = sx * ((npairs + strip::kPairs - 1) / strip::kPairs);
+  for (;;) {
+    uint32_t u = 0;
+    if (lane == 0) u = __hip_atomic_fetch_add(next_unit, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    u = __builtin_amdgcn_readfirstlane(u);
+    if (u >= (uint32_t)n_units) return;
+    const int band = (int)u / sx, tx = (int)u - band * sx;
+    const int p1 = min((band + 1) * strip::kPairs, npairs);
+    const int L = min(2 * p1 - 1, H - 1), C = min(p1 - 1, uv_h - 1);
+    const int m = max(max((L + 3) >> 4, (C + 3) >> 3), 0) + 1;  // ceil((L-12)/16), ceil((C-4)/8), + margin
+    bool ok;
+    if (m >= mb_h - 1) ok = wait_at_least(recon_done, kWaves);
+    else ok = wait_at_least(progress + ((m >> 1) & (kWaves - 1)), ((uint32_t)(m >> 1) << 16) | (uint32_t)mb_w);
+    if (!ok) {
+      if (lane == 0) atomicOr(err, 1);
+      return;
+    }
+    strip::convert_strip<kFancy>(F, tx, band, lane);
+  }
+}
+
 }  // namespace
 
 // kGlobalCols: the per-MB-column store (kColBytes per column) lives in LDS when the frame's
@@ -404,6 +450,7 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
   // is a ds_read (lgkmcnt) -- a volatile generic pointer became a flat load whose
   // vmcnt(0) drained the record/coefficient prefetch every MB.
   __shared__ uint32_t progress[kWaves];
+  __shared__ uint32_t recon_done, next_unit;  // K1 tail (emit_tail): waves done, units claimed
   const FrameDesc* F = frames + blockIdx.x;
   if (!F->valid || (F->cols != nullptr) != kGlobalCols) return;
   const int mb_w = F->mb_w, mb_h = F->mb_h;
@@ -438,6 +485,9 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
   else cols = lds + kHdrBytes + 2 * kWaves * kSlotBytes;
   // per MB column c: cols + c*kColBytes: [0..15] ytop Y, [16..23] U, [24..31] V, [32..159] fbot
   if (threadIdx.x < kWaves) progress[threadIdx.x] = 0;
+  if (threadIdx.x == 0) recon_done = next_unit = 0;
+  const bool emit = F->flags & kFrameEmitRgba;
+  if (emit) __builtin_amdgcn_s_setprio(2);  // reconstruction is the critical path; the tail's conversion yields
   for (int t = threadIdx.x; t < 160; t += blockDim.x) tab[t] = kPred4Table[t];
   K1_TIMELINE_START();
   __syncthreads();
@@ -784,6 +834,12 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
     }
   }
   K1_SECT_FLUSH();
+  if (emit) {
+    if (lane == 0) __hip_atomic_fetch_add(&recon_done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __builtin_amdgcn_s_setprio(0);
+    if (F->flags & kFrameNoFancy) emit_tail<false>(*F, progress, &recon_done, &next_unit, lane, err);
+    else emit_tail<true>(*F, progress, &recon_done, &next_unit, lane, err);
+  }
 }
 
 #ifdef WG_K1_SECTION_TIMING

@@ -43,6 +43,11 @@ struct MbRec {
 };
 static_assert(sizeof(MbRec) == 16, "MbRec must be 16 bytes");
 
+// FrameDesc.flags: WG_FLAG_BYPASS_FILTERING (1) and WG_FLAG_NO_FANCY_UPSAMPLING (2) of the
+// decode, plus kFrameEmitRgba: K1 itself converts the frame to RGBA in its tail (no K2).
+constexpr int32_t kFrameNoFancy = 2;
+constexpr int32_t kFrameEmitRgba = 1 << 8;
+
 struct FrameDesc {
   const MbRec* mbs;
   const uint32_t* row_block0;

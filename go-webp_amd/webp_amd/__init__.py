@@ -133,6 +133,8 @@ _SIGS = {
     "wg_batch_create": (_P, [_P, _P, _P, C.c_int, C.c_int32, _P]),
     "wg_batch_destroy": (None, [_P]),
     "wg_batch_run": (C.c_int, [_P, _P]),
+    "wg_batch_set_emit": (C.c_int, [_P, C.c_int]),
+    "wg_batch_run_emit": (C.c_int, [_P, _P]),
     "wg_batch_kernel_ms": (C.c_int, [_P, _P, C.c_int]),
     "wg_batch_kernel_bytes": (C.c_int, [_P, _P, C.c_int]),
     "wg_batch_size": (C.c_int, [_P]),
@@ -347,6 +349,19 @@ class Batch:
         st = lib().wg_batch_run(self._h, stream)
         if st != Status.OK:
             raise WebPError(st, "wg_batch_run")
+
+    def set_emit(self, separate):
+        """separate=False (default for uncropped batches): K1 emits the lossy RGBA in its
+        tail; True: K1 writes the planes and a K2 launch converts them."""
+        st = lib().wg_batch_set_emit(self._h, 1 if separate else 0)
+        if st != Status.OK:
+            raise WebPError(st, "wg_batch_set_emit")
+
+    def run_emit(self, stream=None):
+        """The YUV420->RGBA stage alone (K2) over the planes of the last run."""
+        st = lib().wg_batch_run_emit(self._h, stream)
+        if st != Status.OK:
+            raise WebPError(st, "wg_batch_run_emit")
 
     def kernel_ms(self):
         """(K1, K2, K3, K4) per-launch ms averaged over the runs since the last call."""

@@ -131,18 +131,32 @@ wg_batch* wg_batch_create_ex(wg_ctx* ctx, const uint8_t* const* data, const size
 void wg_batch_destroy(wg_batch* b);
 
 /* Run the device DSP path for the whole batch on `stream` (NULL = ctx stream):
- * lossy frames: K1 reconstruct+deblock wavefront, K2 YUV420->RGBA, K4 ALPH plane -> A;
+ * lossy frames: K1 reconstruct+deblock wavefront (+ YUV420->RGBA in its tail, or K2), K4 ALPH plane -> A;
  * lossless frames (and lossless ALPH streams): K3 inverse transforms + RGBA.  Kernel durations of the last run
  * (HIP events on that stream) are available from wg_batch_kernel_ms(). */
 int wg_batch_run(wg_batch* b, void* stream);
 
+/* Where a batch's lossy RGBA is produced.  Default (no crop window in the batch): by K1
+ * itself, in the tail of each frame's workgroup (waves done with reconstruction convert
+ * finished row bands while the last rows decode) -- no separate K2 launch.  separate = 1:
+ * K1 writes only the planes and K2 converts them (the path cropped batches always take).
+ * Both are bit-identical; replaces nothing in the reference (its EmitFancyRGB runs per row
+ * inside the decode loop, io_dec.c.go:65-115). */
+int wg_batch_set_emit(wg_batch* b, int separate);
+
+/* The YUV420->RGBA stage alone (K2, EmitFancyRGB / EmitSampledRGB) over the batch's
+ * reconstructed planes (after a wg_batch_run): the stage-roofline measurement of the
+ * metric.  Its duration is reported as ms[1] by wg_batch_kernel_ms(). */
+int wg_batch_run_emit(wg_batch* b, void* stream);
+
 /* Per-launch kernel durations averaged over the runs since the last query:
- * ms[0] = VP8 reconstruct+filter (K1), ms[1] = YUV->RGBA (K2), ms[2] = VP8L inverse
+ * ms[0] = VP8 reconstruct+filter (K1, with its RGBA tail by default), ms[1] = YUV->RGBA (K2), ms[2] = VP8L inverse
  * transforms (K3, lossless frames and lossless ALPH streams), ms[3] = ALPH unfilter + A
  * channel (K4); a kernel with no frames in the batch reports 0.  n_ms >= 1. */
 int wg_batch_kernel_ms(const wg_batch* b, float* ms, int n_ms);
 
-/* Algorithmic HBM bytes per launch of K1, K2, K3, K4. */
+/* Algorithmic HBM bytes per launch of K1, K2, K3, K4; K1 with
+ * its RGBA tail: records + coefficients in, RGBA out (the planes are an intermediate). */
 int wg_batch_kernel_bytes(const wg_batch* b, double* bytes, int n_bytes);
 
 int wg_batch_size(const wg_batch* b);

@@ -29,11 +29,13 @@ def _sha(a):
     return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
 
 
+@pytest.mark.parametrize("emit", ["fused", "separate"])
 @pytest.mark.parametrize("flags", [0, webp_amd.FLAG_BYPASS_FILTERING, webp_amd.FLAG_NO_FANCY_UPSAMPLING])
-def test_batch_all_fixtures_vs_golden_and_oracle(ctx, flags):
+def test_batch_all_fixtures_vs_golden_and_oracle(ctx, flags, emit):
     """All opaque lossy fixtures (odd sizes 1x1..481x270, every filter type/sharpness,
     1/4 segments, 1/4/8 partitions) in ONE batch: per-frame YUV and RGBA identical to
-    libwebp's and to the CPU oracle's."""
+    libwebp's and to the CPU oracle's -- with the RGBA emitted by K1's tail (default) and
+    by a separate K2 launch."""
     datas, golds = [], []
     for n in OPAQUE:
         d, g = load_lossy(n)
@@ -41,7 +43,10 @@ def test_batch_all_fixtures_vs_golden_and_oracle(ctx, flags):
         golds.append(g)
     b = ctx.batch(datas, flags)
     assert (b.status == 0).all(), b.status
+    b.set_emit(emit == "separate")
     b.run()
+    ms = b.kernel_ms()
+    assert (ms[1] > 0) == (emit == "separate"), ms
     for i, (name, d, g) in enumerate(zip(OPAQUE, datas, golds)):
         y, u, v = b.yuv(i)
         rgba = b.rgba(i)
@@ -60,16 +65,26 @@ def test_batch_all_fixtures_vs_golden_and_oracle(ctx, flags):
     b.close()
 
 
+@pytest.mark.parametrize("emit", ["fused", "separate", "stage"])
 @pytest.mark.parametrize("prefix", ["c1_512", "c2_1080p", "c3_4k"])
-def test_bench_frames_sha256(ctx, prefix):
+def test_bench_frames_sha256(ctx, prefix, emit):
     """Full-size bench configs (C1 512^2, C2 1080p, C3 4K deblocked): every frame's
-    Y/U/V and RGBA SHA-256 equals libwebp's."""
+    Y/U/V and RGBA SHA-256 equals libwebp's, whichever kernel emits the RGBA (K1's tail,
+    K2 in the batch run, or the stage entry wg_batch_run_emit after a planes-only run)."""
     m = manifest()["bench"]
     paths = bench_files(prefix)
     datas = [open(p, "rb").read() for p in paths]
     b = ctx.batch(datas)
     assert (b.status == 0).all()
-    b.run()
+    if emit == "stage":
+        b.set_emit(True)
+        b.run()  # planes + RGBA
+        b.set_emit(False)
+        b.run()  # the tail rewrites the RGBA
+        b.run_emit()  # and the stage alone once more
+    else:
+        b.set_emit(emit == "separate")
+        b.run()
     for i, p in enumerate(paths):
         ent = m[p.rsplit("/", 1)[1]]["sha256"]
         y, u, v = b.yuv(i)
