@@ -444,7 +444,7 @@ __device__ __forceinline__ void emit_tail(const FrameDesc& F, uint32_t* progress
 // of one CU the same way (its L1 is shared by the workgroup), no extra s_waitcnt needed.
 template <bool kGlobalCols>
 __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc* __restrict__ frames, int* err,
-                                                                int lead_arg) {
+                                                                int lead_arg, int recon_waves_arg) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   // Progress counters as a typed __shared__ array + relaxed workgroup atomics, so the spin
   // is a ds_read (lgkmcnt) -- a volatile generic pointer became a flat load whose
@@ -488,11 +488,19 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
   if (threadIdx.x == 0) recon_done = next_unit = 0;
   const bool emit = F->flags & kFrameEmitRgba;
   if (emit) __builtin_amdgcn_s_setprio(2);  // reconstruction is the critical path; the tail's conversion yields
+  // Waves that reconstruct (pairs k = wave, wave + R, ...); with the RGBA tail the others
+  // convert bands from the start.  Measured: tall frames (4K, 68 pairs) run
+  // fastest with R = 12 -- three reconstructing waves and one converting wave per SIMD
+  // (10.04 vs 10.63 ms at R = 16); 1080p (34 pairs) with R = 16 (2.72 vs 2.98 ms); SIMD-
+  // unbalanced R (13-15) and R <= 11 are slower.  R <= 16 keeps the progress ring safe:
+  // pair k + 16 only starts on a wave that has completed a pair > k, so pair k is complete.
+  const int R = !emit ? kWaves
+                      : recon_waves_arg > 0 ? min(recon_waves_arg, kWaves) : ((mb_h + 1) >> 1) > 48 ? 12 : kWaves;
   for (int t = threadIdx.x; t < 160; t += blockDim.x) tab[t] = kPred4Table[t];
   K1_TIMELINE_START();
   __syncthreads();
 
-  for (int k = wave; 2 * k < mb_h; k += kWaves) {
+  for (int k = wave; wave < R && 2 * k < mb_h; k += R) {
     const int y = 2 * k + h;
     const bool row_ok = y < mb_h;
     const bool has_odd = 2 * k + 1 < mb_h;
@@ -875,6 +883,12 @@ hipError_t launch_vp8_recon_filter(const FrameDesc* d_frames, int n_frames, int 
     const char* e = getenv("WG_K1_LEAD");
     return e ? atoi(e) : 0;
   }();
+  // WG_K1_RECON_WAVES: waves per frame that reconstruct when K1 emits RGBA (the rest convert
+  // finished bands from the start); 0 / unset = by frame height (see the kernel).
+  static const int recon_waves = [] {
+    const char* e = getenv("WG_K1_RECON_WAVES");
+    return e ? atoi(e) : 0;
+  }();
   if (lds_frames) {
     const size_t lds = vp8_recon_lds_bytes(max_mb_w);
     static size_t configured = 0;
@@ -885,7 +899,7 @@ hipError_t launch_vp8_recon_filter(const FrameDesc* d_frames, int n_frames, int 
       configured = lds;
     }
     hipLaunchKernelGGL(vp8_recon_filter_kernel<false>, dim3(n_frames), dim3(1024), lds, stream, d_frames, d_err,
-                       lead);
+                       lead, recon_waves);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
@@ -899,7 +913,7 @@ hipError_t launch_vp8_recon_filter(const FrameDesc* d_frames, int n_frames, int 
       configured = true;
     }
     hipLaunchKernelGGL(vp8_recon_filter_kernel<true>, dim3(n_frames), dim3(1024), lds, stream, d_frames, d_err,
-                       lead);
+                       lead, recon_waves);
     return hipGetLastError();
   }
   return hipSuccess;
