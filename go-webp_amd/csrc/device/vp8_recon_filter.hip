@@ -468,7 +468,7 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
   const __amdgpu_buffer_rsrc_t planes =
       __builtin_amdgcn_make_buffer_rsrc(F->y, 0, (int)(voff + (uint32_t)(8 * mb_h * uvs)), 0x00020000);
 
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // SGPR: k and the pair loop stay uniform
   const int lane = threadIdx.x & 63;
   K1_SECT_DECL();
   // Required lead of the previous row pair, in MB columns: 2 (top-right samples and the
@@ -500,6 +500,7 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
   K1_TIMELINE_START();
   __syncthreads();
 
+  bool aborted = false;  // a progress wait timed out (error flagged): stop waiting
   for (int k = wave; wave < R && 2 * k < mb_h; k += R) {
     const int y = 2 * k + h;
     const bool row_ok = y < mb_h;
@@ -548,16 +549,27 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
 
       K1_SECT(0);
       // ---- wait for the previous pair's odd row (t = x + 2y wavefront)
+      //      The counter is read into an SGPR (readfirstlane) so the spin is a scalar branch,
+      //      and the timeout does not leave the loop: any path reaching the loop latch without
+      //      this iteration's plane stores makes the waitcnt pass extend the latch's prefetch
+      //      wait over those stores (a vmcnt that waits for store acks every MB).
       if (k > 0 && i < mb_w) {
         const uint32_t need = ((uint32_t)(k - 1) << 16) | (uint32_t)min(i + lead, mb_w);
         uint32_t* pr = progress + ((k - 1) & (kWaves - 1));
-        if (__hip_atomic_load(pr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
+        auto cur = [&] {
+          return __builtin_amdgcn_readfirstlane(__hip_atomic_load(pr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+        };
+        if (!aborted && cur() < need) {
           const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-          while (__hip_atomic_load(pr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
+          for (;;) {
             __builtin_amdgcn_s_sleep(2);
+            if (cur() >= need) break;
             if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s: give up, flag
+              // no exit from the loop here (an exit path skipping the stores would reach the
+              // latch too): the wave runs on without waiting and the batch reports the error
               if (lane == 0) atomicOr(err, 1);
-              return;
+              aborted = true;
+              break;
             }
           }
         }
