@@ -169,19 +169,27 @@ __device__ __forceinline__ uint32_t shr1(uint32_t old, uint32_t v) {  // lane i 
   return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x138, 0xF, 0xF, false);
 }
 
-// Bounded spin on a progress counter: gives up after 2 s (s_memrealtime is 100 MHz),
-// flags the batch error word and makes the caller return.
-__device__ __forceinline__ bool wait_progress(uint32_t* pr, uint32_t need, int* err) {
-  if (__hip_atomic_load(pr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= need) return true;
+// Bounded spin on a progress counter (need is wave-uniform): the counter is read into an
+// SGPR so the spin is a scalar branch.  After 2 s (s_memrealtime is 100 MHz) it flags the
+// batch error word and sets `aborted`, which turns every later wait of the wave into a
+// no-op: the wave runs to its end instead of leaving its loops early -- an exit path that
+// skips a group's stores would make the waitcnt pass extend the loop's load waits over
+// those stores.
+__device__ __forceinline__ void wait_progress(uint32_t* pr, uint32_t need, int* err, bool& aborted) {
+  auto cur = [&] {
+    return __builtin_amdgcn_readfirstlane(__hip_atomic_load(pr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+  };
+  if (aborted || cur() >= need) return;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  while (__hip_atomic_load(pr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
+  for (;;) {
     __builtin_amdgcn_s_sleep(1);
+    if (cur() >= need) return;
     if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {
-      __hip_atomic_fetch_or(as_global(err), 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return false;
+      if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_or(as_global(err), 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      aborted = true;
+      return;
     }
   }
-  return true;
 }
 
 // Per-pass context, all wave-uniform.  Per-pixel ops: up to two (cross-color, add-green;
@@ -249,7 +257,8 @@ __device__ __forceinline__ bool pred_wavefront(const Pass& P, int W, int H, int 
                                __amdgpu_buffer_rsrc_t out_rs, int dst_stride, uint32_t* ring, const uint8_t* mode_tab,
                                const uint32_t* cc_tab, uint8_t* slots, uint32_t* prog, int* err) {
   constexpr bool kCC = !GENERIC && (ops_cc(PRE) || ops_cc(POST));
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;  // wave in an SGPR
+  bool aborted = false;
   const int nbands = (H + kBand - 1) / kBand;
   const int steps = W + 2 * (kBand - 1);
   const int ngroups = (steps + kGroup - 1) / kGroup;
@@ -271,9 +280,9 @@ __device__ __forceinline__ bool pred_wavefront(const Pass& P, int W, int H, int 
     uint32_t* ring_mine = ring + (b & (kWaves - 1)) * kRing;
     // ring slot b&15 was last written by band b-16 and read by band b-15: that reader
     // must be done before this band overwrites it
-    if (b >= kWaves && !wait_progress(prog + ((b - kWaves + 1) & (kWaves - 1)),
-                                      ((uint32_t)(b - kWaves + 1) << 16) | (uint32_t)steps, err))
-      return false;
+    if (b >= kWaves)
+      wait_progress(prog + ((b - kWaves + 1) & (kWaves - 1)), ((uint32_t)(b - kWaves + 1) << 16) | (uint32_t)steps, err,
+                    aborted);
     K3_SECT(6);
     const int mrow = (yc >> P.m_bits) * P.m_tpr;
     const int crow = (yc >> P.cc_bits) * P.cc_tpr;
@@ -352,7 +361,7 @@ __device__ __forceinline__ bool pred_wavefront(const Pass& P, int W, int H, int 
 
     uint32_t o_prev = 0, t1 = 0, t2 = 0, first = 0;  // L; TR of the last two steps (= T, TL)
     // one chunk (cl = 0/1 within its group): inputs from the slot, outputs back to it
-    auto chunk = [&](const int c, const int cl) -> bool {
+    auto chunk = [&](const int c, const int cl) {
       const bool interior = c >= c_lo && c <= c_hi;
       const uint32x4_t in0 = *reinterpret_cast<const uint32x4_t*>(my_lds + 32 * cl);
       const uint32x4_t in1 = *reinterpret_cast<const uint32x4_t*>(my_lds + 32 * cl + 16);
@@ -365,14 +374,12 @@ __device__ __forceinline__ bool pred_wavefront(const Pass& P, int W, int H, int 
       // chunk overwrites
       if (b > 0) {
         const uint32_t need = ((uint32_t)(b - 1) << 16) | (uint32_t)min(c * kChunk + kChunk + 127, steps);
-        if (!wait_progress(prog + ((b - 1) & (kWaves - 1)), need, err)) return false;
+        wait_progress(prog + ((b - 1) & (kWaves - 1)), need, err, aborted);
       }
       K3_SECT(1);
       if (b + 1 < nbands) {
         const int lag = c * kChunk + kChunk - 2 * (kBand - 1) - kRing + 16;  // oldest column still needed
-        if (lag > 0 &&
-            !wait_progress(prog + ((b + 1) & (kWaves - 1)), ((uint32_t)(b + 1) << 16) | (uint32_t)lag, err))
-          return false;
+        if (lag > 0) wait_progress(prog + ((b + 1) & (kWaves - 1)), ((uint32_t)(b + 1) << 16) | (uint32_t)lag, err, aborted);
       }
       K3_SECT(2);
       fix_modes(c, md);
@@ -434,14 +441,13 @@ __device__ __forceinline__ bool pred_wavefront(const Pass& P, int W, int H, int 
         __hip_atomic_store(prog + (b & (kWaves - 1)), ((uint32_t)b << 16) | (uint32_t)min(c * kChunk + kChunk, steps),
                            __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       K3_SECT(5);
-      return true;
     };
     load_group(0);
     stage_group();
     load_group(1);
     for (int g = 0; g < ngroups; ++g) {
-      if (!chunk(2 * g, 0)) return false;
-      if (!chunk(2 * g + 1, 1)) return false;
+      chunk(2 * g, 0);
+      chunk(2 * g + 1, 1);
       emit_group(g);
       K3_SECT(7);
       stage_group();     // group g+1's inputs (in flight since group g started)
@@ -451,7 +457,7 @@ __device__ __forceinline__ bool pred_wavefront(const Pass& P, int W, int H, int 
     }
   }
   K3_SECT_FLUSH();
-  return true;
+  return !aborted;
 }
 
 // VARIANT (chosen per frame on the host, vp8l_variant()): 1..4 = the predictor pass with
