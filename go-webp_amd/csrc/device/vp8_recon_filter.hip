@@ -649,6 +649,23 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
         *reinterpret_cast<uint2*>(res + (b0 + 8) * 16 + q * 4) =
             make_uint2((ry1[0] & 0xffff) | (ry1[1] << 16), (ry1[2] & 0xffff) | (ry1[3] << 16));
       }
+      // ---- chroma prediction + residual (lane = one pixel row of one 4x4 chroma block); independent
+      //      of the luma blocks, so it shares their section (one LDS hand-off less per MB)
+      if (act) {
+        const uint32_t oh = 1u << check_mode(x, y, (fl >> kUVModeShift) & 3);
+        const uint8_t* base = ws + coff;
+        const uint8_t* cleft = left + 16 + 8 * cpl;
+        const int row = 4 * cby + q;
+        uint32_t st = 0, sl = 0;
+        if (__any(oh & 0x31)) {
+          st = __builtin_amdgcn_sad_u8(ld32(base - BPS), 0, 0);
+          st = __builtin_amdgcn_sad_u8(ld32(base - BPS + 4), 0, st);
+          sl = __builtin_amdgcn_sad_u8(ld32(cleft), 0, 0);
+          sl = __builtin_amdgcn_sad_u8(ld32(cleft + 4), 0, sl);
+        }
+        const uint32_t pred = pred_row(oh, ld32(base - BPS + 4 * cbx), cleft[row], base[-BPS - 1], dc_value(oh, st, sl, 3));
+        st32(ws + coff + row * BPS + 4 * cbx, add_res(pred, rcr));
+      }
       lds_sync();
       K1_SECT(5);
       if (__any(act && i4)) {
@@ -693,24 +710,6 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
       }
 
       K1_SECT(6);
-      // ---- chroma prediction + residual (lane = one pixel row of one 4x4 chroma block)
-      if (act) {
-        const uint32_t oh = 1u << check_mode(x, y, (fl >> kUVModeShift) & 3);
-        const uint8_t* base = ws + coff;
-        const uint8_t* cleft = left + 16 + 8 * cpl;
-        const int row = 4 * cby + q;
-        uint32_t st = 0, sl = 0;
-        if (__any(oh & 0x31)) {
-          st = __builtin_amdgcn_sad_u8(ld32(base - BPS), 0, 0);
-          st = __builtin_amdgcn_sad_u8(ld32(base - BPS + 4), 0, st);
-          sl = __builtin_amdgcn_sad_u8(ld32(cleft), 0, 0);
-          sl = __builtin_amdgcn_sad_u8(ld32(cleft + 4), 0, sl);
-        }
-        const uint32_t pred = pred_row(oh, ld32(base - BPS + 4 * cbx), cleft[row], base[-BPS - 1], dc_value(oh, st, sl, 3));
-        st32(ws + coff + row * BPS + 4 * cbx, add_res(pred, rcr));
-      }
-      lds_sync();
-
       K1_SECT(7);
       if (act) {
         // ---- stash unfiltered bottom samples for the row below (frame_dec.c.go:175-179)

@@ -12,6 +12,8 @@ for v in "$@"; do
   rc=$?; if [ $rc -ne 0 ]; then echo "STOP: bench $v rc=$rc"; tail -5 gpurun_out/abq/$v.$round.err; exit $rc; fi
   python3 -c "
 import json,sys; j=json.load(open('gpurun_out/abq/$v.$round.json'))
-print('%-10s r$round' % '$v', ' '.join('%s %.3f' % (k[:12], x) for k, x in j['kernel_ms'].items()), ' value', j['value'])"
+st = j.get('roofline_yuv_to_rgba', {}).get('avg_launch_ms')
+print('%-10s r$round' % '$v', ' '.join('%s %.3f' % (k[:12], x) for k, x in j['kernel_ms'].items()),
+      ' stage %.3f' % st if st else '', ' value', j['value'])"
 done
 done
