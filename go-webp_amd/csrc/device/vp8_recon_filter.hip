@@ -321,12 +321,12 @@ __device__ __forceinline__ void filter_mb(uint8_t* fw, int l, bool on, bool fx, 
   uint8_t* win = fw + (luma ? kFwY : ((l >> 3) & 1 ? kFwV : kFwU));
   int v[20];
   if (lane_on) {  // vertical edges on window row li+4
-    uint32_t* row = reinterpret_cast<uint32_t*>(win + (li + 4) * st);
-    uint32_t w[5];
+    // byte loads/stores like the column pass: the LDS unit zero-extends and narrows, so
+    // the (VALU-bound) wave spends no instructions unpacking and repacking the row
+    // (volatile: kept as single-byte accesses, not merged back into dwords + shifts)
+    volatile __attribute__((address_space(3))) uint8_t* row = (__attribute__((address_space(3))) uint8_t*)(win + (li + 4) * st);
 #pragma unroll
-    for (int k = 0; k < 5; ++k) w[k] = (k < 3 || luma) ? row[k] : 0u;
-#pragma unroll
-    for (int k = 0; k < 20; ++k) v[k] = byte_of(w[k >> 2], k & 3);
+    for (int k = 0; k < 20; ++k) v[k] = (k < 12 || luma) ? row[k] : 0;
     if (fx) filter_at<KMB>(v + 0, t_mb, ilevel, hev_t);  // HFilter16 / HFilter8 / SimpleHFilter16
     if (fin) {
       filter_at<KIN>(v + 4, t_in, ilevel, hev_t);  // HFilter16i / HFilter8i
@@ -336,8 +336,8 @@ __device__ __forceinline__ void filter_mb(uint8_t* fw, int l, bool on, bool fx, 
       }
     }
 #pragma unroll
-    for (int k = 0; k < 5; ++k)
-      if (k < 3 || luma) row[k] = pack4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
+    for (int k = 1; k < 19; ++k)
+      if (k < 11 || luma) row[k] = (uint8_t)v[k];
   }
   lds_sync();
   if (lane_on) {  // horizontal edges on window column li+4
