@@ -118,9 +118,6 @@ __device__ __forceinline__ void lds_sync() {
 }
 
 __device__ __forceinline__ int clamp255(int v) { return min(max(v, 0), 255); }
-__device__ __forceinline__ uint32_t pack4(int a, int b, int c, int d) {
-  return (uint32_t)a | ((uint32_t)b << 8) | ((uint32_t)c << 16) | ((uint32_t)d << 24);
-}
 __device__ __forceinline__ int byte_of(uint32_t w, int i) { return (w >> (8 * i)) & 0xff; }
 __device__ __forceinline__ uint32_t ld32(const uint8_t* p) { return *reinterpret_cast<const uint32_t*>(p); }
 __device__ __forceinline__ void st32(uint8_t* p, uint32_t v) { *reinterpret_cast<uint32_t*>(p) = v; }
@@ -190,9 +187,21 @@ __device__ __forceinline__ void idct_pass(int q, uint2 cv, int r[4]) {
   }
 }
 
+// clamp(a..d, 0, 255) packed little-endian into one dword with gfx950's v_ashr_pk_u8_i32
+// (D[15:0] = sat_u8(S1 >> S2) << 8 | sat_u8(S0 >> S2), D[31:16] kept; measured by
+// scripts/probes/ashr_pk.hip): the high pair first, shifted up, then the low pair written
+// under it -- three instructions instead of four v_med3 and three v_lshl_or.
+__device__ __forceinline__ uint32_t pack_sat4(int a, int b, int c, int d) {
+  uint32_t hi, out;
+  asm("v_ashr_pk_u8_i32 %0, %1, %2, 0" : "=v"(hi) : "v"(c), "v"(d));
+  out = hi << 16;
+  asm("v_ashr_pk_u8_i32 %0, %1, %2, 0" : "+v"(out) : "v"(a), "v"(b));
+  return out;
+}
+
 __device__ __forceinline__ uint32_t add_res(uint32_t pred, const int r[4]) {
-  return pack4(clamp255(byte_of(pred, 0) + r[0]), clamp255(byte_of(pred, 1) + r[1]),
-               clamp255(byte_of(pred, 2) + r[2]), clamp255(byte_of(pred, 3) + r[3]));
+  return pack_sat4(byte_of(pred, 0) + r[0], byte_of(pred, 1) + r[1], byte_of(pred, 2) + r[2],
+                   byte_of(pred, 3) + r[3]);
 }
 
 __device__ __forceinline__ int check_mode(int mb_x, int mb_y, int mode) {  // frame_dec.c.go:28-37
@@ -210,8 +219,8 @@ __device__ __forceinline__ int check_mode(int mb_x, int mb_y, int mode) {  // fr
 __device__ __forceinline__ uint32_t pred_row(uint32_t oh, uint32_t top, int left, int tl, int dc) {
   uint32_t tm = 0;
   if (__any(oh & 0x2))
-    tm = pack4(clamp255(byte_of(top, 0) + left - tl), clamp255(byte_of(top, 1) + left - tl),
-               clamp255(byte_of(top, 2) + left - tl), clamp255(byte_of(top, 3) + left - tl));
+    tm = pack_sat4(byte_of(top, 0) + left - tl, byte_of(top, 1) + left - tl, byte_of(top, 2) + left - tl,
+                   byte_of(top, 3) + left - tl);
   const uint32_t v = (oh & 0x4) ? top : (uint32_t)dc * 0x01010101u;  // VE : DC variants
   const uint32_t w = (oh & 0x8) ? (uint32_t)left * 0x01010101u : tm;  // HE : TM
   return (oh & 0xA) ? w : v;
