@@ -526,6 +526,30 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
     // conservatively drain the NEXT MB's prefetch with a vmcnt(0).
     __builtin_amdgcn_s_waitcnt(0x0F70);
     uint32_t top_carry = 0;  // see "top samples"
+    // Plane offsets of the five HBM store slots (see "final pixels to HBM") at MB column 0,
+    // once per pair: per MB only `x << shift` is added.  A slot that never stores for this
+    // row/lane starts at kDrop, and kDrop + 16x stays beyond the planes (dropped store).
+    uint32_t sbA0, sbA1, sbB, sbC, sbE, shB, shC;
+    {
+      const int l0 = lane & 31, q0 = l0 & 3, b00 = l0 >> 2;
+      sbA0 = b00 < nrows_y ? (uint32_t)__mul24(16 * y + b00, ys) - 4u + 4u * q0 : kDrop;
+      sbA1 = b00 + 8 < nrows_y ? (uint32_t)__mul24(16 * y + b00 + 8, ys) - 4u + 4u * q0 : kDrop;
+      const int bk = l0 - 12, bp = bk >= 6, brem = bk - 6 * bp;
+      const int brr = l0 < 12 ? (l0 >> 2) - 3 : (brem >> 1) - 3;
+      const int bd = l0 < 12 ? (l0 & 3) : (brem & 1);
+      sbB = !(y > 0 && l0 < 24) ? kDrop
+            : l0 < 12 ? (uint32_t)__mul24(16 * y + brr, ys) + 4u * bd
+                      : (bp ? voff : uoff) + (uint32_t)__mul24(8 * y + brr, uvs) + 4u * bd;
+      shB = l0 < 12 ? 4 : 3;
+      const bool cl = l0 >= 16;
+      const uint32_t cpoff = ((l0 >> 3) & 1) ? voff : uoff;
+      sbC = cl ? ((l0 & 7) < nrows_c ? cpoff + (uint32_t)__mul24(8 * y + (l0 & 7), uvs) + 4u : kDrop)
+               : (l0 < nrows_y ? (uint32_t)__mul24(16 * y + l0, ys) + 12u : kDrop);
+      shC = cl ? 3 : 4;
+      const int ep = l0 >> 4, er = (l0 >> 1) & 7, ed = l0 & 1;
+      sbE = er < nrows_c ? (ep ? voff : uoff) + (uint32_t)__mul24(8 * y + er, uvs) - 4u + 4u * ed : kDrop;
+    }
+
     K1_SECT_START();
 
     for (int i = 0; i < mb_w + 2; ++i) {
@@ -793,10 +817,8 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
       {
         const bool cl = l >= 16;  // chroma lane (slots C, E by plane)
         const int pl = (l >> 3) & 1;
-        const uint32_t cpoff = pl ? voff : uoff;                    // slot C chroma plane
         const uint8_t* cwin = fw + (pl ? kFwV : kFwU);
         const int ep = l >> 4, er = (l >> 1) & 7, ed = l & 1;      // slot E
-        const uint32_t epoff = ep ? voff : uoff;
         const uint8_t* ewin = fw + (ep ? kFwV : kFwU);
         // slot B: lanes 0..11 luma rows -3..-1 of the MB above (cols 0..15),
         //         lanes 12..23 chroma rows -3..-1 (cols 0..7), U then V
@@ -810,19 +832,13 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
         const uint32_t vB = ld32(bsrc);
         const uint32_t vC = cl ? ld32(cwin + ((l & 7) + 4) * FWC + 8) : ld32(fw + kFwY + (l + 4) * FWY + 16);
         const uint32_t vE = ld32(ewin + (er + 4) * FWC + 4 * ed);
+        const uint32_t ux = (uint32_t)x;
         const bool aok = act && (q > 0 || x > 0);
-        const uint32_t oA = (uint32_t)(16 * x - 4 + 4 * q);
-        const uint32_t oA0 = aok && b0 < nrows_y ? (uint32_t)__mul24(16 * y + b0, ys) + oA : kDrop;
-        const uint32_t oA1 = aok && b0 + 8 < nrows_y ? (uint32_t)__mul24(16 * y + b0 + 8, ys) + oA : kDrop;
-        const uint32_t oB = !(act && y > 0 && l < 24) ? kDrop
-                            : l < 12 ? (uint32_t)__mul24(16 * y + brr, ys) + 16 * x + 4 * bd
-                                     : (bp ? voff : uoff) + (uint32_t)__mul24(8 * y + brr, uvs) + 8 * x + 4 * bd;
-        const uint32_t oC = !(act && last_x) ? kDrop
-                            : cl ? ((l & 7) < nrows_c ? cpoff + (uint32_t)__mul24(8 * y + (l & 7), uvs) + 8 * x + 4 : kDrop)
-                                 : (l < nrows_y ? (uint32_t)__mul24(16 * y + l, ys) + 16 * x + 12 : kDrop);
-        const uint32_t oE = act && er < nrows_c && (ed > 0 || x > 0)
-                                ? epoff + (uint32_t)__mul24(8 * y + er, uvs) + 8 * x - 4 + 4 * ed
-                                : kDrop;
+        const uint32_t oA0 = aok ? sbA0 + (ux << 4) : kDrop;
+        const uint32_t oA1 = aok ? sbA1 + (ux << 4) : kDrop;
+        const uint32_t oB = act ? sbB + (ux << shB) : kDrop;
+        const uint32_t oC = act && last_x ? sbC + (ux << shC) : kDrop;
+        const uint32_t oE = act && (ed > 0 || x > 0) ? sbE + (ux << 3) : kDrop;
         __builtin_amdgcn_raw_buffer_store_b32(vA0, planes, (int)oA0, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b32(vA1, planes, (int)oA1, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b32(vB, planes, (int)oB, 0, 0);

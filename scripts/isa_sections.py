@@ -43,11 +43,15 @@ def main():
         asm = glob.glob(os.path.join(t, "*gfx950*.s"))[0]
         cur, cnt = "pre", collections.OrderedDict()
         meta = {}
+        dump = os.environ.get("DUMP_SECTION")  # write that section's ISA to /tmp/isa_<name>.s
+        out = open(f"/tmp/isa_{dump}.s", "w") if dump else None
         for line in open(asm):
             m = re.search(r";MARK (\w+)", line)
             if m:
                 cur = m.group(1)
                 continue
+            if out and cur == dump:
+                out.write(line)
             m = re.match(r"\s+\.(vgpr_count|sgpr_count|private_segment_fixed_size):\s+(\d+)", line)
             if m:
                 meta[m.group(1)] = m.group(2)
