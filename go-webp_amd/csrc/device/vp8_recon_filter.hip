@@ -879,6 +879,10 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
   }
   K1_SECT_FLUSH();
   if (emit) {
+    // Own plane stores complete before announcing the wave done: converters may read the
+    // bottom rows right after the last wave's increment, with no row of margin left.
+    // (Workgroup-scope release alone emits no vmcnt wait; this costs one wait per wave.)
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     if (lane == 0) __hip_atomic_fetch_add(&recon_done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     __builtin_amdgcn_s_setprio(0);
     if (F->flags & kFrameNoFancy) emit_tail<false>(*F, progress, &recon_done, &next_unit, lane, err);

@@ -54,3 +54,27 @@ def test_unsupported_and_invalid_options(ctx):
                        (webp_amd.options(1, crop=(0, 0, 0, 5)), webp_amd.Status.INVALID_PARAM)):
         _, status = ctx.decode_batch_opts([data], opts)
         assert status[0] == want
+
+
+def test_cropped_batch_keeps_separate_emit(ctx):
+    """A batch with a crop window converts through K2 (the window is upsampled as a standalone
+    image): wg_batch_set_emit refuses to switch it to K1's tail; separate stays accepted."""
+    import ctypes as C
+    from oracle_lib import load_lossy
+    d, _ = load_lossy("synth_481x270")
+    bufs, ptrs, sizes = webp_amd._ptr_arrays([d])
+    st = np.zeros(1, np.int32)
+    opt = webp_amd.options(crop=(10, 12, 64, 40))
+    L = webp_amd.lib()
+    h = L.wg_batch_create_ex(ctx._h, ptrs, sizes, 1, C.byref(opt), st.ctypes.data)
+    assert h and st[0] == 0, st
+    try:
+        assert L.wg_batch_set_emit(h, 0) == webp_amd.Status.INVALID_PARAM
+        assert L.wg_batch_set_emit(h, 1) == webp_amd.Status.OK
+        assert L.wg_batch_run(h, None) == webp_amd.Status.OK
+        ms = (C.c_float * 4)()
+        assert L.wg_batch_kernel_ms(h, ms, 4) == webp_amd.Status.OK
+        assert ms[0] > 0 and ms[1] > 0, list(ms)  # K1 planes + K2 on the crop window
+    finally:
+        L.wg_batch_destroy(h)
+    assert L.wg_batch_set_emit(None, 0) == webp_amd.Status.INVALID_PARAM
