@@ -225,6 +225,9 @@ def main():
         ran = [k for k in range(len(KERNELS)) if kms[k] > 0]
         roofs = {KERNELS[k]: roof(kby[k], kms[k], KERNELS[k]) for k in ran}
         dominant = roofs[KERNELS[max(ran, key=lambda k: kms[k])]]
+        if dominant["kernel"] == "vp8_recon_filter_kernel":
+            # measured limiter: VALU issue on the frame's CU, not HBM
+            dominant["limiter"] = "VALU issue per CU (each added VALU op per MB step costs ~2.5 SIMD cycles)"
         if stage_ms > 0:
             roofs["yuv_to_rgba_kernel"] = dict(roof(kby[1], stage_ms, "yuv_to_rgba_kernel"),
                                                note="stage timed alone over the same planes; in the "
@@ -243,6 +246,7 @@ def main():
             "dtype": "u8",
             "data": "synthetic (SURVEY App. B frames encoded by libwebp 1.6.0, committed bitstreams)",
             "config": {"workload": wl["name"], "description": wl["desc"], "frames_per_gpu": args.batch,
+                       "frames_total": args.batch * world,
                        "distinct_bitstreams": len(datas), "input_bpp": round(bpp, 3),
                        "parallelism": f"frame-sharded over {world} GPU(s), no collectives",
                        "inputs": "resident in HBM (host entropy stage + H2D outside the timed region)"},
