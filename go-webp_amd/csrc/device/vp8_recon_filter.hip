@@ -746,10 +746,10 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
       K1_SECT(7);
       if (act) {
         // ---- stash unfiltered bottom samples for the row below (frame_dec.c.go:175-179)
-        if (!last_row) {
-          if (l < 4) st32(col + 4 * l, ld32(ws + Y_OFF + 15 * BPS + 4 * l));
-          else if (l < 6) st32(col + 16 + 4 * (l - 4), ld32(ws + U_OFF + 7 * BPS + 4 * (l - 4)));
-          else if (l < 8) st32(col + 24 + 4 * (l - 6), ld32(ws + V_OFF + 7 * BPS + 4 * (l - 6)));
+        //      (lanes 0..3 luma, 4..5 U, 6..7 V: the column store's dword l either way)
+        if (!last_row && l < 8) {
+          const int so = l < 4 ? Y_OFF + 15 * BPS + 4 * l : (l < 6 ? U_OFF - 16 : V_OFF - 24) + 7 * BPS + 4 * l;
+          st32(col + 4 * l, ld32(ws + so));
         }
         // ---- filter window: MB body from the workspace, rows above from fbot
         st32(fw + kFwY + (b0 + 4) * FWY + 4 + 4 * q, ld32(ws + Y_OFF + b0 * BPS + 4 * q));
