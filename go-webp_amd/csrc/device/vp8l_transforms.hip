@@ -291,22 +291,32 @@ __device__ __forceinline__ bool pred_wavefront(const Pass& P, int W, int H, int 
     // frame get kDrop.  Columns left of the frame read the previous row (ignored) or, in
     // row 0, wrap to an out-of-range offset (reads 0).
     const int rows_left = H - b * kBand;
-    const uint32_t in_q = 16u * (uint32_t)w_in * 4u - 128u, out_q = 16u * (uint32_t)dst_stride - 128u;
-    const uint32_t in_base = (uint32_t)((b * kBand + io_r) * w_in * 4) + 16u * io_p - 8u * io_r;
+    const uint32_t out_q = 16u * (uint32_t)dst_stride - 128u;
     const uint32_t out_base = (uint32_t)((b * kBand + io_r) * dst_stride) + 16u * io_p - 8u * io_r;
     const int x_io = 4 * io_p - 2 * io_r;  // column of the quad (group 0, q = 0)
 
-    uint32x4_t R[4];  // the next group's inputs, in flight
-    auto load_group = [&](int g) {
+    // Inputs are loaded two groups at a time: 128 contiguous bytes per row (groups 2p and
+    // 2p+1), 8 lanes per row, rows io_r2 + 8q (q = 0..7), so each row's line is requested
+    // once per pair instead of once per group (the 64-byte-per-group loads re-fetched lines
+    // the L2 had evicted in between).  Quads 0..3 of a row are group 2p, 4..7 group 2p+1;
+    // a group's staging has the other half's lanes write into the slot's row padding.
+    const int io_r2 = lane >> 3, io_p2 = lane & 7;
+    const uint32_t in_q2 = 8u * (uint32_t)w_in * 4u - 64u;  // +8 rows, -16 columns of skew
+    const uint32_t in_base2 = (uint32_t)((b * kBand + io_r2) * w_in * 4) + 16u * io_p2 - 8u * io_r2;
+    uint8_t* const io_lds2 = slot + io_r2 * kSlotStride + 16 * (io_p2 & 3);
+    uint8_t* const io_pad2 = slot + io_r2 * kSlotStride + 4 * kGroup;  // row padding (never read)
+    uint32x4_t R[8];  // the current pair of groups' inputs
+    auto load_pair = [&](int p) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const uint32_t off = io_r + 16 * q < rows_left ? in_base + q * in_q + 64u * g : kDrop;
+      for (int q = 0; q < 8; ++q) {
+        const uint32_t off = io_r2 + 8 * q < rows_left ? in_base2 + q * in_q2 + 128u * p : kDrop;
         R[q] = __builtin_amdgcn_raw_buffer_load_b128(in_rs, off, 0, 0);
       }
     };
-    auto stage_group = [&]() {
+    auto stage_half = [&](bool upper) {
+      uint8_t* const dst = (io_p2 >= 4) == upper ? io_lds2 : io_pad2;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) *reinterpret_cast<uint32x4_t*>(io_lds + 16 * q * kSlotStride) = R[q];
+      for (int q = 0; q < 8; ++q) *reinterpret_cast<uint32x4_t*>(dst + 8 * q * kSlotStride) = R[q];
     };
     auto emit_group = [&](int g) {
       uint32x4_t S[4];
@@ -442,17 +452,21 @@ __device__ __forceinline__ bool pred_wavefront(const Pass& P, int W, int H, int 
                            __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       K3_SECT(5);
     };
-    load_group(0);
-    stage_group();
-    load_group(1);
+    load_pair(0);
+    stage_half(false);
     for (int g = 0; g < ngroups; ++g) {
       chunk(2 * g, 0);
       chunk(2 * g + 1, 1);
       emit_group(g);
       K3_SECT(7);
-      stage_group();     // group g+1's inputs (in flight since group g started)
-      K3_SECT(8);
-      load_group(g + 2);  // past the end: all out of range, reads 0
+      if ((g & 1) == 0) {
+        stage_half(true);     // group g+1: the resident pair's upper half
+        K3_SECT(8);
+        load_pair(g / 2 + 1);  // groups g+2, g+3 in flight (past the end: out of range, reads 0)
+      } else {
+        stage_half(false);    // group g+1: lower half of the pair loaded one group ago
+        K3_SECT(8);
+      }
       K3_SECT(9);
     }
   }
