@@ -597,7 +597,7 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
         if (!aborted && cur() < need) {
           const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
           for (;;) {
-            __builtin_amdgcn_s_sleep(2);
+            __builtin_amdgcn_s_sleep(4);  // 2 / 4 / 8 measured within 0.3 %; 4 leaves more slots
             if (cur() >= need) break;
             if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s: give up, flag
               // no exit from the loop here (an exit path skipping the stores would reach the
