@@ -627,6 +627,9 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
         } else {
           if (l < 21) ws[Y_OFF - BPS - 1 + l] = 127;
           if (l < 18) ws[(l < 9 ? U_OFF - BPS - 1 + l : V_OFF - BPS - 1 + (l - 9))] = 127;
+          // row 0's top-right samples (127) replicated to rows 3, 7, 11 for i4 blocks; nothing
+          // else writes those workspace bytes, so they hold for the whole MB row
+          if (l >= 21 && l < 24) st32(ws + Y_OFF + (3 + 4 * (l - 21)) * BPS + 16, 0x7f7f7f7fu);
         }
       }
       lds_sync();
@@ -642,11 +645,15 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
             ws[(l == 3 ? Y_OFF : l == 5 ? U_OFF : V_OFF) - BPS - 1] = (uint8_t)(top_carry >> 24);
           top_carry = tv;
         } else if (l == 8 && i4) {
-          st32(ws + Y_OFF - BPS + 16, last_x ? (uint32_t)col[15] * 0x01010101u : ld32(col + kColBytes));
+          // top-right samples, replicated down to rows 3, 7, 11 by the same lane (no read-back)
+          const uint32_t tr = last_x ? (uint32_t)col[15] * 0x01010101u : ld32(col + kColBytes);
+          st32(ws + Y_OFF - BPS + 16, tr);
+          st32(ws + Y_OFF + 3 * BPS + 16, tr);
+          st32(ws + Y_OFF + 7 * BPS + 16, tr);
+          st32(ws + Y_OFF + 11 * BPS + 16, tr);
         }
       }
       lds_sync();
-      if (act && i4 && l < 3) st32(ws + Y_OFF + (3 + 4 * l) * BPS + 16, ld32(ws + Y_OFF - BPS + 16));
 
       K1_SECT(3);
       // ---- residuals of all blocks (prediction-independent)
