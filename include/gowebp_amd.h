@@ -144,7 +144,7 @@ int wg_batch_run(wg_batch* b, void* stream);
  * inside the decode loop, io_dec.c.go:65-115). */
 int wg_batch_set_emit(wg_batch* b, int separate);
 
-/* The YUV420->RGBA stage alone (K2, EmitFancyRGB / EmitSampledRGB) over the batch's
+/* The YUV420->RGBA stage alone (K2: EmitFancyRGB / EmitSampledRGB, io_dec.c.go:53-115) over the batch's
  * reconstructed planes (after a wg_batch_run): the stage-roofline measurement of the
  * metric.  Its duration is reported as ms[1] by wg_batch_kernel_ms(). */
 int wg_batch_run_emit(wg_batch* b, void* stream);
