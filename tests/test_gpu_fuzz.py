@@ -61,3 +61,39 @@ def test_mutated_streams_gpu_equals_oracle(emit):
     assert checked >= 40, checked
     b.close()
     ctx.close()
+
+
+def test_mutated_lossless_streams_gpu_equals_oracle():
+    """The same for VP8L: bit-flipped lossless fixtures that still parse (other prefix codes,
+    transform data, palettes, cache bits) -> K3 (every kernel variant the mutants select)
+    == the oracle's inverse transforms, bit for bit."""
+    from oracle_lib import load_lossless, lossless_names, oracle_vp8l_decode
+    if webp_amd.device_count() < 1:
+        pytest.fail("no HIP device visible")
+    rng = np.random.default_rng(11)
+    cases = []
+    for n in sorted(lossless_names(), key=lambda n: len(load_lossless(n)[0]))[:10]:
+        d = bytearray(load_lossless(n)[0])
+        for _ in range(24):
+            m = bytearray(d)
+            for _ in range(int(rng.integers(1, 3))):
+                pos = int(rng.integers(25, len(m)))  # past the RIFF header and VP8L size fields
+                m[pos] ^= 1 << int(rng.integers(0, 8))
+            try:
+                info, argb, tdata = webp_amd.vp8l_parse(bytes(m))
+            except webp_amd.WebPError:
+                continue
+            cases.append((bytes(m), info, argb, tdata))
+    assert len(cases) >= 30, len(cases)
+    ctx = webp_amd.Context(0)
+    b = ctx.batch([c[0] for c in cases])
+    b.run()
+    checked = 0
+    for i, (_, info, argb, tdata) in enumerate(cases):
+        if b.status[i] != 0:
+            continue
+        np.testing.assert_array_equal(b.rgba(i), oracle_vp8l_decode(info, argb, tdata), err_msg=f"mutant {i}")
+        checked += 1
+    assert checked >= 30, checked
+    b.close()
+    ctx.close()
