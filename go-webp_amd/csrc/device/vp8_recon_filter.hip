@@ -7,34 +7,41 @@
 //   intra predictors     pkg/libwebp/dsp/dec.c.go:178-474 (indexed by mode enum)
 //   loop filters         pkg/libwebp/dsp/dec.c.go:484-682
 //
-// Geometry.  One 1024-thread workgroup per frame.  Wave w owns MB-row PAIRS
-// k = w, w+16, ...: half-wave 0 (lanes 0..31) decodes row 2k at column i while half 1
-// (lanes 32..63) decodes row 2k+1 at column i-2 -- the t = x + 2y wavefront, since
-// intra prediction (top-right samples) and the loop filter (MB (x+1,y-1)'s left-edge
-// writes) both reach one MB up and to the right.  Inside a pair the lockstep skew
-// satisfies the dependency; across pairs an LDS progress counter does (32 MB rows in
-// flight per frame).
+// Geometry.  One 1024-thread workgroup per frame.  Wave w < R owns MB-row QUADS
+// k = w, w+R, ...: lane group g = lane >> 4 decodes row 4k+g, at column i-2g in step i --
+// the t = x + 2y wavefront, since intra prediction (top-right samples) and the loop filter
+// (MB (x+1,y-1)'s left-edge writes) both reach one MB up and to the right.  Inside a quad
+// the lockstep skew satisfies the dependency; across quads an LDS progress counter does
+// (4R MB rows in flight per frame).
 //
-// One macroblock = 32 lanes.  Lane l owns column/row q = l&3 of luma 4x4 blocks l>>2 and
-// (l>>2)+8 and of chroma block 16+(l>>2).  IDCT (TransformOne, all blocks at once since
-// the residual (v>>3) does not depend on the prediction): vertical pass per column lane,
-// quad DPP transpose, horizontal pass.  i16/chroma prediction: one pixel row per lane.
-// i4x4 prediction walks the 10-step intra wavefront (block t = bx + 2by) with ONE PIXEL
-// PER LANE: each pixel of each predictor is a 3-tap recipe of edge samples
-// (pred4_table.inc, generated from dec.c.go's DST() formulas), so no lane branches on
-// the mode.  A non-zero block always goes through TransformOne: TransformAC3 /
+// One macroblock = 16 lanes.  Lane m = lane & 15 plays two "roles" r = m + 16s (s = 0, 1;
+// two unrolled passes per section) of a 32-role MB layout: role r owns column/row q = r&3
+// of luma 4x4 blocks r>>2 and (r>>2)+8 and of chroma block 16+(r>>2).  IDCT (TransformOne,
+// all blocks at once since the residual (v>>3) does not depend on the prediction):
+// vertical pass per column lane, quad DPP transpose, horizontal pass.  i16/chroma
+// prediction: one 4-pixel row per role.  i4x4 prediction walks the 16 blocks in the order
+// t = bx + 2by (a block's left, top, top-left and top-right neighbours all have a smaller
+// t) with ONE PIXEL PER LANE: each pixel of each predictor is a 3-tap recipe of edge
+// samples (pred4_table.inc, generated from dec.c.go's DST() formulas), so no lane branches
+// on the mode.  A non-zero block always goes through TransformOne: TransformAC3 /
 // TransformDC / TransformDCUV are exact special cases of it
 // (tests/test_oracle.py::test_transform_shortcuts_exact).
 //
-// Loop filter (per MB, libwebp edge order): lanes 0..15 luma lines, 16..31 chroma
-// lines of a per-MB LDS window; each lane runs all vertical edges on its row in
-// registers, then all horizontal edges on its column (two LDS round trips per MB).
+// Loop filter (per MB, libwebp edge order): lane m filters luma line m (4 edges), then
+// chroma line m&7 of U (m < 8) or V (2 edges), of a per-MB LDS window: every vertical edge
+// of a line in registers, then the same on columns (two LDS round trips per MB).
+//
+// Why four MBs per wave step.  The kernel is bound by instruction issue on the frame's CU
+// (DESIGN.md §4).  With 32 lanes per MB the filter's chroma lanes sat out the two luma-only
+// inner edges of each pass (8 edge slots per 2 MBs; here 12 per 4), and every per-step cost
+// that does not scale with the lanes -- scalar control, branches, the wavefront wait, the
+// LDS hand-off latency of the ~20 dependent sections -- is shared by twice the MBs.
 //
 // Memory.  Cross-MB state lives in LDS only: the unfiltered top samples `ytop`
 // (VP8TopSamples), the final bottom rows `fbot` of each MB column for the next row's
 // top-edge filter, progress counters.  Every HBM byte of the Y/U/V planes is written
-// exactly once, when final.  MB records and coefficients are software-pipelined:
-// record x+2 and coefficients x+1 are in flight while MB x is processed.
+// exactly once, when final.  MB records and coefficients are software-pipelined: record
+// x+2 and coefficients x+1 are in flight while MB x is processed.
 #include <hip/hip_runtime.h>
 #include <type_traits>
 #include <stdint.h>
@@ -50,7 +57,9 @@ namespace {
 #include "pred4_table.inc"
 
 constexpr int kWaves = 16;
-constexpr int BPS = 32;  // libwebp workspace stride (vp8/constants.go BPS)
+constexpr int kRows = 4;       // MB rows per wave (a quad); 16 lanes per MB
+constexpr int kMaxRecon = 12;  // waves that may reconstruct: LDS slots for 4 x 12 MB rows
+constexpr int BPS = 32;        // libwebp workspace stride (vp8/constants.go BPS)
 constexpr int Y_OFF = BPS * 1 + 8;
 constexpr int U_OFF = Y_OFF + BPS * 16 + BPS;
 constexpr int V_OFF = U_OFF + 16;
@@ -67,6 +76,9 @@ constexpr int kTabBytes = 640;
 constexpr int kHdrBytes = kProgBytes + kTabBytes;
 constexpr int kColBytes = 32 + 128;  // ytop (y16 u8 v8) + fbot (Y 4x16, U 4x8, V 4x8)
 constexpr uint32_t kDrop = 0x80000000u;  // buffer offset beyond any frame: store dropped
+// i4x4 blocks in wavefront order t = bx + 2*by, and their t
+constexpr int kI4Order[16] = {0, 1, 2, 4, 3, 5, 6, 8, 7, 9, 10, 12, 11, 13, 14, 15};
+constexpr int kI4Step[16] = {0, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 9};
 
 // Opt-in per-section cycle accounting (make VARIANT=timing -> libgowebp_amd_timing.so,
 // read back by scripts/k1_sections.py): s_memtime deltas summed per loop section in
@@ -173,10 +185,10 @@ __device__ __forceinline__ void idct_quad(int q, uint2 cv, int r[4]) {
   r[3] = (a - d) >> 3;
 }
 
-// Residuals of one IDCT pass (3 per MB: luma blocks b0, b0+8, chroma).  When every block
-// in the pass (both half-waves) is zero or DC-only, TransformOne reduces to
-// (in[0] + 4) >> 3 on every pixel (TransformDC, dec.c.go:112-118): broadcast the DC from
-// the quad's column-0 lane instead of running both butterfly passes.
+// Residuals of one IDCT pass (6 per MB step: luma blocks b0, b0+8 and chroma, for both
+// roles).  When every block in the pass (all four MBs) is zero or DC-only, TransformOne
+// reduces to (in[0] + 4) >> 3 on every pixel (TransformDC, dec.c.go:112-118): broadcast
+// the DC from the quad's column-0 lane instead of running both butterfly passes.
 __device__ __forceinline__ void idct_pass(int q, uint2 cv, int r[4]) {
   const uint32_t ac = (q == 0 ? (cv.x & 0xffff0000u) : cv.x) | cv.y;
   if (__all(ac == 0)) {
@@ -243,10 +255,6 @@ struct Line { int p3, p2, p1, p0, q0, q1, q2, q3; };
 __device__ __forceinline__ int sclip1(int v) { return min(max(v, -128), 127); }
 __device__ __forceinline__ int sclip2(int v) { return min(max(v, -16), 15); }
 
-// KIND 0: simple (NeedsFilter + DoFilter2, dec.c.go:552-586);
-// KIND 1: complex MB edge (FilterLoop26: hev ? DoFilter2 : DoFilter6, :592-606);
-// KIND 2: complex inner edge (FilterLoop24: hev ? DoFilter2 : DoFilter4, :608-622).
-// Branch-free: every variant is computed and selected.  t2 = 2*thresh + 1.
 // |a - b| (+ c) for byte values in one v_sad_u32 (sub/neg/max otherwise).
 __device__ __forceinline__ int absd(int a, int b, int c = 0) {
   int r;
@@ -254,6 +262,10 @@ __device__ __forceinline__ int absd(int a, int b, int c = 0) {
   return r;
 }
 
+// KIND 0: simple (NeedsFilter + DoFilter2, dec.c.go:552-586);
+// KIND 1: complex MB edge (FilterLoop26: hev ? DoFilter2 : DoFilter6, :592-606);
+// KIND 2: complex inner edge (FilterLoop24: hev ? DoFilter2 : DoFilter4, :608-622).
+// Branch-free: every variant is computed and selected.  t2 = 2*thresh + 1.
 template <int KIND>
 __device__ __forceinline__ void filter_line(Line& l, int t2, int it, int hev_t) {
   const int d0 = l.q0 - l.p0;
@@ -311,59 +323,54 @@ __device__ __forceinline__ void filter_at(int* v, int t2, int it, int ht) {
   v[6] = l.q2;
 }
 
-// DoFilter (frame_dec.c.go:204-251) for one MB per half-wave, libwebp edge order
-// (left MB edge, inner vertical edges, top MB edge, inner horizontal edges).
-// Lane l < 16 owns luma line l; lanes 16..31 chroma line l&7 of U (16..23) / V (24..31),
-// complex filter only.  Vertical edges: the lane loads its whole window row (luma cols
-// -4..15, chroma -4..7) and runs every vertical edge in registers; one LDS round trip
-// later it loads its window column and runs every horizontal edge the same way.  Two LDS
-// round trips per MB instead of one per edge step.
-template <bool kComplex>
-__device__ __forceinline__ void filter_mb(uint8_t* fw, int l, bool on, bool fx, bool fy, bool fin, int limit,
-                                          int ilevel, int hev_t) {
+// One line of DoFilter (frame_dec.c.go:204-251): the lane's window row (vertical edges,
+// the left MB edge first) or column (kCol: horizontal edges, the top MB edge first) of
+// luma (-4..15, edges at 0, 4, 8, 12) or chroma (-4..7, edges at 0, 4), loaded once, every
+// edge in registers, stored back.  Single-byte LDS accesses: the LDS unit zero-extends and
+// narrows, so the (issue-bound) wave spends no instructions unpacking and repacking.
+template <bool kComplex, bool kLuma, bool kCol>
+__device__ __forceinline__ void filter_line_pass(uint8_t* win, int li, bool f_mb, bool fin, int limit, int ilevel,
+                                                 int hev_t) {
   constexpr int KMB = kComplex ? 1 : 0, KIN = kComplex ? 2 : 0;
+  constexpr int st = kLuma ? FWY : FWC;
+  constexpr int n = kLuma ? 20 : 12;
+  constexpr int step = kCol ? st : 1;
   const int t_mb = 2 * (limit + 4) + 1, t_in = 2 * limit + 1;
-  const bool luma = l < 16;
-  const bool lane_on = on && (luma || kComplex);
-  const int li = luma ? l : (l & 7);
-  const int st = luma ? FWY : FWC;
-  uint8_t* win = fw + (luma ? kFwY : ((l >> 3) & 1 ? kFwV : kFwU));
-  int v[20];
-  if (lane_on) {  // vertical edges on window row li+4
-    // byte loads/stores like the column pass: the LDS unit zero-extends and narrows, so
-    // the (VALU-bound) wave spends no instructions unpacking and repacking the row
-    // (volatile: kept as single-byte accesses, not merged back into dwords + shifts)
-    volatile __attribute__((address_space(3))) uint8_t* row = (__attribute__((address_space(3))) uint8_t*)(win + (li + 4) * st);
+  // volatile: kept as single-byte accesses, not merged back into dwords + shifts
+  volatile __attribute__((address_space(3))) uint8_t* p =
+      (__attribute__((address_space(3))) uint8_t*)(kCol ? win + 4 + li : win + (li + 4) * st);
+  int v[n];
 #pragma unroll
-    for (int k = 0; k < 20; ++k) v[k] = (k < 12 || luma) ? row[k] : 0;
-    if (fx) filter_at<KMB>(v + 0, t_mb, ilevel, hev_t);  // HFilter16 / HFilter8 / SimpleHFilter16
-    if (fin) {
-      filter_at<KIN>(v + 4, t_in, ilevel, hev_t);  // HFilter16i / HFilter8i
-      if (luma) {
-        filter_at<KIN>(v + 8, t_in, ilevel, hev_t);
-        filter_at<KIN>(v + 12, t_in, ilevel, hev_t);
-      }
+  for (int k = 0; k < n; ++k) v[k] = p[k * step];
+  if (f_mb) filter_at<KMB>(v + 0, t_mb, ilevel, hev_t);  // {H,V}Filter16 / {H,V}Filter8 / Simple{H,V}Filter16
+  if (fin) {
+    filter_at<KIN>(v + 4, t_in, ilevel, hev_t);  // {H,V}Filter16i / {H,V}Filter8i
+    if (kLuma) {
+      filter_at<KIN>(v + 8, t_in, ilevel, hev_t);
+      filter_at<KIN>(v + 12, t_in, ilevel, hev_t);
     }
+  }
 #pragma unroll
-    for (int k = 1; k < 19; ++k)
-      if (k < 11 || luma) row[k] = (uint8_t)v[k];
+  for (int k = 1; k < n - 1; ++k) p[k * step] = (uint8_t)v[k];
+}
+
+// DoFilter (frame_dec.c.go:204-251) for the lane group's MB, libwebp edge order (left MB
+// edge, inner vertical edges, top MB edge, inner horizontal edges): lane m filters luma line
+// m and -- complex filter only -- chroma line m & 7 of U (m < 8) / V (m >= 8).
+template <bool kComplex>
+__device__ __forceinline__ void filter_mb(uint8_t* fw, int m, bool on, bool fx, bool fy, bool fin, int limit,
+                                          int ilevel, int hev_t) {
+  uint8_t* wy = fw + kFwY;
+  uint8_t* wc = fw + (m >= 8 ? kFwV : kFwU);
+  const int mc = m & 7;
+  if (on) {
+    filter_line_pass<kComplex, true, false>(wy, m, fx, fin, limit, ilevel, hev_t);
+    if (kComplex) filter_line_pass<true, false, false>(wc, mc, fx, fin, limit, ilevel, hev_t);
   }
   lds_sync();
-  if (lane_on) {  // horizontal edges on window column li+4
-    uint8_t* col = win + 4 + li;
-#pragma unroll
-    for (int k = 0; k < 20; ++k) v[k] = (k < 12 || luma) ? col[k * st] : 0;
-    if (fy) filter_at<KMB>(v + 0, t_mb, ilevel, hev_t);  // VFilter16 / VFilter8 / SimpleVFilter16
-    if (fin) {
-      filter_at<KIN>(v + 4, t_in, ilevel, hev_t);  // VFilter16i / VFilter8i
-      if (luma) {
-        filter_at<KIN>(v + 8, t_in, ilevel, hev_t);
-        filter_at<KIN>(v + 12, t_in, ilevel, hev_t);
-      }
-    }
-#pragma unroll
-    for (int k = 1; k < 19; ++k)
-      if (k < 11 || luma) col[k * st] = (uint8_t)v[k];
+  if (on) {
+    filter_line_pass<kComplex, true, true>(wy, m, fy, fin, limit, ilevel, hev_t);
+    if (kComplex) filter_line_pass<true, false, true>(wc, mc, fy, fin, limit, ilevel, hev_t);
   }
   lds_sync();
 }
@@ -411,16 +418,17 @@ __device__ __forceinline__ bool wait_at_least(uint32_t* p, uint32_t need) {
 }
 
 // K1's tail: the frame's YUV420 -> RGBA (K2's strip conversion, yuv_rgba_strip.h) done by
-// the waves whose reconstruction work is over, while the last MB-row pairs are still being
-// decoded (68 pairs of a 4K frame over 16 waves leave 12 waves idle for the last ~15 % of
-// the frame).  Units = (band, strip), claimed top-down from an LDS counter.  A band needs
-// luma rows <= L and chroma rows <= C final: MB row m has published luma rows <= 16m + 12
-// and chroma rows <= 8m + 4 once its pair's progress reaches mb_w (rows 13-15 / 5-7 are
-// written by the row below; the last MB row writes all).  One MB row of margin beyond that.
+// the waves whose reconstruction work is over, while the last MB-row quads are still being
+// decoded.  Units = (band, strip), claimed top-down from an LDS counter.  A band needs luma
+// rows <= L and chroma rows <= C final: MB row m has published luma rows <= 16m + 12 and
+// chroma rows <= 8m + 4 once its quad's progress reaches mb_w (rows 13-15 / 5-7 are written
+// by the row below; the last MB row writes all).  One MB row of margin beyond that.  The
+// last quad publishes no progress (no quad waits on it): its rows wait for every wave.
 template <bool kFancy>
-__device__ __forceinline__ void emit_tail(const FrameDesc& F, uint32_t* progress, uint32_t* recon_done, uint32_t* next_unit, int lane,
-                          int* err) {
+__device__ __forceinline__ void emit_tail(const FrameDesc& F, uint32_t* progress, uint32_t* recon_done,
+                                          uint32_t* next_unit, int lane, int* err) {
   const int W = F.width, H = F.height, uv_h = (H + 1) >> 1, mb_w = F.mb_w, mb_h = F.mb_h;
+  const int nquads = (mb_h + kRows - 1) / kRows;
   const int sx = strip::strips_x(W);
   const int npairs = kFancy ? (H >> 1) + 1 : (H + 1) >> 1;
   const int n_units = sx * ((npairs + strip::kPairs - 1) / strip::kPairs);
@@ -433,9 +441,10 @@ __device__ __forceinline__ void emit_tail(const FrameDesc& F, uint32_t* progress
     const int p1 = min((band + 1) * strip::kPairs, npairs);
     const int L = min(2 * p1 - 1, H - 1), C = min(p1 - 1, uv_h - 1);
     const int m = max(max((L + 3) >> 4, (C + 3) >> 3), 0) + 1;  // ceil((L-12)/16), ceil((C-4)/8), + margin
+    const int qm = m / kRows;
     bool ok;
-    if (m >= mb_h - 1) ok = wait_at_least(recon_done, kWaves);
-    else ok = wait_at_least(progress + ((m >> 1) & (kWaves - 1)), ((uint32_t)(m >> 1) << 16) | (uint32_t)mb_w);
+    if (m >= mb_h - 1 || qm >= nquads - 1) ok = wait_at_least(recon_done, kWaves);
+    else ok = wait_at_least(progress + (qm & (kWaves - 1)), ((uint32_t)qm << 16) | (uint32_t)mb_w);
     if (!ok) {
       if (lane == 0) atomicOr(err, 1);
       return;
@@ -447,12 +456,12 @@ __device__ __forceinline__ void emit_tail(const FrameDesc& F, uint32_t* progress
 }  // namespace
 
 // kGlobalCols: the per-MB-column store (kColBytes per column) lives in LDS when the frame's
-// columns fit next to the workspaces (mb_w <= vp8_recon_max_mb_w(), 9600 px), else in a
-// per-frame global buffer (FrameDesc::cols, wide frames up to VP8's 16383 px).  Each variant
-// skips the other's frames.  The hand-offs through the store keep their ordering: within a
-// wave (row 2k -> 2k+1) by the fences of lds_sync, across waves by the release/acquire
-// progress counters -- at workgroup scope the AMDGPU memory model orders global accesses
-// of one CU the same way (its L1 is shared by the workgroup), no extra s_waitcnt needed.
+// columns fit next to the workspaces (mb_w <= vp8_recon_max_mb_w()), else in a per-frame
+// global buffer (FrameDesc::cols, wide frames up to VP8's 16383 px).  Each variant skips the
+// other's frames.  The hand-offs through the store keep their ordering: within a wave (row
+// 4k+g -> 4k+g+1) by the fences of lds_sync, across waves by the release/acquire progress
+// counters -- at workgroup scope the AMDGPU memory model orders global accesses of one CU
+// the same way (its L1 is shared by the workgroup), no extra s_waitcnt needed.
 template <bool kGlobalCols>
 __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc* __restrict__ frames, int* err,
                                                                 int lead_arg, int recon_waves_arg) {
@@ -479,111 +488,111 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
   const __amdgpu_buffer_rsrc_t planes =
       __builtin_amdgcn_make_buffer_rsrc(F->y, 0, (int)(voff + (uint32_t)(8 * mb_h * uvs)), 0x00020000);
 
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // SGPR: k and the pair loop stay uniform
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // SGPR: k and the quad loop stay uniform
   const int lane = threadIdx.x & 63;
   K1_SECT_DECL();
-  // Required lead of the previous row pair, in MB columns: 2 (top-right samples and the
-  // left-edge filter of MB (x+1, y-1) reach one MB up-right).  Larger leads were measured
-  // slower (c3: lead 2 9.7 ms, 8 10.2 ms, 16 11.6 ms): waves held back at start-up idle
-  // while the running ones gain nothing, so the pairs are packed as tightly as allowed.
+  // Required lead of the previous quad's last row, in MB columns: 2 (top-right samples and
+  // the left-edge filter of MB (x+1, y-1) reach one MB up-right).  Larger leads were
+  // measured slower (round 1, pairs): waves held back at start-up idle while the running
+  // ones gain nothing.
   const int lead = max(2, lead_arg);
-  const int h = lane >> 5;  // half-wave: 0 = row 2k, 1 = row 2k+1
-  const int l = lane & 31;
+  const int g = lane >> 4;  // MB row of the quad this lane decodes
   uint32_t* tab = reinterpret_cast<uint32_t*>(lds + kProgBytes);
   using ColPtr = std::conditional_t<kGlobalCols, gptr<uint8_t>, uint8_t*>;
   ColPtr cols;
   if constexpr (kGlobalCols) cols = as_global(F->cols);
-  else cols = lds + kHdrBytes + 2 * kWaves * kSlotBytes;
+  else cols = lds + kHdrBytes + kMaxRecon * kRows * kSlotBytes;
   // per MB column c: cols + c*kColBytes: [0..15] ytop Y, [16..23] U, [24..31] V, [32..159] fbot
   if (threadIdx.x < kWaves) progress[threadIdx.x] = 0;
   if (threadIdx.x == 0) recon_done = next_unit = 0;
   const bool emit = F->flags & kFrameEmitRgba;
   if (emit) __builtin_amdgcn_s_setprio(2);  // reconstruction is the critical path; the tail's conversion yields
-  // Waves that reconstruct (pairs k = wave, wave + R, ...); with the RGBA tail the others
-  // convert bands from the start.  Measured: tall frames (4K, 68 pairs) run
-  // fastest with R = 12 -- three reconstructing waves and one converting wave per SIMD
-  // (10.04 vs 10.63 ms at R = 16); 1080p (34 pairs) with R = 16 (2.72 vs 2.98 ms); SIMD-
-  // unbalanced R (13-15) and R <= 11 are slower.  R <= 16 keeps the progress ring safe:
-  // pair k + 16 only starts on a wave that has completed a pair > k, so pair k is complete.
-  const int R = !emit ? kWaves
-                      : recon_waves_arg > 0 ? min(recon_waves_arg, kWaves) : ((mb_h + 1) >> 1) > 48 ? 12 : kWaves;
+  const int nquads = (mb_h + kRows - 1) / kRows;
+  // Waves that reconstruct (quads k = wave, wave + R, ...); with the RGBA tail the others
+  // convert bands from the start.  R <= kMaxRecon (the LDS slots) also keeps the progress
+  // ring safe: quad k + 16 only starts on a wave that has completed a quad > k, so quad k
+  // is complete whenever its slot holds a later quad's value.
+  const int R = recon_waves_arg > 0 ? min(recon_waves_arg, kMaxRecon) : kMaxRecon;
   for (int t = threadIdx.x; t < 160; t += blockDim.x) tab[t] = kPred4Table[t];
   K1_TIMELINE_START();
   __syncthreads();
 
   bool aborted = false;  // a progress wait timed out (error flagged): stop waiting
-  for (int k = wave; wave < R && 2 * k < mb_h; k += R) {
-    const int y = 2 * k + h;
+  for (int k = wave; wave < R && k < nquads; k += R) {
+    const int y = kRows * k + g;
     const bool row_ok = y < mb_h;
-    const bool has_odd = 2 * k + 1 < mb_h;
+    const bool has_next = kRows * (k + 1) < mb_h;  // a later quad waits on this one's last row
     const bool last_row = y == mb_h - 1;
     const int nrows_y = last_row ? 16 : 13;  // luma rows of this MB row final after its pass
     const int nrows_c = last_row ? 8 : 5;
     uint32_t blk = row_ok ? row_block0[y] : 0u;
-    MbRec rc = load_rec(recs, mb_w, y, row_ok, -2 * h);
-    MbRec rn = load_rec(recs, mb_w, y, row_ok, -2 * h + 1);
-    Coefs cc = load_coefs(blks, rc.flags & kNzMask, blk, (l >> 2), 16 + (l >> 2), l & 3);
+    MbRec rc = load_rec(recs, mb_w, y, row_ok, -2 * g);
+    MbRec rn = load_rec(recs, mb_w, y, row_ok, -2 * g + 1);
+    Coefs cc[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int r = (lane & 15) + 16 * s;
+      cc[s] = load_coefs(blks, rc.flags & kNzMask, blk, r >> 2, 16 + (r >> 2), r & 3);
+    }
     // Retire the prologue loads here (visible to the waitcnt pass: 0x0F70 = vmcnt(0)), so the
     // loop header has no pending loads on cc/rc/rn and the in-loop uses of cc do not
     // conservatively drain the NEXT MB's prefetch with a vmcnt(0).
     __builtin_amdgcn_s_waitcnt(0x0F70);
     uint32_t top_carry = 0;  // see "top samples"
-    // Plane offsets of the five HBM store slots (see "final pixels to HBM") at MB column 0,
-    // once per pair: per MB only `x << shift` is added.  A slot that never stores for this
-    // row/lane starts at kDrop, and kDrop + 16x stays beyond the planes (dropped store).
-    uint32_t sbA0, sbA1, sbB, sbC, sbE, shB, shC;
-    {
-      const int l0 = lane & 31, q0 = l0 & 3, b00 = l0 >> 2;
-      sbA0 = b00 < nrows_y ? (uint32_t)__mul24(16 * y + b00, ys) - 4u + 4u * q0 : kDrop;
-      sbA1 = b00 + 8 < nrows_y ? (uint32_t)__mul24(16 * y + b00 + 8, ys) - 4u + 4u * q0 : kDrop;
+    // Plane offsets of the five HBM store slots (see "final pixels to HBM") of both roles at
+    // MB column 0, once per quad: per MB only `x << shift` is added.  A slot that never
+    // stores for this row/role starts at kDrop, and kDrop + 16x stays beyond the planes.
+    uint32_t sbA0[2], sbA1[2], sbB[2], sbC[2], sbE[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int l0 = (lane & 15) + 16 * s, q0 = l0 & 3, b00 = l0 >> 2;
+      sbA0[s] = b00 < nrows_y ? (uint32_t)__mul24(16 * y + b00, ys) - 4u + 4u * q0 : kDrop;
+      sbA1[s] = b00 + 8 < nrows_y ? (uint32_t)__mul24(16 * y + b00 + 8, ys) - 4u + 4u * q0 : kDrop;
       const int bk = l0 - 12, bp = bk >= 6, brem = bk - 6 * bp;
       const int brr = l0 < 12 ? (l0 >> 2) - 3 : (brem >> 1) - 3;
       const int bd = l0 < 12 ? (l0 & 3) : (brem & 1);
-      sbB = !(y > 0 && l0 < 24) ? kDrop
-            : l0 < 12 ? (uint32_t)__mul24(16 * y + brr, ys) + 4u * bd
-                      : (bp ? voff : uoff) + (uint32_t)__mul24(8 * y + brr, uvs) + 4u * bd;
-      shB = l0 < 12 ? 4 : 3;
+      sbB[s] = !(y > 0 && l0 < 24) ? kDrop
+               : l0 < 12 ? (uint32_t)__mul24(16 * y + brr, ys) + 4u * bd
+                         : (bp ? voff : uoff) + (uint32_t)__mul24(8 * y + brr, uvs) + 4u * bd;
       const bool cl = l0 >= 16;
       const uint32_t cpoff = ((l0 >> 3) & 1) ? voff : uoff;
-      sbC = cl ? ((l0 & 7) < nrows_c ? cpoff + (uint32_t)__mul24(8 * y + (l0 & 7), uvs) + 4u : kDrop)
-               : (l0 < nrows_y ? (uint32_t)__mul24(16 * y + l0, ys) + 12u : kDrop);
-      shC = cl ? 3 : 4;
+      sbC[s] = cl ? ((l0 & 7) < nrows_c ? cpoff + (uint32_t)__mul24(8 * y + (l0 & 7), uvs) + 4u : kDrop)
+                  : (l0 < nrows_y ? (uint32_t)__mul24(16 * y + l0, ys) + 12u : kDrop);
       const int ep = l0 >> 4, er = (l0 >> 1) & 7, ed = l0 & 1;
-      sbE = er < nrows_c ? (ep ? voff : uoff) + (uint32_t)__mul24(8 * y + er, uvs) - 4u + 4u * ed : kDrop;
+      sbE[s] = er < nrows_c ? (ep ? voff : uoff) + (uint32_t)__mul24(8 * y + er, uvs) - 4u + 4u * ed : kDrop;
     }
 
     K1_SECT_START();
 
-    for (int i = 0; i < mb_w + 2; ++i) {
+    for (int i = 0; i < mb_w + 2 * (kRows - 1); ++i) {
       // Lane roles, recomputed every iteration from an opaque lane id: hoisted out of the
-      // loop, the ~40 lane-constant LDS addresses derived from them spill (rule from
+      // loop, the lane-constant LDS addresses derived from them spill (rule from
       // cdna_hip_programming.md: recompute per block with v_mbcnt).
       int lid;
       asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lid));
-      const int l = lid & 31;
-      uint8_t* ws = lds + kHdrBytes + (wave * 2 + h) * kSlotBytes;  // recon workspace (libwebp yuv_b)
-      uint8_t* fw = ws + kWsBytes;                                  // filter window
-      uint8_t* left = fw + kFwBytes;                                // unfiltered left columns
-      int16_t* res = reinterpret_cast<int16_t*>(left + kLeftBytes);  // i4x4 residuals
-      const int q = l & 3;
-      const int b0 = l >> 2;              // luma blocks b0 and b0+8
-      const int lbx = b0 & 3, lby = b0 >> 2;
-      const int cpl = (l >> 4) & 1, cbk = (l >> 2) & 3;
-      const int cbx = cbk & 1, cby = cbk >> 1;
-      const int cb = 16 + cpl * 4 + cbk;  // chroma block index
-      const int coff = cpl ? V_OFF : U_OFF;
-      const int ps = l >> 4, pp = l & 15, ppx = pp & 3, ppy = pp >> 2;  // i4x4 pixel lanes
-      const int x = i - 2 * h;
+      const int m = lid & 15;
+      const int gg = lid >> 4;
+      uint8_t* ws = lds + kHdrBytes + (wave * kRows + gg) * kSlotBytes;  // recon workspace (libwebp yuv_b)
+      uint8_t* fw = ws + kWsBytes;                                        // filter window
+      uint8_t* left = fw + kFwBytes;                                      // unfiltered left columns
+      int16_t* res = reinterpret_cast<int16_t*>(left + kLeftBytes);        // i4x4 residuals
+      const int q = m & 3;
+      const int x = i - 2 * gg;
       const bool act = row_ok && x >= 0 && x < mb_w;
       const bool last_x = x == mb_w - 1;
       K1_SECT(13);
       // ---- software pipeline: record x+2 and coefficients x+1 in flight during MB x
       const MbRec rnn = load_rec(recs, mb_w, y, row_ok, x + 2);
       const uint32_t blk_next = blk + __builtin_popcount(rc.flags & kNzMask);
-      const Coefs cn = load_coefs(blks, rn.flags & kNzMask, blk_next, b0, cb, q);
+      Coefs cn[2];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int r = m + 16 * s;
+        cn[s] = load_coefs(blks, rn.flags & kNzMask, blk_next, r >> 2, 16 + (r >> 2), q);
+      }
 
       K1_SECT(0);
-      // ---- wait for the previous pair's odd row (t = x + 2y wavefront)
+      // ---- wait for the previous quad's last row (t = x + 2y wavefront)
       //      The counter is read into an SGPR (readfirstlane) so the spin is a scalar branch,
       //      and the timeout does not leave the loop: any path reaching the loop latch without
       //      this iteration's plane stores makes the waitcnt pass extend the latch's prefetch
@@ -597,7 +606,7 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
         if (!aborted && cur() < need) {
           const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
           for (;;) {
-            __builtin_amdgcn_s_sleep(4);  // 2 / 4 / 8 measured within 0.3 %; 4 leaves more slots
+            __builtin_amdgcn_s_sleep(4);
             if (cur() >= need) break;
             if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s: give up, flag
               // no exit from the loop here (an exit path skipping the stores would reach the
@@ -616,35 +625,40 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
       K1_SECT(1);
       // ---- ReconstructRow prologue at the row's first MB (frame_dec.c.go:79-98)
       if (act && x == 0) {
-        if (l < 16) ws[Y_OFF + l * BPS - 1] = 129;
-        else if (l < 24) ws[U_OFF + (l - 16) * BPS - 1] = 129;
-        else ws[V_OFF + (l - 24) * BPS - 1] = 129;
-        left[l] = 129;
-        if (y > 0) {
-          if (l == 0) ws[Y_OFF - BPS - 1] = 129;
-          if (l == 1) ws[U_OFF - BPS - 1] = 129;
-          if (l == 2) ws[V_OFF - BPS - 1] = 129;
-        } else {
-          if (l < 21) ws[Y_OFF - BPS - 1 + l] = 127;
-          if (l < 18) ws[(l < 9 ? U_OFF - BPS - 1 + l : V_OFF - BPS - 1 + (l - 9))] = 127;
-          // row 0's top-right samples (127) replicated to rows 3, 7, 11 for i4 blocks; nothing
-          // else writes those workspace bytes, so they hold for the whole MB row
-          if (l >= 21 && l < 24) st32(ws + Y_OFF + (3 + 4 * (l - 21)) * BPS + 16, 0x7f7f7f7fu);
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const int l = m + 16 * s;
+          if (l < 16) ws[Y_OFF + l * BPS - 1] = 129;
+          else if (l < 24) ws[U_OFF + (l - 16) * BPS - 1] = 129;
+          else ws[V_OFF + (l - 24) * BPS - 1] = 129;
+          left[l] = 129;
+          if (y > 0) {
+            if (l == 0) ws[Y_OFF - BPS - 1] = 129;
+            if (l == 1) ws[U_OFF - BPS - 1] = 129;
+            if (l == 2) ws[V_OFF - BPS - 1] = 129;
+          } else {
+            if (l < 21) ws[Y_OFF - BPS - 1 + l] = 127;
+            if (l < 18) ws[(l < 9 ? U_OFF - BPS - 1 + l : V_OFF - BPS - 1 + (l - 9))] = 127;
+            // row 0's top-right samples (127) replicated to rows 3, 7, 11 for i4 blocks;
+            // nothing else writes those workspace bytes, so they hold for the whole MB row
+            if (l >= 21 && l < 24) st32(ws + Y_OFF + (3 + 4 * (l - 21)) * BPS + 16, 0x7f7f7f7fu);
+          }
         }
       }
       lds_sync();
       K1_SECT(2);
-      // ---- top samples (frame_dec.c.go:122-142).  The top-left sample (row -1, col -1) is
-      //      the previous column's top byte 15 (chroma: 7), which the current row has already
-      //      overwritten in `cols`: lanes 3, 5, 7 carry it over from their previous load.
+      // ---- top samples (frame_dec.c.go:122-142), lanes m < 9.  The top-left sample (row -1,
+      //      col -1) is the previous column's top byte 15 (chroma: 7), which the current row
+      //      has already overwritten in `cols`: lanes 3, 5, 7 carry it over from their
+      //      previous load.
       if (act && y > 0) {
-        if (l < 8) {
-          const uint32_t tv = ld32(col + 4 * l);
-          st32(ws + (l < 4 ? Y_OFF - BPS + 4 * l : l < 6 ? U_OFF - BPS + 4 * (l - 4) : V_OFF - BPS + 4 * (l - 6)), tv);
-          if (x > 0 && (l == 3 || l == 5 || l == 7))
-            ws[(l == 3 ? Y_OFF : l == 5 ? U_OFF : V_OFF) - BPS - 1] = (uint8_t)(top_carry >> 24);
+        if (m < 8) {
+          const uint32_t tv = ld32(col + 4 * m);
+          st32(ws + (m < 4 ? Y_OFF - BPS + 4 * m : m < 6 ? U_OFF - BPS + 4 * (m - 4) : V_OFF - BPS + 4 * (m - 6)), tv);
+          if (x > 0 && (m == 3 || m == 5 || m == 7))
+            ws[(m == 3 ? Y_OFF : m == 5 ? U_OFF : V_OFF) - BPS - 1] = (uint8_t)(top_carry >> 24);
           top_carry = tv;
-        } else if (l == 8 && i4) {
+        } else if (m == 8 && i4) {
           // top-right samples, replicated down to rows 3, 7, 11 by the same lane (no read-back)
           const uint32_t tr = last_x ? (uint32_t)col[15] * 0x01010101u : ld32(col + kColBytes);
           st32(ws + Y_OFF - BPS + 16, tr);
@@ -657,19 +671,19 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
 
       K1_SECT(3);
       // ---- residuals of all blocks (prediction-independent)
-      int ry0[4], ry1[4], rcr[4];
-      idct_pass(q, cc.y0, ry0);
-      idct_pass(q, cc.y1, ry1);
-      idct_pass(q, cc.c, rcr);
+      int ry0[2][4], ry1[2][4], rcr[2][4];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        idct_pass(q, cc[s].y0, ry0[s]);
+        idct_pass(q, cc[s].y1, ry1[s]);
+        idct_pass(q, cc[s].c, rcr[s]);
+      }
 
       K1_SECT(4);
-      // ---- luma prediction + residual
-      const int row_a = 4 * lby + q, row_b = row_a + 8;
-      uint8_t* dst_a = ws + Y_OFF + row_a * BPS + 4 * lbx;
-      uint8_t* dst_b = ws + Y_OFF + row_b * BPS + 4 * lbx;
+      // ---- luma prediction + residual (role r: block column (r>>2)&3, pixel rows
+      //      4*((r>>2)>>2)+q and that + 8)
       if (act && !i4) {
         const uint32_t oh = 1u << check_mode(x, y, (fl >> kYModeShift) & 3);
-        const uint32_t top = ld32(ws + Y_OFF - BPS + 4 * lbx);
         const int tl = ws[Y_OFF - BPS - 1];
         uint32_t st = 0, sl = 0;
         if (__any(oh & 0x31)) {
@@ -680,57 +694,72 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
           }
         }
         const int dc = dc_value(oh, st, sl, 4);
-        const uint32_t pa = pred_row(oh, top, left[row_a], tl, dc);
-        const uint32_t pb = pred_row(oh, top, left[row_b], tl, dc);
-        st32(dst_a, add_res(pa, ry0));
-        st32(dst_b, add_res(pb, ry1));
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const int b0 = (m + 16 * s) >> 2, lbx = b0 & 3, lby = b0 >> 2;
+          const int row_a = 4 * lby + q, row_b = row_a + 8;
+          const uint32_t top = ld32(ws + Y_OFF - BPS + 4 * lbx);
+          st32(ws + Y_OFF + row_a * BPS + 4 * lbx, add_res(pred_row(oh, top, left[row_a], tl, dc), ry0[s]));
+          st32(ws + Y_OFF + row_b * BPS + 4 * lbx, add_res(pred_row(oh, top, left[row_b], tl, dc), ry1[s]));
+        }
       }
-      if (act && i4) {  // stage residuals for the pixel-per-lane wavefront
-        *reinterpret_cast<uint2*>(res + b0 * 16 + q * 4) =
-            make_uint2((ry0[0] & 0xffff) | (ry0[1] << 16), (ry0[2] & 0xffff) | (ry0[3] << 16));
-        *reinterpret_cast<uint2*>(res + (b0 + 8) * 16 + q * 4) =
-            make_uint2((ry1[0] & 0xffff) | (ry1[1] << 16), (ry1[2] & 0xffff) | (ry1[3] << 16));
+      if (act && i4) {  // stage residuals for the pixel-per-lane block walk
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const int b0 = (m + 16 * s) >> 2;
+          *reinterpret_cast<uint2*>(res + b0 * 16 + q * 4) =
+              make_uint2((ry0[s][0] & 0xffff) | (ry0[s][1] << 16), (ry0[s][2] & 0xffff) | (ry0[s][3] << 16));
+          *reinterpret_cast<uint2*>(res + (b0 + 8) * 16 + q * 4) =
+              make_uint2((ry1[s][0] & 0xffff) | (ry1[s][1] << 16), (ry1[s][2] & 0xffff) | (ry1[s][3] << 16));
+        }
       }
-      // ---- chroma prediction + residual (lane = one pixel row of one 4x4 chroma block); independent
-      //      of the luma blocks, so it shares their section (one LDS hand-off less per MB)
+      // ---- chroma prediction + residual (role m + 16s: plane U for s = 0, V for s = 1; one
+      //      pixel row of one 4x4 block); independent of the luma blocks, so it shares their
+      //      section (one LDS hand-off less per MB)
       if (act) {
         const uint32_t oh = 1u << check_mode(x, y, (fl >> kUVModeShift) & 3);
-        const uint8_t* base = ws + coff;
-        const uint8_t* cleft = left + 16 + 8 * cpl;
+        const int cbk = (m >> 2) & 3, cbx = cbk & 1, cby = cbk >> 1;
         const int row = 4 * cby + q;
-        uint32_t st = 0, sl = 0;
-        if (__any(oh & 0x31)) {
-          st = __builtin_amdgcn_sad_u8(ld32(base - BPS), 0, 0);
-          st = __builtin_amdgcn_sad_u8(ld32(base - BPS + 4), 0, st);
-          sl = __builtin_amdgcn_sad_u8(ld32(cleft), 0, 0);
-          sl = __builtin_amdgcn_sad_u8(ld32(cleft + 4), 0, sl);
+        const bool any_dc = __any(oh & 0x31);
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const int coff = s ? V_OFF : U_OFF;
+          const uint8_t* base = ws + coff;
+          const uint8_t* cleft = left + 16 + 8 * s;
+          uint32_t st = 0, sl = 0;
+          if (any_dc) {
+            st = __builtin_amdgcn_sad_u8(ld32(base - BPS), 0, 0);
+            st = __builtin_amdgcn_sad_u8(ld32(base - BPS + 4), 0, st);
+            sl = __builtin_amdgcn_sad_u8(ld32(cleft), 0, 0);
+            sl = __builtin_amdgcn_sad_u8(ld32(cleft + 4), 0, sl);
+          }
+          const uint32_t pred =
+              pred_row(oh, ld32(base - BPS + 4 * cbx), cleft[row], base[-BPS - 1], dc_value(oh, st, sl, 3));
+          st32(ws + coff + row * BPS + 4 * cbx, add_res(pred, rcr[s]));
         }
-        const uint32_t pred = pred_row(oh, ld32(base - BPS + 4 * cbx), cleft[row], base[-BPS - 1], dc_value(oh, st, sl, 3));
-        st32(ws + coff + row * BPS + 4 * cbx, add_res(pred, rcr));
       }
       lds_sync();
       K1_SECT(5);
       if (__any(act && i4)) {
-        // recipe words and residuals of all ten steps fetched up front (independent loads)
+        // recipe words and residuals of all sixteen blocks fetched up front (independent loads)
         const uint32_t im_lo = rc.imodes_lo, im_hi = rc.imodes_hi;
-        uint32_t e[10];
-        int rs[10];
+        const int ppx = m & 3, ppy = m >> 2;
+        uint32_t e[16];
+        int rs[16];
 #pragma unroll
-        for (int t = 0; t < 10; ++t) {
-          const int by = min(max(0, (t - 2) >> 1) + ps, 3);
-          const int bx = min(max(t - 2 * by, 0), 3);
-          const int bi = by * 4 + bx;
+        for (int j = 0; j < 16; ++j) {
+          const int bi = kI4Order[j];
           const int mode = (bi < 8 ? im_lo >> (4 * bi) : im_hi >> (4 * (bi - 8))) & 0xf;
-          e[t] = tab[mode * 16 + pp];
-          rs[t] = res[bi * 16 + pp];
+          e[j] = tab[mode * 16 + m];
+          rs[j] = res[bi * 16 + m];
         }
+        // blocks of equal t are independent: one LDS hand-off per t
 #pragma unroll
-        for (int t = 0; t < 10; ++t) {
-          const int by = max(0, (t - 2) >> 1) + ps;
-          const int bx = t - 2 * by;
-          if (act && i4 && by <= min(3, t >> 1) && bx >= 0) {
+        for (int j = 0; j < 16; ++j) {
+          const int bi = kI4Order[j], bx = bi & 3, by = bi >> 2;
+          if (act && i4) {
             uint8_t* org = ws + Y_OFF + 4 * by * BPS + 4 * bx;
-            const uint32_t ew = e[t];
+            const uint32_t ew = e[j];
             const int kind = ew >> 24;
             const int a = org[(int8_t)(ew & 0xff)];
             const int b = org[(int8_t)((ew >> 8) & 0xff)];
@@ -745,9 +774,9 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
               const int tm = clamp255(a + b - c);
               v = (kind & 2) ? tm : (kind & 1) ? avg2 : avg3;
             }
-            org[ppy * BPS + ppx] = (uint8_t)clamp255(v + rs[t]);
+            org[ppy * BPS + ppx] = (uint8_t)clamp255(v + rs[j]);
           }
-          lds_sync();
+          if (j == 15 || kI4Step[j + 1] != kI4Step[j]) lds_sync();
         }
       }
 
@@ -755,25 +784,25 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
       K1_SECT(7);
       if (act) {
         // ---- stash unfiltered bottom samples for the row below (frame_dec.c.go:175-179)
-        //      (lanes 0..3 luma, 4..5 U, 6..7 V: the column store's dword l either way)
-        if (!last_row && l < 8) {
-          const int so = l < 4 ? Y_OFF + 15 * BPS + 4 * l : (l < 6 ? U_OFF - 16 : V_OFF - 24) + 7 * BPS + 4 * l;
-          st32(col + 4 * l, ld32(ws + so));
+        //      (lanes 0..3 luma, 4..5 U, 6..7 V: the column store's dword m either way)
+        if (!last_row && m < 8) {
+          const int so = m < 4 ? Y_OFF + 15 * BPS + 4 * m : (m < 6 ? U_OFF - 16 : V_OFF - 24) + 7 * BPS + 4 * m;
+          st32(col + 4 * m, ld32(ws + so));
         }
         // ---- filter window: MB body from the workspace, rows above from fbot
-        st32(fw + kFwY + (b0 + 4) * FWY + 4 + 4 * q, ld32(ws + Y_OFF + b0 * BPS + 4 * q));
-        st32(fw + kFwY + (b0 + 12) * FWY + 4 + 4 * q, ld32(ws + Y_OFF + (b0 + 8) * BPS + 4 * q));
-        {
-          const int p = l >> 4, rr = (l >> 1) & 7, dd = l & 1;
-          st32(fw + (p ? kFwV : kFwU) + (rr + 4) * FWC + 4 + 4 * dd, ld32(ws + (p ? V_OFF : U_OFF) + rr * BPS + 4 * dd));
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const int l = m + 16 * s, b0 = l >> 2;
+          st32(fw + kFwY + (b0 + 4) * FWY + 4 + 4 * q, ld32(ws + Y_OFF + b0 * BPS + 4 * q));
+          st32(fw + kFwY + (b0 + 12) * FWY + 4 + 4 * q, ld32(ws + Y_OFF + (b0 + 8) * BPS + 4 * q));
+          const int rr = (l >> 1) & 7, dd = l & 1;
+          st32(fw + (s ? kFwV : kFwU) + (rr + 4) * FWC + 4 + 4 * dd,
+               ld32(ws + (s ? V_OFF : U_OFF) + rr * BPS + 4 * dd));
         }
         if (y > 0) {
-          if (l < 16) {
-            st32(fw + kFwY + (l >> 2) * FWY + 4 + 4 * (l & 3), ld32(col + 32 + 4 * l));
-          } else {
-            const int kk = l - 16, p = kk >> 3, rr = (kk >> 1) & 3, dd = kk & 1;
-            st32(fw + (p ? kFwV : kFwU) + rr * FWC + 4 + 4 * dd, ld32(col + 96 + 32 * p + 8 * rr + 4 * dd));
-          }
+          st32(fw + kFwY + (m >> 2) * FWY + 4 + 4 * (m & 3), ld32(col + 32 + 4 * m));
+          const int p = m >> 3, rr = (m >> 1) & 3, dd = m & 1;
+          st32(fw + (p ? kFwV : kFwU) + rr * FWC + 4 + 4 * dd, ld32(col + 96 + 32 * p + 8 * rr + 4 * dd));
         }
       }
       lds_sync();
@@ -786,51 +815,52 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
         const bool on = act && limit > 0;
         if (ftype > 0 && __any(on)) {
           const int ilevel = (fi >> 8) & 0xff, inner = (fi >> 16) & 0xff, hev_t = (fi >> 24) & 0xff;
-          if (ftype == 2) filter_mb<true>(fw, l, on, x > 0, y > 0, inner != 0, limit, ilevel, hev_t);
-          else filter_mb<false>(fw, l, on, x > 0, y > 0, inner != 0, limit, ilevel, hev_t);
+          if (ftype == 2) filter_mb<true>(fw, m, on, x > 0, y > 0, inner != 0, limit, ilevel, hev_t);
+          else filter_mb<false>(fw, m, on, x > 0, y > 0, inner != 0, limit, ilevel, hev_t);
         }
       }
 
       K1_SECT(9);
-      if (act) {
-        // ---- deposit final bottom rows of this MB column (and the left neighbour's
-        //      cols 12..15 / 4..7, final now) for the row below's top-edge filter
-        if (!last_row) {
-          if (l < 16) {
-            const int rr = l >> 2, d = l & 3;
-            const uint8_t* src = fw + kFwY + (rr + 16) * FWY;
-            if (d == 0) {
-              if (x > 0) st32(col - kColBytes + 32 + rr * 16 + 12, ld32(src));
-              if (last_x) st32(col + 32 + rr * 16 + 12, ld32(src + 16));
-            } else {
-              st32(col + 32 + rr * 16 + 4 * (d - 1), ld32(src + 4 * d));
-            }
+      // ---- deposit final bottom rows of this MB column (and the left neighbour's cols 12..15
+      //      / 4..7, final now) for the row below's top-edge filter: luma role m, chroma m+16
+      if (act && !last_row) {
+        {
+          const int rr = m >> 2, d = m & 3;
+          const uint8_t* src = fw + kFwY + (rr + 16) * FWY;
+          if (d == 0) {
+            if (x > 0) st32(col - kColBytes + 32 + rr * 16 + 12, ld32(src));
+            if (last_x) st32(col + 32 + rr * 16 + 12, ld32(src + 16));
           } else {
-            const int kk = l - 16, p = kk >> 3, rr = (kk >> 1) & 3, d = kk & 1;
-            const uint8_t* src = fw + (p ? kFwV : kFwU) + (rr + 8) * FWC;
-            const ColPtr cb0 = col + 96 + 32 * p + 8 * rr;
-            if (d == 0) {
-              if (x > 0) st32(cb0 - kColBytes + 4, ld32(src));
-              if (last_x) st32(cb0 + 4, ld32(src + 8));
-            } else {
-              st32(cb0, ld32(src + 4));
-            }
+            st32(col + 32 + rr * 16 + 4 * (d - 1), ld32(src + 4 * d));
+          }
+        }
+        {
+          const int p = m >> 3, rr = (m >> 1) & 3, d = m & 1;
+          const uint8_t* src = fw + (p ? kFwV : kFwU) + (rr + 8) * FWC;
+          const ColPtr cb0 = col + 96 + 32 * p + 8 * rr;
+          if (d == 0) {
+            if (x > 0) st32(cb0 - kColBytes + 4, ld32(src));
+            if (last_x) st32(cb0 + 4, ld32(src + 8));
+          } else {
+            st32(cb0, ld32(src + 4));
           }
         }
       }
       K1_SECT(10);
-      // ---- final pixels to HBM (each byte written once).  Five dword slots per lane, all
+      // ---- final pixels to HBM (each byte written once).  Five dword slots per role, all
       //      buffer stores against one descriptor spanning the frame's Y|U|V planes; an idle
       //      slot gets an out-of-range offset and the hardware bounds check drops it, so the
       //      section is branch-free and its LDS reads issue back to back.
-      {
-        const bool cl = l >= 16;  // chroma lane (slots C, E by plane)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int l = m + 16 * s, b0 = l >> 2;
+        const bool cl = s == 1;  // chroma role (slots C, E by plane)
         const int pl = (l >> 3) & 1;
         const uint8_t* cwin = fw + (pl ? kFwV : kFwU);
-        const int ep = l >> 4, er = (l >> 1) & 7, ed = l & 1;      // slot E
-        const uint8_t* ewin = fw + (ep ? kFwV : kFwU);
-        // slot B: lanes 0..11 luma rows -3..-1 of the MB above (cols 0..15),
-        //         lanes 12..23 chroma rows -3..-1 (cols 0..7), U then V
+        const int er = (l >> 1) & 7, ed = l & 1;  // slot E
+        const uint8_t* ewin = fw + (s ? kFwV : kFwU);
+        // slot B: roles 0..11 luma rows -3..-1 of the MB above (cols 0..15),
+        //         roles 12..23 chroma rows -3..-1 (cols 0..7), U then V
         const int bk = l - 12, bp = bk >= 6, brem = bk - 6 * bp;
         const int brr = l < 12 ? (l >> 2) - 3 : (brem >> 1) - 3;
         const int bd = l < 12 ? (l & 3) : (brem & 1);
@@ -843,11 +873,12 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
         const uint32_t vE = ld32(ewin + (er + 4) * FWC + 4 * ed);
         const uint32_t ux = (uint32_t)x;
         const bool aok = act && (q > 0 || x > 0);
-        const uint32_t oA0 = aok ? sbA0 + (ux << 4) : kDrop;
-        const uint32_t oA1 = aok ? sbA1 + (ux << 4) : kDrop;
-        const uint32_t oB = act ? sbB + (ux << shB) : kDrop;
-        const uint32_t oC = act && last_x ? sbC + (ux << shC) : kDrop;
-        const uint32_t oE = act && (ed > 0 || x > 0) ? sbE + (ux << 3) : kDrop;
+        const int shB = l < 12 ? 4 : 3, shC = cl ? 3 : 4;
+        const uint32_t oA0 = aok ? sbA0[s] + (ux << 4) : kDrop;
+        const uint32_t oA1 = aok ? sbA1[s] + (ux << 4) : kDrop;
+        const uint32_t oB = act ? sbB[s] + (ux << shB) : kDrop;
+        const uint32_t oC = act && last_x ? sbC[s] + (ux << shC) : kDrop;
+        const uint32_t oE = act && (ed > 0 || x > 0) ? sbE[s] + (ux << 3) : kDrop;
         __builtin_amdgcn_raw_buffer_store_b32(vA0, planes, (int)oA0, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b32(vA1, planes, (int)oA1, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b32(vB, planes, (int)oB, 0, 0);
@@ -859,30 +890,31 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
       K1_SECT(11);
       // ---- rotate for the next MB (frame_dec.c.go:106-114) + the filter window: cols 12..15
       //      (chroma 4..7) become cols -4..-1 for rows 0..15 (0..7); row -1 is not needed
-      //      (its col -1 comes from the top-left carry).  Pass 0: workspace + left[],
-      //      pass 1: filter window; lanes 0..15 luma rows, 16..31 chroma rows.
+      //      (its col -1 comes from the top-left carry).  Role m: luma row m; role m+16:
+      //      chroma row m&7 (U for m < 8, else V).
       if (act) {
-        const bool ly = l < 16;
-        const int cp = (l >> 3) & 1, cr = l & 7;
-        {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const int l = m + 16 * s;
+          const bool ly = s == 0;
+          const int cp = (l >> 3) & 1, cr = l & 7;
           uint8_t* src = ly ? ws + Y_OFF + l * BPS + 12 : ws + (cp ? V_OFF : U_OFF) + cr * BPS + 4;
           const uint32_t v = ld32(src);
           st32(src - (ly ? 16 : 8), v);
           left[l] = (uint8_t)(v >> 24);
-        }
-        {
-          uint8_t* src = ly ? fw + kFwY + (l + 4) * FWY + 16 : fw + (cp ? kFwV : kFwU) + (cr + 4) * FWC + 8;
-          st32(src - (ly ? 16 : 8), ld32(src));
+          uint8_t* src2 = ly ? fw + kFwY + (l + 4) * FWY + 16 : fw + (cp ? kFwV : kFwU) + (cr + 4) * FWC + 8;
+          st32(src2 - (ly ? 16 : 8), ld32(src2));
         }
       }
       lds_sync();
-      if (lane == 32 && has_odd && x >= 0)
+      if (lane == 16 * (kRows - 1) && has_next && x >= 0)
         __hip_atomic_store(progress + (k & (kWaves - 1)), ((uint32_t)k << 16) | (uint32_t)(x + 1), __ATOMIC_RELEASE,
                            __HIP_MEMORY_SCOPE_WORKGROUP);
       K1_SECT(12);
       rc = rn;
       rn = rnn;
-      cc = cn;
+      cc[0] = cn[0];
+      cc[1] = cn[1];
       blk = blk_next;
     }
   }
@@ -920,20 +952,20 @@ extern "C" int wg_debug_k1_timeline(unsigned long long* out, int n_frames) {
 #endif
 
 size_t vp8_recon_lds_bytes(int mb_w) {
-  return (size_t)kHdrBytes + (size_t)2 * kWaves * kSlotBytes + (size_t)mb_w * kColBytes;
+  return (size_t)kHdrBytes + (size_t)kMaxRecon * kRows * kSlotBytes + (size_t)mb_w * kColBytes;
 }
 
-int vp8_recon_max_mb_w() { return (int)((163840 - kHdrBytes - 2 * kWaves * kSlotBytes) / kColBytes); }
+int vp8_recon_max_mb_w() { return (int)((163840 - kHdrBytes - kMaxRecon * kRows * kSlotBytes) / kColBytes); }
 
 hipError_t launch_vp8_recon_filter(const FrameDesc* d_frames, int n_frames, int max_mb_w, bool lds_frames,
                                    bool wide_frames, int* d_err, hipStream_t stream) {
-  // WG_K1_LEAD overrides the inter-pair lead (tuning experiments only).
+  // WG_K1_LEAD overrides the inter-quad lead (tuning experiments only).
   static const int lead = [] {
     const char* e = getenv("WG_K1_LEAD");
     return e ? atoi(e) : 0;
   }();
-  // WG_K1_RECON_WAVES: waves per frame that reconstruct when K1 emits RGBA (the rest convert
-  // finished bands from the start); 0 / unset = by frame height (see the kernel).
+  // WG_K1_RECON_WAVES: waves per frame that reconstruct (at most 12; with the RGBA tail the
+  // rest convert finished bands from the start); 0 / unset = 12.
   static const int recon_waves = [] {
     const char* e = getenv("WG_K1_RECON_WAVES");
     return e ? atoi(e) : 0;

@@ -23,7 +23,7 @@ for f in glob.glob(f"gpurun_out/ab/prof_{v}/**/*counter_collection.csv", recursi
         if "recon" in r["Kernel_Name"]:
             acc[r["Counter_Name"]].append(float(r["Counter_Value"]))
 c = {k: sum(x) / len(x) for k, x in acc.items()}
-print(f"{v:12s} K1 {j['kernel_ms']['vp8_recon_filter_kernel']:7.3f} ms  K2 {j['kernel_ms']['yuv_to_rgba_kernel']:6.3f} ms  "
+print(f"{v:12s} K1 {j['kernel_ms']['vp8_recon_filter_kernel']:7.3f} ms  K2 {j['kernel_ms'].get('yuv_to_rgba_kernel', 0):6.3f} ms  "
       f"VALU {c.get('SQ_INSTS_VALU', 0):.3e}  SALU {c.get('SQ_INSTS_SALU', 0):.3e}  LDS {c.get('SQ_INSTS_LDS', 0):.3e}  "
       f"value {j['value']}")
 PY
