@@ -10,6 +10,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <climits>
+#include <new>
 #include <cstring>
 #include <mutex>
 #include <thread>
@@ -78,39 +80,130 @@ bool ll_two_pass(const wg::VP8LFrame& f) {
   return cores > 1;
 }
 
-int parse_one(const uint8_t* data, size_t size, int flags, FrameParse* fp) {
+// Allocation failure anywhere in the host stages (vectors sized by the bitstream) is
+// reported as WebPDecode does, never thrown across the C ABI or out of a parse thread.
+template <class F>
+int guarded(F&& f) {
+  try {
+    return f();
+  } catch (const std::bad_alloc&) {
+    return WG_STATUS_OUT_OF_MEMORY;
+  }
+}
+
+constexpr int kFilterExtraRows[3] = {0, 2, 8};  // frame_dec.c.go (VP8EnterCritical)
+
+// Output options (WebPIoInitFromOptions / WebPAllocateDecBuffer, webp.go): colorspace,
+// scaling (disabled in the reference, io_dec.c.go:540-541), cropping (WebPCheckCropDimensions
+// -> INVALID_PARAM).  Sets the frame's output window.
+int apply_output_options(const wg_decoder_options& opt, FrameParse* f) {
+  if (!wg::output_bpp(opt.colorspace))
+    return (opt.colorspace == 11 || opt.colorspace == 12) ? WG_STATUS_UNSUPPORTED_FEATURE : WG_STATUS_INVALID_PARAM;
+  if (opt.use_scaling) return WG_STATUS_UNSUPPORTED_FEATURE;
+  f->out_w = f->width;
+  f->out_h = f->height;
+  if (opt.use_cropping) {
+    // WebPAllocateDecBuffer checks the window with its origin snapped to even
+    // (buffer_dec.c.go:201-209); the decoder's window (WebPIoInitFromOptions, webp.go:922-945)
+    // snaps only for YUV sources: lossy frames use the snapped origin, lossless the exact one
+    const int cw = opt.crop_width, ch = opt.crop_height;
+    auto inside = [&](int x, int y) {
+      return x >= 0 && y >= 0 && cw > 0 && ch > 0 && x < f->width && y < f->height && cw <= f->width - x &&
+             ch <= f->height - y;
+    };
+    const int x = f->lossless ? opt.crop_left : (opt.crop_left & ~1);
+    const int y = f->lossless ? opt.crop_top : (opt.crop_top & ~1);
+    if (!inside(opt.crop_left & ~1, opt.crop_top & ~1) || !inside(x, y)) return WG_STATUS_INVALID_PARAM;
+    f->cropped = x != 0 || y != 0 || cw != f->width || ch != f->height;
+    f->out_w = cw;
+    f->out_h = ch;
+    f->win_x = f->lossless ? x : 0;  // lossy: K2 writes the window itself
+    f->win_y = f->lossless ? y : 0;
+  }
+  f->rgba_w = f->lossless ? f->width : f->out_w;
+  f->rgba_h = f->lossless ? f->height : f->out_h;
+  return WG_STATUS_OK;
+}
+
+// The MB row at whose FinishRow libwebp's lazy alpha decode fails, INT_MAX if never.
+// FinishRow(m) (frame_dec.c.go) requests alpha rows [y_start, y_end): 16m minus the filter
+// delay, the last parsed row (m = rows - 1) through its bottom, clamped to the crop bottom;
+// the first request runs ALPHInit (header + lossless stream header), pre-processed
+// (quantized) alpha is decoded whole at that first request (VP8DecompressAlphaRows).  A
+// lossless pixel failure is hit once the requested rows reach it.
+int alpha_fail_row(int rows, int extra, int bottom, bool init_fails, size_t fail_pixel, int coded_width,
+                   bool whole_plane) {
+  for (int m = 0; m < rows; ++m) {
+    const int y_start = m ? 16 * m - extra : 0;
+    const int y_end = std::min(m == rows - 1 ? 16 * (m + 1) : 16 * (m + 1) - extra, bottom);
+    if (y_start >= y_end) continue;
+    if (init_fails) return m;
+    const uint64_t last = (uint64_t)(whole_plane ? bottom : y_end);
+    if (last * (uint64_t)coded_width > (uint64_t)fail_pixel) return m;
+    if (whole_plane) break;
+  }
+  return INT_MAX;
+}
+
+// One frame's host stages and its WebPDecode status, in DecodeInto's order (webp.go:483-556):
+// container, bitstream headers, output options, then the image data -- bounded, like
+// libwebp's, to the rows a crop window needs, with a lossy frame's ALPH data decoded
+// lazily per MB row (its failure wins over a token failure further down).
+int parse_one(const uint8_t* data, size_t size, const wg_decoder_options& opt, FrameParse* fp) {
   wg::Container c;
   wg_features feat{};
-  int st = wg::parse_container(data, size, &c, &feat);
+  // WebPDecode first runs GetFeatures; its NOT_ENOUGH_DATA is "treated as error"
+  int st = wg::parse_container(data, size, &c, &feat, /*have_all_data=*/false);
+  if (st != WG_STATUS_OK) return st == WG_STATUS_NOT_ENOUGH_DATA ? WG_STATUS_BITSTREAM_ERROR : st;
+  st = wg::parse_container(data, size, &c, &feat);  // DecodeInto's WebPParseHeaders
   if (st != WG_STATUS_OK) return st;
   if (c.is_lossless) {  // VP8L: host entropy stage, K3 on device
     fp->lossless = true;
     st = wg::vp8l_parse(data + c.payload_off, c.payload_size, &fp->lf);
-    if (st != WG_STATUS_OK) return st;
+    if (st != WG_STATUS_OK && fp->lf.fail_pixel == SIZE_MAX) return st;  // VP8LDecodeHeader
     fp->width = fp->lf.width;
     fp->height = fp->lf.height;
+    const int ost = apply_output_options(opt, fp);
+    if (ost != WG_STATUS_OK) return ost;
+    if (st != WG_STATUS_OK) {  // DecodeImageData stops at the crop bottom (io->crop_bottom)
+      const int bottom = opt.use_cropping ? opt.crop_top + opt.crop_height : fp->height;
+      if ((uint64_t)bottom * (uint64_t)fp->lf.coded_width > (uint64_t)fp->lf.fail_pixel) return st;
+    }
     return WG_STATUS_OK;
   }
-  st = wg::vp8_parse(data, size, flags, nullptr, nullptr, &fp->sf);
-  if (st != WG_STATUS_OK) return st;
+  const int flags = opt.bypass_filtering ? WG_FLAG_BYPASS_FILTERING : 0;
+  const int crop_bottom = opt.use_cropping ? (opt.crop_top & ~1) + opt.crop_height : -1;
+  st = wg::vp8_parse(data, size, flags, nullptr, nullptr, &fp->sf, crop_bottom);
+  if (st != WG_STATUS_OK && fp->sf.fail_row < 0) return st;  // VP8GetHeaders
   fp->width = fp->sf.info.width;
   fp->height = fp->sf.info.height;
+  const int ost = apply_output_options(opt, fp);
+  if (ost != WG_STATUS_OK) return ost;
   if (c.alpha_size > 0) {  // ALPH (VP8DecompressAlphaRows, alpha_dec.go:164-213)
     const uint8_t* ad = data + c.alpha_off;
     fp->alpha = true;
-    if (!wg::parse_alpha_header(ad, c.alpha_size, fp->width, fp->height, &fp->ah))
-      return WG_STATUS_OUT_OF_MEMORY;  // ALPHInit failure without a VP8L decoder
-    if (fp->ah.method == 1) {
-      st = wg::vp8l_parse_alpha(ad + 1, c.alpha_size - 1, fp->width, fp->height, &fp->af);
-      if (st != WG_STATUS_OK) return st;
+    int ast = WG_STATUS_OK;
+    bool init_fails = false;
+    if (!wg::parse_alpha_header(ad, c.alpha_size, fp->width, fp->height, &fp->ah)) {
+      ast = WG_STATUS_OUT_OF_MEMORY;  // ALPHInit failure without a VP8L decoder
+      init_fails = true;
+    } else if (fp->ah.method == 1) {
+      ast = wg::vp8l_parse_alpha(ad + 1, c.alpha_size - 1, fp->width, fp->height, &fp->af);
+      init_fails = ast == WG_STATUS_OUT_OF_MEMORY;
     } else {
       fp->alpha_raw = ad + 1;
     }
+    if (ast != WG_STATUS_OK) {
+      const int bottom = crop_bottom >= 0 ? crop_bottom : fp->height;
+      const int arow = alpha_fail_row(fp->sf.br_mb_y, kFilterExtraRows[fp->sf.info.filter_type], bottom, init_fails,
+                                      fp->af.fail_pixel, fp->af.coded_width, fp->ah.pre_processing == 1);
+      if (arow < (st != WG_STATUS_OK ? fp->sf.fail_row : INT_MAX)) return ast;
+    }
   }
-  return WG_STATUS_OK;
+  return st;
 }
 
-void parse_all(const uint8_t* const* data, const size_t* sizes, int n, int flags, int threads,
+void parse_all(const uint8_t* const* data, const size_t* sizes, int n, const wg_decoder_options& opt, int threads,
                std::vector<FrameParse>& out) {
   out.resize(n);
   std::atomic<int> next{0};
@@ -122,7 +215,8 @@ void parse_all(const uint8_t* const* data, const size_t* sizes, int n, int flags
         out[i].status = WG_STATUS_INVALID_PARAM;
         continue;
       }
-      out[i].status = parse_one(data[i], sizes[i], flags, &out[i]);
+      out[i].status = guarded([&] { return parse_one(data[i], sizes[i], opt, &out[i]); });
+      if (out[i].status != WG_STATUS_OK) out[i] = FrameParse{out[i].status};  // drop partial host data
     }
   };
   const int t = std::max(1, std::min(threads, n));
@@ -197,15 +291,23 @@ int wg_get_features(const uint8_t* data, size_t size, wg_features* out) {
   if (out == nullptr) return WG_STATUS_INVALID_PARAM;
   std::memset(out, 0, sizeof(*out));
   wg::Container c;
-  const int st = wg::parse_container(data, size, &c, out);
-  // animated files: WebPGetFeatures reports the VP8X features with OK
-  if (st == WG_STATUS_UNSUPPORTED_FEATURE && c.has_animation) return WG_STATUS_OK;
-  return st;
+  return wg::parse_container(data, size, &c, out, /*have_all_data=*/false);
 }
 
 int wg_vp8_parse(const uint8_t* data, size_t size, int flags, wg_vp8_info* info, wg_vp8_mb* mbs) {
   if (data == nullptr) return WG_STATUS_INVALID_PARAM;
-  return wg::vp8_parse(data, size, flags, info, mbs, nullptr);
+  return guarded([&] { return wg::vp8_parse(data, size, flags, info, mbs, nullptr); });
+}
+
+int wg_decode_status(const uint8_t* data, size_t size, const wg_decoder_options* opt) {
+  if (data == nullptr) return WG_STATUS_INVALID_PARAM;
+  wg_decoder_options o{};
+  o.colorspace = 1;  // MODE_RGBA
+  if (opt) o = *opt;
+  return guarded([&] {
+    FrameParse fp;
+    return parse_one(data, size, o, &fp);
+  });
 }
 
 int wg_vp8l_parse(const uint8_t* data, size_t size, wg_vp8l_info* info, uint32_t* argb,
@@ -216,11 +318,13 @@ int wg_vp8l_parse(const uint8_t* data, size_t size, wg_vp8l_info* info, uint32_t
   int st = wg::parse_container(data, size, &c, &feat);
   if (st != WG_STATUS_OK) return st;
   if (!c.is_lossless) return WG_STATUS_UNSUPPORTED_FEATURE;
-  wg::VP8LFrame f;
-  st = wg::vp8l_parse(data + c.payload_off, c.payload_size, &f);
-  if (st != WG_STATUS_OK) return st;
-  fill_vp8l_info(f, info, argb, transform_data);
-  return WG_STATUS_OK;
+  return guarded([&] {
+    wg::VP8LFrame f;
+    const int st2 = wg::vp8l_parse(data + c.payload_off, c.payload_size, &f);
+    if (st2 != WG_STATUS_OK) return st2;
+    fill_vp8l_info(f, info, argb, transform_data);
+    return (int)WG_STATUS_OK;
+  });
 }
 
 int wg_alpha_parse(const uint8_t* data, size_t size, wg_alpha_info* info, uint8_t* filtered,
@@ -248,11 +352,13 @@ int wg_alpha_parse(const uint8_t* data, size_t size, wg_alpha_info* info, uint8_
     if (filtered) std::memcpy(filtered, ad + 1, (size_t)c.width * c.height);
     return WG_STATUS_OK;
   }
-  wg::VP8LFrame f;
-  st = wg::vp8l_parse_alpha(ad + 1, c.alpha_size - 1, c.width, c.height, &f);
-  if (st != WG_STATUS_OK) return st;
-  if (ll_info) fill_vp8l_info(f, ll_info, argb, transform_data);
-  return WG_STATUS_OK;
+  return guarded([&] {
+    wg::VP8LFrame f;
+    const int st2 = wg::vp8l_parse_alpha(ad + 1, c.alpha_size - 1, c.width, c.height, &f);
+    if (st2 != WG_STATUS_OK) return st2;
+    if (ll_info) fill_vp8l_info(f, ll_info, argb, transform_data);
+    return (int)WG_STATUS_OK;
+  });
 }
 
 }  // extern "C"
@@ -276,6 +382,11 @@ void fill_vp8l_info(const wg::VP8LFrame& f, wg_vp8l_info* info, uint32_t* argb, 
   if (argb) std::memcpy(argb, f.argb.data(), f.argb.size() * 4);
 }
 }  // namespace
+
+namespace {
+wg_batch* batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t* sizes, int n,
+                       const wg_decoder_options* opt, int32_t* status);
+}
 
 extern "C" {
 
@@ -332,6 +443,23 @@ int wg_output_bpp(int colorspace) { return wg::output_bpp(colorspace); }
 wg_batch* wg_batch_create_ex(wg_ctx* ctx, const uint8_t* const* data, const size_t* sizes, int n,
                              const wg_decoder_options* opt, int32_t* status) {
   if (!ctx || !data || !sizes || n <= 0 || !opt) return nullptr;
+  try {
+    return batch_create(ctx, data, sizes, n, opt, status);
+  } catch (const std::bad_alloc&) {  // host-side layout / descriptor vectors
+    if (status)
+      for (int i = 0; i < n; ++i)
+        if (status[i] == WG_STATUS_OK) status[i] = WG_STATUS_OUT_OF_MEMORY;
+    return nullptr;
+  }
+}
+
+}  // extern "C"
+
+namespace {
+wg_batch* batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t* sizes, int n,
+                       const wg_decoder_options* opt, int32_t* status) {
+  if (status)
+    for (int i = 0; i < n; ++i) status[i] = WG_STATUS_OK;
   std::lock_guard<std::mutex> lock(ctx->mu);
   if (hipSetDevice(ctx->device) != hipSuccess) return nullptr;
   wg_batch* b = new wg_batch();
@@ -341,54 +469,7 @@ wg_batch* wg_batch_create_ex(wg_ctx* ctx, const uint8_t* const* data, const size
   const int32_t flags = (opt->bypass_filtering ? WG_FLAG_BYPASS_FILTERING : 0) |
                         (opt->no_fancy_upsampling ? WG_FLAG_NO_FANCY_UPSAMPLING : 0);
   b->flags = flags;
-  parse_all(data, sizes, n, flags, ctx->host_threads, b->fp);
-  // output options (WebPIoInitFromOptions / WebPAllocateDecBuffer, webp.go): colorspace,
-  // scaling (disabled in the reference, io_dec.c.go:540-541), cropping (left/top snapped to
-  // even, WebPCheckCropDimensions -> INVALID_PARAM)
-  const int mode_status = wg::output_bpp(opt->colorspace) ? WG_STATUS_OK
-                          : (opt->colorspace == 11 || opt->colorspace == 12) ? WG_STATUS_UNSUPPORTED_FEATURE
-                                                                              : WG_STATUS_INVALID_PARAM;
-  for (int i = 0; i < n; ++i) {
-    FrameParse& f = b->fp[i];
-    if (f.status != WG_STATUS_OK) continue;
-    if (mode_status != WG_STATUS_OK) {
-      f.status = mode_status;
-      continue;
-    }
-    if (opt->use_scaling) {
-      f.status = WG_STATUS_UNSUPPORTED_FEATURE;
-      continue;
-    }
-    f.out_w = f.width;
-    f.out_h = f.height;
-    if (opt->use_cropping) {
-      // WebPAllocateDecBuffer checks the window with its origin snapped to even
-      // (buffer_dec.c.go:201-209); the decoder's window (WebPIoInitFromOptions, webp.go:922-945)
-      // snaps only for YUV sources: lossy frames use the snapped origin, lossless the exact one
-      const int cw = opt->crop_width, ch = opt->crop_height;
-      auto inside = [&](int x, int y) {
-        return x >= 0 && y >= 0 && cw > 0 && ch > 0 && x < f.width && y < f.height && cw <= f.width - x &&
-               ch <= f.height - y;
-      };
-      const int x = f.lossless ? opt->crop_left : (opt->crop_left & ~1);
-      const int y = f.lossless ? opt->crop_top : (opt->crop_top & ~1);
-      if (!inside(opt->crop_left & ~1, opt->crop_top & ~1) || !inside(x, y)) {
-        f.status = WG_STATUS_INVALID_PARAM;
-        continue;
-      }
-      f.cropped = x != 0 || y != 0 || cw != f.width || ch != f.height;
-      f.out_w = cw;
-      f.out_h = ch;
-      if (!f.lossless) {
-        f.win_x = f.win_y = 0;  // K2 writes the window itself
-      } else {
-        f.win_x = x;
-        f.win_y = y;
-      }
-    }
-    f.rgba_w = f.lossless ? f.width : f.out_w;
-    f.rgba_h = f.lossless ? f.height : f.out_h;
-  }
+  parse_all(data, sizes, n, *opt, ctx->host_threads, b->fp);
   // layout
   size_t in_b = 0, pl_b = 0, rg_b = 0;
   double k1 = 0, k2 = 0, k3 = 0, k4 = 0;
@@ -699,6 +780,9 @@ wg_batch* wg_batch_create_ex(wg_ctx* ctx, const uint8_t* const* data, const size
   if (e != hipSuccess) return fail(WG_STATUS_OUT_OF_MEMORY);
   return b;
 }
+}  // namespace
+
+extern "C" {
 
 int wg_batch_run(wg_batch* b, void* stream) {
   if (!b) return WG_STATUS_INVALID_PARAM;

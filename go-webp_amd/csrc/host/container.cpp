@@ -3,8 +3,10 @@
 // Follows ParseHeadersInternal and its helpers in the reference
 // (pkg/libwebp/decoder/webp.go: ParseRIFF :85-120, ParseVP8X :122-175,
 // ParseOptionalChunks :177-237, ParseVP8Header :247-295, ParseHeadersInternal
-// :300-440) with have_all_data = 1 (the batch API always has whole files), plus
-// VP8GetInfo (pkg/vp8/vp8_dec.go:189-228) and VP8LGetInfo for the frame size.
+// :300-440), plus VP8GetInfo (pkg/vp8/vp8_dec.go:189-228) and VP8LGetInfo for the frame
+// size.  have_all_data = 1 is DecodeInto's pass (whole files: a chunk running past the end
+// is NOT_ENOUGH_DATA); have_all_data = 0 is WebPGetFeatures' (headers == NULL: truncated
+// chunks pass, and a VP8X file short of its image header still reports its features).
 #include <cstring>
 
 #include "host.h"
@@ -58,7 +60,7 @@ bool vp8l_get_info(const uint8_t* d, size_t size, int* w, int* h, int* a) {
 
 }  // namespace
 
-int parse_container(const uint8_t* data, size_t data_size, Container* c, wg_features* feat) {
+int parse_container(const uint8_t* data, size_t data_size, Container* c, wg_features* feat, bool have_all_data) {
   *c = Container{};
   if (data == nullptr || data_size < kRiffHdr) return WG_STATUS_NOT_ENOUGH_DATA;
   const uint8_t* p = data;
@@ -70,7 +72,7 @@ int parse_container(const uint8_t* data, size_t data_size, Container* c, wg_feat
     const uint32_t size = le32(p + kTag);
     if (size < kTag + kChunkHdr) return WG_STATUS_BITSTREAM_ERROR;
     if (size > kMaxChunkPayload) return WG_STATUS_BITSTREAM_ERROR;
-    if (size > left - kChunkHdr) return WG_STATUS_NOT_ENOUGH_DATA;
+    if (have_all_data && size > left - kChunkHdr) return WG_STATUS_NOT_ENOUGH_DATA;
     riff_size = size;
     p += kRiffHdr;
     left -= kRiffHdr;
@@ -97,6 +99,10 @@ int parse_container(const uint8_t* data, size_t data_size, Container* c, wg_feat
   c->has_animation = !!(vflags & kAnimFlag);
   int image_w = canvas_w, image_h = canvas_h;
   auto finish = [&](int status) {
+    // ParseHeadersInternal's ReturnWidthHeight: GetFeatures on a VP8X file short of data
+    // still succeeds with the canvas size
+    if (status == WG_STATUS_NOT_ENOUGH_DATA && found_vp8x && !have_all_data) status = WG_STATUS_OK;
+    if (status != WG_STATUS_OK) return status;
     if (feat) {
       feat->width = image_w;
       feat->height = image_h;
@@ -111,21 +117,21 @@ int parse_container(const uint8_t* data, size_t data_size, Container* c, wg_feat
   if (found_vp8x && c->has_animation) {
     // WebPDecode does not decode animations; features come from VP8X only.
     finish(WG_STATUS_OK);
-    return WG_STATUS_UNSUPPORTED_FEATURE;
+    return have_all_data ? WG_STATUS_UNSUPPORTED_FEATURE : WG_STATUS_OK;
   }
-  if (left < kTag) return WG_STATUS_NOT_ENOUGH_DATA;
+  if (left < kTag) return finish(WG_STATUS_NOT_ENOUGH_DATA);
   // ParseOptionalChunks
   if ((found_riff && found_vp8x) || (!found_riff && !found_vp8x && tag_is(p, "ALPH"))) {
     uint64_t total = kTag + kChunkHdr + kVp8xChunk;
     for (;;) {
-      if (left < kChunkHdr) return WG_STATUS_NOT_ENOUGH_DATA;
+      if (left < kChunkHdr) return finish(WG_STATUS_NOT_ENOUGH_DATA);
       const uint32_t csize = le32(p + kTag);
       if (csize > kMaxChunkPayload) return WG_STATUS_BITSTREAM_ERROR;
       const uint64_t disk = (kChunkHdr + (uint64_t)csize + 1) & ~1ull;
       total += disk;
       if (riff_size > 0 && total > riff_size) return WG_STATUS_BITSTREAM_ERROR;
       if (tag_is(p, "VP8 ") || tag_is(p, "VP8L")) break;
-      if (left < disk) return WG_STATUS_NOT_ENOUGH_DATA;
+      if (left < disk) return finish(WG_STATUS_NOT_ENOUGH_DATA);
       if (tag_is(p, "ALPH")) {
         c->alpha_off = (size_t)(p + kChunkHdr - data);
         c->alpha_size = csize;
@@ -135,14 +141,14 @@ int parse_container(const uint8_t* data, size_t data_size, Container* c, wg_feat
     }
   }
   // ParseVP8Header
-  if (left < kChunkHdr) return WG_STATUS_NOT_ENOUGH_DATA;
+  if (left < kChunkHdr) return finish(WG_STATUS_NOT_ENOUGH_DATA);
   const bool is_vp8 = tag_is(p, "VP8 "), is_vp8l = tag_is(p, "VP8L");
   size_t chunk_size;
   if (is_vp8 || is_vp8l) {
     const uint32_t size = le32(p + kTag);
     const uint64_t minimal = kTag + kChunkHdr;
     if (riff_size >= minimal && size > riff_size - minimal) return WG_STATUS_BITSTREAM_ERROR;
-    if (size > left - kChunkHdr) return WG_STATUS_NOT_ENOUGH_DATA;
+    if (have_all_data && size > left - kChunkHdr) return finish(WG_STATUS_NOT_ENOUGH_DATA);
     chunk_size = size;
     p += kChunkHdr;
     left -= kChunkHdr;

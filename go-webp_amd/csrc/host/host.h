@@ -24,7 +24,8 @@ struct Container {
   int is_lossless = 0;
 };
 
-int parse_container(const uint8_t* data, size_t size, Container* c, wg_features* feat);
+// have_all_data: 1 = DecodeInto's header pass, 0 = WebPGetFeatures' (see container.cpp).
+int parse_container(const uint8_t* data, size_t size, Container* c, wg_features* feat, bool have_all_data = true);
 
 // Growable buffer of trivially copyable T without zero-filling on growth (the entropy
 // stage writes every element it keeps).
@@ -59,11 +60,16 @@ struct SparseFrame {
   std::vector<MbRec> mbs;              // mb_w * mb_h, raster order
   std::vector<uint32_t> row_block0;    // first coefficient block of each MB row
   PodBuf<int16_t> blocks;              // 16 int16 per non-zero 4x4 block, column-major
+  int br_mb_y = 0;                     // MB rows parsed (VP8EnterCritical's br_mb_y_)
+  int fail_row = -1;                   // MB row whose parse failed (-1: none, or the headers)
 };
 
 // Entropy-decode one lossy frame.  `dense` (mb_w*mb_h) and/or `sparse` may be null.
+// crop_bottom >= 0 bounds the MB rows parsed as WebPDecode does for a crop window
+// (br_mb_y_ = (crop_bottom + 15 + kFilterExtraRows[filter_type]) >> 4, frame_dec.c.go);
+// rows below it are left zero and a corrupt token stream there is not seen.
 int vp8_parse(const uint8_t* data, size_t size, int flags, wg_vp8_info* info,
-              wg_vp8_mb* dense, SparseFrame* sparse);
+              wg_vp8_mb* dense, SparseFrame* sparse, int crop_bottom = -1);
 
 // VP8L (lossless) after the host entropy stage: the entropy-coded ARGB image and the
 // transforms in bitstream (read) order; the device applies them in reverse.
@@ -81,6 +87,11 @@ struct VP8LFrame {
   int coded_width = 0;                    // width of `argb` (reduced by color-index packing)
   std::vector<VP8LTransform> transforms;  // read order
   std::vector<uint32_t> argb;             // coded_width * height
+  // After a failure in the pixel data: the first coded pixel whose symbol failed (SIZE_MAX:
+  // the failure was in the header, transforms or codes).  A decode bounded to image rows
+  // [0, r) -- a crop window, or the alpha rows requested so far -- fails iff
+  // r * coded_width > fail_pixel.
+  size_t fail_pixel = SIZE_MAX;
 };
 
 // Entropy-decode a VP8L bitstream (the VP8L chunk payload).

@@ -16,7 +16,9 @@
 //   PrecomputeFilterStrengths pkg/libwebp/decoder/frame_dec.c.go:266-315
 // Output: the libwebp MB model (wg_vp8_mb, for the CPU checker) and/or the sparse
 // device layout of device_format.h.
+#include <algorithm>
 #include <cstring>
+#include <memory>
 
 #include "bool_reader.h"
 #include "host.h"
@@ -551,20 +553,21 @@ int get_headers(Decoder* d, const uint8_t* buf, size_t buf_size) {  // vp8_dec.g
 }  // namespace
 
 int vp8_parse(const uint8_t* data, size_t size, int flags, wg_vp8_info* info, wg_vp8_mb* dense,
-              SparseFrame* sparse) {
+              SparseFrame* sparse, int crop_bottom) {
   Container c;
   int st = parse_container(data, size, &c, nullptr);
   if (st != WG_STATUS_OK) return st;
   if (c.is_lossless) return WG_STATUS_UNSUPPORTED_FEATURE;  // VP8L: not this entry point
-  Decoder* d = new Decoder();
+  std::unique_ptr<Decoder> dp(new Decoder());
+  Decoder* d = dp.get();
   st = get_headers(d, data + c.payload_off, c.payload_size);
-  if (st != WG_STATUS_OK) {
-    delete d;
-    return st;
-  }
+  if (st != WG_STATUS_OK) return st;
   if (flags & WG_FLAG_BYPASS_FILTERING) d->filter_type = 0;  // VP8EnterCritical
   precompute_filter_strengths(d);
   const int mb_w = d->mb_w, mb_h = d->mb_h;
+  static const int kFilterExtraRows[3] = {0, 2, 8};  // frame_dec.c.go (VP8EnterCritical)
+  const int br_mb_y =
+      crop_bottom < 0 ? mb_h : std::min(mb_h, (crop_bottom + 15 + kFilterExtraRows[d->filter_type]) >> 4);
   wg_vp8_info inf{};
   inf.width = d->width;
   inf.height = d->height;
@@ -575,10 +578,7 @@ int vp8_parse(const uint8_t* data, size_t size, int flags, wg_vp8_info* info, wg
   inf.use_segment = d->use_segment;
   inf.frame_offset = (int32_t)c.payload_off;
   if (info) *info = inf;
-  if (!dense && !sparse) {
-    delete d;
-    return WG_STATUS_OK;
-  }
+  if (!dense && !sparse) return WG_STATUS_OK;
   // bands_ptr (tree_dec.c.go:127-129)
   const BandProbas* bands_ptr[4][17];
   for (int t = 0; t < 4; ++t)
@@ -597,7 +597,8 @@ int vp8_parse(const uint8_t* data, size_t size, int flags, wg_vp8_info* info, wg
   MBOut blk;
   size_t nblocks = 0;
   st = WG_STATUS_OK;
-  for (int mb_y = 0; mb_y < mb_h && st == WG_STATUS_OK; ++mb_y) {
+  int fail_row = -1;
+  for (int mb_y = 0; mb_y < br_mb_y && st == WG_STATUS_OK; ++mb_y) {
     BoolReader* token_br = &d->parts[mb_y & d->num_parts_minus_one];
     std::memset(intra_l, 0, sizeof(intra_l));  // VP8InitScanline: B_DC_PRED
     left->nz = left->nz_dc = 0;
@@ -633,6 +634,7 @@ int vp8_parse(const uint8_t* data, size_t size, int flags, wg_vp8_info* info, wg
       }
       if (token_br->eof) {
         st = WG_STATUS_NOT_ENOUGH_DATA;  // "Premature end-of-file encountered."
+        fail_row = mb_y;
         break;
       }
       const size_t idx = (size_t)mb_y * mb_w + mb_x;
@@ -677,9 +679,15 @@ int vp8_parse(const uint8_t* data, size_t size, int flags, wg_vp8_info* info, wg
         sparse->mbs[idx] = r;
       }
     }
-    if (st == WG_STATUS_OK && d->br.eof) st = WG_STATUS_NOT_ENOUGH_DATA;  // partition 0 exhausted
+    if (st == WG_STATUS_OK && d->br.eof) {  // partition 0 exhausted
+      st = WG_STATUS_NOT_ENOUGH_DATA;
+      fail_row = mb_y;
+    }
   }
-  delete d;
+  if (sparse) {
+    sparse->br_mb_y = br_mb_y;
+    sparse->fail_row = fail_row;
+  }
   return st;
 }
 

@@ -27,6 +27,8 @@ constexpr int kNumDistanceCodes = 40;
 constexpr int kMaxCodeLength = 15;
 constexpr int kRootBits = 8;
 constexpr int kCodeLengthCodes = 19;
+constexpr int kMaxCacheBits = 11;
+constexpr int kMaxAlphabet = kNumLiteralCodes + kNumLengthCodes + (1 << kMaxCacheBits);
 constexpr uint8_t kCodeLengthCodeOrder[kCodeLengthCodes] = {17, 18, 0, 1, 2, 3, 4, 5, 16, 6,
                                                             7,  8,  9, 10, 11, 12, 13, 14, 15};
 // (dy, 8 - dx) pairs of the 120 short-distance plane codes (VP8L spec, kCodeToPlane).
@@ -105,6 +107,7 @@ class PrefixCode {
   // libwebp's BuildHuffmanTable rejects.  A single used symbol decodes with 0 bits.
   bool build(const int* lengths, int n) {
     table_.assign(1u << kRootBits, 0);
+    single_ = false;
     int count[kMaxCodeLength + 1] = {0};
     int used = 0, last = -1;
     for (int s = 0; s < n; ++s) {
@@ -118,6 +121,7 @@ class PrefixCode {
     if (used == 0) return false;
     if (used == 1) {  // single symbol: 0 bits
       std::fill(table_.begin(), table_.end(), (uint32_t)last);
+      single_ = true;
       return true;
     }
     // completeness (Kraft sum == 1)
@@ -136,17 +140,15 @@ class PrefixCode {
       next[len] = code;
     }
     // second-level sizes: for each root prefix, the longest code under it
-    std::vector<int> sub_max(1u << kRootBits, 0);
-    std::vector<std::pair<uint32_t, int>> syms;  // (reversed code, symbol) with length
-    std::vector<int> lens;
+    int sub_max[1 << kRootBits] = {0};
+    syms_.clear();
     for (int s = 0; s < n; ++s) {
       const int len = lengths[s];
       if (!len) continue;
       const uint32_t c = (uint32_t)next[len]++;
       uint32_t r = 0;
       for (int b = 0; b < len; ++b) r |= ((c >> b) & 1u) << (len - 1 - b);
-      syms.emplace_back(r, s);
-      lens.push_back(len);
+      syms_.push_back(Sym{r, s, len});
       if (len > kRootBits) {
         const uint32_t root = r & ((1u << kRootBits) - 1);
         sub_max[root] = std::max(sub_max[root], len - kRootBits);
@@ -158,10 +160,10 @@ class PrefixCode {
       table_[root] = 0x80000000u | ((uint32_t)sub_max[root] << 16) | off;
       table_.resize(off + (1u << sub_max[root]), 0);
     }
-    for (size_t i = 0; i < syms.size(); ++i) {
-      const uint32_t r = syms[i].first;
-      const int len = lens[i];
-      const uint32_t e = ((uint32_t)len << 16) | (uint32_t)syms[i].second;
+    for (const Sym& sy : syms_) {
+      const uint32_t r = sy.rev;
+      const int len = sy.len;
+      const uint32_t e = ((uint32_t)len << 16) | (uint32_t)sy.sym;
       if (len <= kRootBits) {
         for (uint32_t k = r; k < (1u << kRootBits); k += 1u << len) table_[k] = e;
       } else {
@@ -175,6 +177,8 @@ class PrefixCode {
     }
     return true;
   }
+  // One used symbol (decodes with 0 bits): libwebp's htrees[c][0].bits == 0.
+  bool single() const { return single_; }
   int read(BitReader& br) const {
     const uint32_t bits = br.peek15();
     uint32_t e = table_[bits & ((1u << kRootBits) - 1)];
@@ -187,7 +191,13 @@ class PrefixCode {
   }
 
  private:
+  struct Sym {
+    uint32_t rev;  // code, bit-reversed (LSB-first stream order)
+    int sym, len;
+  };
   std::vector<uint32_t> table_;
+  std::vector<Sym> syms_;  // build() scratch, kept for reuse
+  bool single_ = false;
 };
 
 struct HTreeGroup {
@@ -197,14 +207,23 @@ struct HTreeGroup {
 struct Decoder {
   BitReader br;
   int status = WG_STATUS_OK;
-  explicit Decoder(const uint8_t* p, size_t n) : br(p, n) {}
+  // The headerless ALPH stream: libwebp decodes it with DecodeAlphaData (8-bit path) when
+  // it only has a color-indexing transform and trivial red/blue/alpha codes.
+  bool alpha_stream = false;
+  bool in_main_pixels = false;  // the level-0 pixel loop has started (alpha error mapping)
+  size_t fail_pos = SIZE_MAX;   // main image: first pixel of the symbol that failed
+  std::vector<int> lengths;     // code lengths of the code being read (libwebp's code_lengths)
+  PrefixCode scratch;           // codes of meta groups the image never selects: read, validated, dropped
+  explicit Decoder(const uint8_t* p, size_t n) : br(p, n), lengths(kMaxAlphabet, 0) {}
   bool fail(int st) {
     if (status == WG_STATUS_OK) status = st;
     return false;
   }
-  bool check_eos() { return br.eos() ? fail(WG_STATUS_NOT_ENOUGH_DATA) : true; }
+  // Non-incremental WebPDecode reports every end-of-stream as a bitstream error
+  // (DecodeImageStream / DecodeImageData, vp8l_dec.c.go:1180-1187).
+  bool check_eos() { return br.eos() ? fail(WG_STATUS_BITSTREAM_ERROR) : true; }
 
-  bool read_code_lengths(const int* cl_lengths, int num_symbols, int* lengths) {
+  bool read_code_lengths(const int* cl_lengths, int num_symbols, int* lens) {
     PrefixCode cl;
     if (!cl.build(cl_lengths, kCodeLengthCodes)) return fail(WG_STATUS_BITSTREAM_ERROR);
     int max_symbol = num_symbols;
@@ -216,10 +235,10 @@ struct Decoder {
     int symbol = 0, prev = 8;
     while (symbol < num_symbols) {
       if (max_symbol-- == 0) break;
-      if (br.eos()) return fail(WG_STATUS_NOT_ENOUGH_DATA);
+      if (br.eos()) return fail(WG_STATUS_BITSTREAM_ERROR);
       const int code_len = cl.read(br);
       if (code_len < 16) {
-        lengths[symbol++] = code_len;
+        lens[symbol++] = code_len;
         if (code_len != 0) prev = code_len;
       } else {
         static const int kExtra[3] = {2, 3, 7}, kOffset[3] = {3, 3, 11};
@@ -227,33 +246,35 @@ struct Decoder {
         const int repeat = (int)br.read(kExtra[slot]) + kOffset[slot];
         if (symbol + repeat > num_symbols) return fail(WG_STATUS_BITSTREAM_ERROR);
         const int v = code_len == 16 ? prev : 0;
-        for (int r = 0; r < repeat; ++r) lengths[symbol++] = v;
+        for (int r = 0; r < repeat; ++r) lens[symbol++] = v;
       }
     }
     return check_eos();
   }
 
+  // ReadHuffmanCode (libwebp 1.6.0 vp8l_dec.c; the reference's vp8l_dec.c.go:309-319 for the
+  // simple code).  A simple-code symbol >= alphabet_size lands outside the range the table
+  // is built over, so it is ignored; a code left with no symbol is invalid.
   bool read_code(int alphabet_size, PrefixCode* out) {
-    std::vector<int> lengths((size_t)alphabet_size, 0);
+    int* lens = lengths.data();
+    std::fill(lens, lens + alphabet_size, 0);
     if (br.read(1)) {  // simple code: one or two symbols of length 1
       const int num_symbols = (int)br.read(1) + 1;
       const int first_bits = br.read(1) ? 8 : 1;
       const int s0 = (int)br.read(first_bits);
-      if (s0 >= alphabet_size) return fail(WG_STATUS_BITSTREAM_ERROR);
-      lengths[s0] = 1;
+      if (s0 < alphabet_size) lens[s0] = 1;
       if (num_symbols == 2) {
         const int s1 = (int)br.read(8);
-        if (s1 >= alphabet_size) return fail(WG_STATUS_BITSTREAM_ERROR);
-        lengths[s1] = 1;
+        if (s1 < alphabet_size) lens[s1] = 1;
       }
     } else {
       int cl_lengths[kCodeLengthCodes] = {0};
       const int num_codes = (int)br.read(4) + 4;
       for (int i = 0; i < num_codes; ++i) cl_lengths[kCodeLengthCodeOrder[i]] = (int)br.read(3);
-      if (!read_code_lengths(cl_lengths, alphabet_size, lengths.data())) return false;
+      if (!read_code_lengths(cl_lengths, alphabet_size, lens)) return false;
     }
     if (!check_eos()) return false;
-    if (!out->build(lengths.data(), alphabet_size)) return fail(WG_STATUS_BITSTREAM_ERROR);
+    if (!out->build(lens, alphabet_size)) return fail(WG_STATUS_BITSTREAM_ERROR);
     return true;
   }
 
@@ -270,8 +291,6 @@ struct Decoder {
     const int dist = (dc >> 4) * xsize + (8 - (dc & 0xf));
     return dist >= 1 ? dist : 1;
   }
-
-  bool in_main_pixels = false;  // the level-0 pixel loop has started (alpha error mapping)
 
   // One entropy-coded image (main image when `level0`, else a side image).
   bool decode_stream(int xsize, int ysize, bool level0, VP8LFrame* f, std::vector<uint32_t>* out) {
@@ -318,29 +337,50 @@ struct Decoder {
     int cache_bits = 0;
     if (br.read(1)) {
       cache_bits = (int)br.read(4);
-      if (cache_bits < 1 || cache_bits > 11) return fail(WG_STATUS_BITSTREAM_ERROR);
+      if (cache_bits < 1 || cache_bits > kMaxCacheBits) return fail(WG_STATUS_BITSTREAM_ERROR);
     }
-    // prefix codes (meta codes only on the main image)
+    // prefix codes (meta codes only on the main image).  Tables are built only for the
+    // groups the meta image selects, renumbered densely in order of first use; the codes
+    // of the other group indices are still read and validated (ReadHuffmanCodes' mapping),
+    // so a large index costs parse time, not memory.
     int huff_bits = 0, huff_xsize = 0;
     std::vector<uint32_t> huff_image;
-    int num_groups = 1;
+    int num_groups = 1, num_groups_max = 1;
+    std::vector<int> mapping;  // group index -> dense index, -1 = never selected
     if (level0 && br.read(1)) {
       huff_bits = (int)br.read(3) + 2;
       huff_xsize = div_round_up(xsize, huff_bits);
       if (!decode_stream(huff_xsize, div_round_up(ysize, huff_bits), false, nullptr, &huff_image)) return false;
       for (uint32_t& p : huff_image) {
         p = (p >> 8) & 0xffff;
-        num_groups = std::max(num_groups, (int)p + 1);
+        num_groups_max = std::max(num_groups_max, (int)p + 1);
+      }
+      mapping.assign((size_t)num_groups_max, -1);
+      num_groups = 0;
+      for (uint32_t& p : huff_image) {
+        int& m = mapping[p];
+        if (m < 0) m = num_groups++;
+        p = (uint32_t)m;
       }
     }
     if (!check_eos()) return false;
+    // libwebp itself keeps unused groups unless num_groups_max > 1000 or > the pixel count;
+    // the groups it keeps decide whether its 8-bit alpha path applies (Is8bOptimizable).
+    const bool libwebp_maps =
+        !mapping.empty() && (num_groups_max > 1000 || (int64_t)num_groups_max > (int64_t)xsize * ysize);
     const int cache_size = cache_bits ? 1 << cache_bits : 0;
     std::vector<HTreeGroup> groups((size_t)num_groups);
     const int alphabet[5] = {kNumLiteralCodes + kNumLengthCodes + cache_size, kNumLiteralCodes, kNumLiteralCodes,
                              kNumLiteralCodes, kNumDistanceCodes};
-    for (int g = 0; g < num_groups; ++g)
-      for (int j = 0; j < 5; ++j)
-        if (!read_code(alphabet[j], &groups[(size_t)g].code[j])) return false;
+    bool rba_single = true;  // every kept group's red, blue and alpha codes have one symbol
+    for (int gi = 0; gi < num_groups_max; ++gi) {
+      const int m = mapping.empty() ? gi : mapping[(size_t)gi];
+      for (int j = 0; j < 5; ++j) {
+        PrefixCode* pc = m >= 0 ? &groups[(size_t)m].code[j] : &scratch;
+        if (!read_code(alphabet[j], pc)) return false;
+        if (j >= 1 && j <= 3 && (m >= 0 || !libwebp_maps)) rba_single = rba_single && pc->single();
+      }
+    }
     // pixels
     if (level0) in_main_pixels = true;
     const size_t total = (size_t)xsize * ysize;
@@ -356,17 +396,27 @@ struct Decoder {
     auto insert = [&](uint32_t argb) {
       if (cache_bits) cache[(argb * 0x1e35a7bdu) >> cache_shift] = argb;
     };
+    // The 8-bit alpha path (DecodeAlphaData) checks the end of stream only after storing a
+    // symbol's pixels: a stream that runs out on the symbol completing the image still
+    // decodes.  Everywhere else a symbol that reads past the end fails at its first pixel.
+    const bool late_eos = alpha_stream && level0 && f->transforms.size() == 1 &&
+                          f->transforms[0].type == kVP8LColorIndexing && cache_bits == 0 && rba_single;
+    auto bad = [&](size_t at) {
+      if (level0) fail_pos = at;
+      return fail(WG_STATUS_BITSTREAM_ERROR);
+    };
     size_t pos = 0;
     int x = 0, y = 0;
     const HTreeGroup* hg = &group_at(0, 0);
     while (pos < total) {
+      const size_t start = pos;
       if ((x & mask) == 0) hg = &group_at(x, y);
-      if (br.eos()) return fail(WG_STATUS_NOT_ENOUGH_DATA);
       const int code = hg->code[0].read(br);
       if (code < kNumLiteralCodes) {
         const uint32_t r = (uint32_t)hg->code[1].read(br);
         const uint32_t b = (uint32_t)hg->code[2].read(br);
         const uint32_t a = (uint32_t)hg->code[3].read(br);
+        if (br.eos() && !(late_eos && pos + 1 == total)) return bad(start);
         const uint32_t argb = (a << 24) | (r << 16) | ((uint32_t)code << 8) | b;
         data[pos++] = argb;
         insert(argb);
@@ -378,8 +428,9 @@ struct Decoder {
         const int length = copy_distance(code - kNumLiteralCodes, br);
         const int dist_sym = hg->code[4].read(br);
         const int dist = plane_code_to_distance(xsize, copy_distance(dist_sym, br));
-        if (br.eos()) return fail(WG_STATUS_NOT_ENOUGH_DATA);
-        if ((size_t)dist > pos || total - pos < (size_t)length) return fail(WG_STATUS_BITSTREAM_ERROR);
+        if (br.eos() && !late_eos) return bad(start);
+        if ((size_t)dist > pos || total - pos < (size_t)length) return bad(start);
+        if (br.eos() && pos + (size_t)length < total) return bad(start);
         for (int i = 0; i < length; ++i) {
           const uint32_t argb = data[pos - dist];
           data[pos++] = argb;
@@ -392,8 +443,9 @@ struct Decoder {
         }
         if (pos < total && (x & mask)) hg = &group_at(x, y);
       } else {
+        if (br.eos()) return bad(start);
         const int key = code - (kNumLiteralCodes + kNumLengthCodes);
-        if (key >= cache_size) return fail(WG_STATUS_BITSTREAM_ERROR);
+        if (key >= cache_size) return bad(start);
         const uint32_t argb = cache[(size_t)key];
         data[pos++] = argb;
         insert(argb);
@@ -403,7 +455,7 @@ struct Decoder {
         }
       }
     }
-    return check_eos();
+    return true;
   }
 };
 
@@ -411,6 +463,7 @@ struct Decoder {
 
 int vp8l_parse(const uint8_t* data, size_t size, VP8LFrame* out) {
   if (!data || size < 5 || !out) return WG_STATUS_NOT_ENOUGH_DATA;
+  out->fail_pixel = SIZE_MAX;
   Decoder d(data, size);
   if (d.br.read(8) != 0x2f) return WG_STATUS_BITSTREAM_ERROR;
   out->width = (int)d.br.read(14) + 1;
@@ -419,7 +472,10 @@ int vp8l_parse(const uint8_t* data, size_t size, VP8LFrame* out) {
   if (d.br.read(3) != 0) return WG_STATUS_BITSTREAM_ERROR;
   out->transforms.clear();
   out->coded_width = out->width;
-  if (!d.decode_stream(out->width, out->height, true, out, &out->argb)) return d.status;
+  if (!d.decode_stream(out->width, out->height, true, out, &out->argb)) {
+    out->fail_pixel = d.fail_pos;
+    return d.status;
+  }
   return WG_STATUS_OK;
 }
 
@@ -428,16 +484,22 @@ int vp8l_parse(const uint8_t* data, size_t size, VP8LFrame* out) {
 // Status as WebPDecode reports it: a failure while reading the stream's transforms and
 // codes leaves the alpha decoder without a VP8L decoder, which VP8DecompressAlphaRows
 // reports as OUT_OF_MEMORY (alpha_dec.go:177-182); a failure in the pixel data is
-// "Could not decode alpha data" = BITSTREAM_ERROR.
+// "Could not decode alpha data" = BITSTREAM_ERROR, seen only once the rows it lies in are
+// requested (out->fail_pixel).
 int vp8l_parse_alpha(const uint8_t* data, size_t size, int width, int height, VP8LFrame* out) {
   out->width = width;
   out->height = height;
   out->has_alpha = 0;
   out->transforms.clear();
   out->coded_width = width;
+  out->fail_pixel = SIZE_MAX;
   Decoder d(data, size);
-  if (!d.decode_stream(width, height, true, out, &out->argb))
-    return d.in_main_pixels ? WG_STATUS_BITSTREAM_ERROR : WG_STATUS_OUT_OF_MEMORY;
+  d.alpha_stream = true;
+  if (!d.decode_stream(width, height, true, out, &out->argb)) {
+    if (!d.in_main_pixels) return WG_STATUS_OUT_OF_MEMORY;
+    out->fail_pixel = d.fail_pos;
+    return WG_STATUS_BITSTREAM_ERROR;
+  }
   return WG_STATUS_OK;
 }
 

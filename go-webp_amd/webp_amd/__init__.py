@@ -155,6 +155,7 @@ _SIGS = {
     "wg_batch_download": (C.c_int, [_P, C.c_int, _P, C.c_int]),
     "wg_batch_frame_status": (C.c_int, [_P, C.c_int]),
     "wg_anim_decode": (C.c_int, [_P, _P, C.c_size_t, _P, _P, C.c_int32]),
+    "wg_decode_status": (C.c_int, [_P, C.c_size_t, _P]),
 }
 EXPORTED = tuple(_SIGS)
 
@@ -242,6 +243,12 @@ def decode(data, flags=0):
     if st != Status.OK:
         raise WebPError(st, "wg_decode_rgba_into")
     return out
+
+
+def decode_status(data, opts=None):
+    """WebPDecode's status for `data` under DecoderOptions `opts` (None = RGBA), host only."""
+    b = bytes(data)
+    return lib().wg_decode_status(b, len(b), C.byref(opts) if opts is not None else None)
 
 
 def vp8_parse(data, flags=0, with_mbs=True):

@@ -91,6 +91,12 @@ typedef struct {
 /* Bytes per pixel of a colorspace (3, 4 or 2); 0 if not an RGB-family mode. */
 int wg_output_bpp(int colorspace);
 
+/* The status WebPDecode (webp.go:870-909) returns for this input and options (NULL = RGBA,
+ * no crop), from the host stages alone: container, headers, options, then the entropy-coded
+ * data in libwebp's order (crop-bounded rows, lazily decoded alpha).  Host only, no GPU
+ * needed; the batch entry points report the same per-frame status. */
+int wg_decode_status(const uint8_t* data, size_t size, const wg_decoder_options* opt);
+
 /* Replaces WebPDecode with config.output in external memory (webp.go:870-909): one frame on
  * the GPU (device 0 context) in the options' colorspace / crop window / orientation, rows of
  * `stride` bytes. */

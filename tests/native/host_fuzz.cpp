@@ -2,7 +2,8 @@
 // demux) for tests/test_host_fuzz.py, built with ASan + UBSan: truncations and bit flips
 // of every fixture must return a status, never crash, and successful VP8 parses must
 // satisfy the invariants K1 relies on (record count, row index, one 16-coefficient block
-// per set non-zero bit).
+// per set non-zero bit).  The meta-code amplification fixture (status/crafted_65536_groups)
+// runs here too: it must parse within ASan's default memory.
 #include <cstdio>
 #include <cstdlib>
 #include <fstream>
@@ -40,7 +41,9 @@ int main(int argc, char** argv) {
         wg::vp8l_parse(d.data() + c.payload_off, c.payload_size, &lf);
       } else {
         wg_vp8_info info; wg::SparseFrame sf;
-        int st = wg::vp8_parse(d.data(), d.size(), 0, &info, nullptr, &sf);
+        // every third run bounded to a random crop bottom (the WebPDecode crop path)
+        const int crop_bottom = it % 3 == 1 ? (int)(rng() % 64) : -1;
+        int st = wg::vp8_parse(d.data(), d.size(), 0, &info, nullptr, &sf, crop_bottom);
         if (st == 0) {
           // device-side invariants the kernels rely on
           size_t nmb = (size_t)info.mb_w * info.mb_h;

@@ -239,3 +239,61 @@ def parse_mode_key(key):
     m, rest = key.split("_", 1)
     crop, fl, nf = rest.rsplit("_", 2)
     return int(m[1:]), crop, int(fl[1:]), int(nf[2:])
+
+
+# ----------------------------------------------------------------------------- status sweep
+def riff_truncate(data, cut):
+    """`data` cut to `cut` bytes with a consistent RIFF: the cut chunk's size field and the
+    RIFF size rewritten (pad byte added for an odd chunk), so the container parses and the
+    truncation reaches the bitstream.  None when the cut falls inside a chunk header."""
+    if cut < 20:
+        return None
+    off = 12
+    while off < len(data):
+        size = int.from_bytes(data[off + 4:off + 8], "little")
+        end = off + 8 + size + (size & 1)
+        if cut == off:
+            out = bytearray(data[:cut])
+            break
+        if cut <= off + 8:
+            return None
+        if cut < end:
+            n = cut - off - 8
+            out = bytearray(data[:cut])
+            out[off + 4:off + 8] = n.to_bytes(4, "little")
+            if n & 1:
+                out.append(0)
+            break
+        off = end
+    else:
+        return None
+    out[4:8] = (len(out) - 8).to_bytes(4, "little")
+    return bytes(out)
+
+
+def mutate(data, op, arg):
+    """One status-sweep mutant (tests/golden/status/sweep.json): 'none', 'trunc_riff'
+    (fraction, riff_truncate), 'trunc' (fraction, raw cut) or 'flip' ([[pos, bit], ...])."""
+    if op == "none":
+        return data
+    if op == "trunc_riff":
+        return riff_truncate(data, int(len(data) * arg))
+    if op == "trunc":
+        return data[:int(len(data) * arg)]
+    if op == "flip":
+        m = bytearray(data)
+        for pos, bit in arg:
+            m[pos] ^= 1 << bit
+        return bytes(m)
+    raise ValueError(op)
+
+
+def status_sweep():
+    with open(os.path.join(GOLDEN, "status", "sweep.json")) as f:
+        return json.load(f)
+
+
+def load_fixture(src):
+    """Bytes of tests/golden/<section>/<name>.webp for src = '<section>/<name>'."""
+    with open(os.path.join(GOLDEN, src + ".webp"), "rb") as f:
+        return f.read()

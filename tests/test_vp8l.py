@@ -45,9 +45,18 @@ def test_vp8l_c5_bench_frame_sha256():
 
 def test_vp8l_truncated_and_corrupt():
     data, _ = load_lossless("ll_corr_64x64")
+    # raw cut: the VP8L chunk runs past the end of the file (DecodeInto's header pass)
     with pytest.raises(webp_amd.WebPError) as e:
         webp_amd.vp8l_parse(data[: len(data) // 2])
-    assert e.value.status in (webp_amd.Status.NOT_ENOUGH_DATA, webp_amd.Status.BITSTREAM_ERROR)
+    assert e.value.status == webp_amd.Status.NOT_ENOUGH_DATA
+    # consistent RIFF, bitstream cut: any end of stream is a bitstream error in WebPDecode
+    from oracle_lib import riff_truncate
+    for frac in (0.3, 0.5, 0.9, 0.99):
+        cut = riff_truncate(data, int(len(data) * frac))
+        with pytest.raises(webp_amd.WebPError) as e:
+            webp_amd.vp8l_parse(cut)
+        assert e.value.status == webp_amd.Status.BITSTREAM_ERROR
+        assert webp_amd.decode_status(cut) == webp_amd.Status.BITSTREAM_ERROR
     with pytest.raises(webp_amd.WebPError):
         webp_amd.vp8l_parse(data[:30])
     lossy = open(os.path.join(GOLDEN, "bench", "c1_512_s0.webp"), "rb").read()
