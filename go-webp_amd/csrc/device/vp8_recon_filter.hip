@@ -130,6 +130,9 @@ __device__ __forceinline__ void lds_sync() {
 }
 
 __device__ __forceinline__ int clamp255(int v) { return min(max(v, 0), 255); }
+// byte 0 of v in all four bytes: one v_perm_b32 (a multiply by 0x01010101 is a quarter-rate
+// v_mul_lo_u32)
+__device__ __forceinline__ uint32_t bcast(uint32_t v) { return __builtin_amdgcn_perm(v, v, 0u); }
 __device__ __forceinline__ int byte_of(uint32_t w, int i) { return (w >> (8 * i)) & 0xff; }
 __device__ __forceinline__ uint32_t ld32(const uint8_t* p) { return *reinterpret_cast<const uint32_t*>(p); }
 __device__ __forceinline__ void st32(uint8_t* p, uint32_t v) { *reinterpret_cast<uint32_t*>(p) = v; }
@@ -233,8 +236,8 @@ __device__ __forceinline__ uint32_t pred_row(uint32_t oh, uint32_t top, int left
   if (__any(oh & 0x2))
     tm = pack_sat4(byte_of(top, 0) + left - tl, byte_of(top, 1) + left - tl, byte_of(top, 2) + left - tl,
                    byte_of(top, 3) + left - tl);
-  const uint32_t v = (oh & 0x4) ? top : (uint32_t)dc * 0x01010101u;  // VE : DC variants
-  const uint32_t w = (oh & 0x8) ? (uint32_t)left * 0x01010101u : tm;  // HE : TM
+  const uint32_t v = (oh & 0x4) ? top : bcast((uint32_t)dc);  // VE : DC variants
+  const uint32_t w = (oh & 0x8) ? bcast((uint32_t)left) : tm;  // HE : TM
   return (oh & 0xA) ? w : v;
 }
 
@@ -255,11 +258,10 @@ struct Line { int p3, p2, p1, p0, q0, q1, q2, q3; };
 __device__ __forceinline__ int sclip1(int v) { return min(max(v, -128), 127); }
 __device__ __forceinline__ int sclip2(int v) { return min(max(v, -16), 15); }
 
-// |a - b| (+ c) for byte values in one v_sad_u32 (sub/neg/max otherwise).
+// |a - b| (+ c) for byte values (0..255) in one v_sad_u8 (sub/neg/max otherwise); a builtin,
+// not inline asm, so the hazard recognizer sees it (no conservative s_nop after each).
 __device__ __forceinline__ int absd(int a, int b, int c = 0) {
-  int r;
-  asm("v_sad_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
+  return (int)__builtin_amdgcn_sad_u8((uint32_t)a, (uint32_t)b, (uint32_t)c);
 }
 
 // KIND 0: simple (NeedsFilter + DoFilter2, dec.c.go:552-586);
@@ -271,8 +273,8 @@ __device__ __forceinline__ void filter_line(Line& l, int t2, int it, int hev_t) 
   const int d0 = l.q0 - l.p0;
   const int sp = sclip1(l.p1 - l.q1);
   const bool edge_ok = absd(l.p1, l.q1, 4 * absd(l.p0, l.q0)) <= t2;
-  // DoFilter2
-  const int a = 3 * d0 + sp;
+  // DoFilter2 (24-bit multiplies: a 32-bit 3*d0 + sp became a quarter-rate v_mad_u64_u32)
+  const int a = __mul24(d0, 3) + sp;
   const int f2p0 = clamp255(l.p0 + sclip2((a + 3) >> 3));
   const int f2q0 = clamp255(l.q0 - sclip2((a + 4) >> 3));
   if (KIND == 0) {
@@ -288,7 +290,7 @@ __device__ __forceinline__ void filter_line(Line& l, int t2, int it, int hev_t) 
   const bool f2 = on & hv, fx = on & !hv;
   if (KIND == 1) {  // DoFilter6
     const int w = sclip1(a);
-    const int a1 = (27 * w + 63) >> 7, a2 = (18 * w + 63) >> 7, a3 = (9 * w + 63) >> 7;
+    const int a1 = (__mul24(w, 27) + 63) >> 7, a2 = (__mul24(w, 18) + 63) >> 7, a3 = (__mul24(w, 9) + 63) >> 7;
     const int np2 = clamp255(l.p2 + a3), np1 = clamp255(l.p1 + a2), np0 = clamp255(l.p0 + a1);
     const int nq0 = clamp255(l.q0 - a1), nq1 = clamp255(l.q1 - a2), nq2 = clamp255(l.q2 - a3);
     l.p2 = fx ? np2 : l.p2;
@@ -299,7 +301,7 @@ __device__ __forceinline__ void filter_line(Line& l, int t2, int it, int hev_t) 
     l.q0 = fx ? nq0 : (f2 ? f2q0 : l.q0);
   } else {  // DoFilter4, or DoFilter2 on hev lines: both are p0 += sclip2((a+3)>>3),
             // q0 -= sclip2((a+4)>>3) with a = 3*(q0-p0) [+ sclip1(p1-q1) when hev]
-    const int a = 3 * d0 + (hv ? sp : 0);
+    const int a = __mul24(d0, 3) + (hv ? sp : 0);
     const int a1 = sclip2((a + 4) >> 3), a2 = sclip2((a + 3) >> 3), a3 = (a1 + 1) >> 1;
     const int np0 = clamp255(l.p0 + a2), nq0 = clamp255(l.q0 - a1);
     const int np1 = clamp255(l.p1 + a3), nq1 = clamp255(l.q1 - a3);
@@ -572,7 +574,7 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
       asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lid));
       const int m = lid & 15;
       const int gg = lid >> 4;
-      uint8_t* ws = lds + kHdrBytes + (wave * kRows + gg) * kSlotBytes;  // recon workspace (libwebp yuv_b)
+      uint8_t* ws = lds + kHdrBytes + __mul24(wave * kRows + gg, kSlotBytes);  // recon workspace (libwebp yuv_b)
       uint8_t* fw = ws + kWsBytes;                                        // filter window
       uint8_t* left = fw + kFwBytes;                                      // unfiltered left columns
       int16_t* res = reinterpret_cast<int16_t*>(left + kLeftBytes);        // i4x4 residuals
@@ -620,7 +622,7 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
       }
       const uint32_t fl = rc.flags;
       const bool i4 = (fl >> kI4Shift) & 1;
-      const ColPtr col = cols + x * kColBytes;
+      const ColPtr col = cols + __mul24(x, kColBytes);
 
       K1_SECT(1);
       // ---- ReconstructRow prologue at the row's first MB (frame_dec.c.go:79-98)
@@ -660,7 +662,7 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
           top_carry = tv;
         } else if (m == 8 && i4) {
           // top-right samples, replicated down to rows 3, 7, 11 by the same lane (no read-back)
-          const uint32_t tr = last_x ? (uint32_t)col[15] * 0x01010101u : ld32(col + kColBytes);
+          const uint32_t tr = last_x ? bcast(col[15]) : ld32(col + kColBytes);
           st32(ws + Y_OFF - BPS + 16, tr);
           st32(ws + Y_OFF + 3 * BPS + 16, tr);
           st32(ws + Y_OFF + 7 * BPS + 16, tr);

@@ -16,7 +16,7 @@ import tempfile
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(HERE, "..", "go-webp_amd", "csrc", "device", "vp8_recon_filter.hip")
-MARKS = [("// ---- software pipeline", "prefetch"), ("// ---- wait for the previous pair", "wait"),
+MARKS = [("// ---- software pipeline", "prefetch"), ("// ---- wait for the previous quad", "wait"),
          ("// ---- ReconstructRow prologue", "prologue"), ("// ---- top samples", "top"),
          ("// ---- residuals of all blocks", "idct"), ("// ---- luma prediction + residual", "lumapred"),
          ("if (__any(act && i4))", "i4"), ("// ---- chroma prediction + residual", "chroma"),
