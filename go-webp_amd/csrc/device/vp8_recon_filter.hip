@@ -88,7 +88,8 @@ constexpr int kSections = 14;
 __device__ unsigned long long g_k1_sections[kSections];
 // timeline: per workgroup (frame) the start time and each wave's exit time (s_memrealtime)
 constexpr int kTimelineFrames = 1024;
-__device__ unsigned long long g_k1_timeline[kTimelineFrames][1 + kWaves];
+// [0] start, [1 + w] wave w leaves reconstruction, [1 + kWaves + w] wave w leaves the kernel
+__device__ unsigned long long g_k1_timeline[kTimelineFrames][1 + 2 * kWaves];
 #define K1_SECT_DECL() uint64_t sect_acc[kSections] = {}, sect_t = 0
 #define K1_SECT_START() (sect_t = __builtin_amdgcn_s_memtime())
 #define K1_SECT(id)                                       \
@@ -105,6 +106,19 @@ __device__ unsigned long long g_k1_timeline[kTimelineFrames][1 + kWaves];
         g_k1_timeline[blockIdx.x][1 + wave] = __builtin_amdgcn_s_memrealtime(); \
     }                                                                          \
   } while (0)
+// per frame and quad: start and end of the quad's MB loop
+constexpr int kTimelineQuads = 64;
+__device__ unsigned long long g_k1_quads[kTimelineFrames][kTimelineQuads][2];
+#define K1_QUAD_MARK(k, which)                                                 \
+  do {                                                                         \
+    if (lane == 0 && blockIdx.x < kTimelineFrames && (k) < kTimelineQuads)     \
+      g_k1_quads[blockIdx.x][k][which] = __builtin_amdgcn_s_memrealtime();     \
+  } while (0)
+#define K1_TIMELINE_END()                                                      \
+  do {                                                                         \
+    if (lane == 0 && blockIdx.x < kTimelineFrames)                             \
+      g_k1_timeline[blockIdx.x][1 + kWaves + wave] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
 #define K1_TIMELINE_START()                                                    \
   do {                                                                         \
     if (threadIdx.x == 0 && blockIdx.x < kTimelineFrames)                     \
@@ -116,6 +130,8 @@ __device__ unsigned long long g_k1_timeline[kTimelineFrames][1 + kWaves];
 #define K1_SECT(id) (void)0
 #define K1_SECT_FLUSH() (void)0
 #define K1_TIMELINE_START() (void)0
+#define K1_TIMELINE_END() (void)0
+#define K1_QUAD_MARK(k, which) (void)0
 #endif
 
 __device__ __forceinline__ void lds_sync() {
@@ -128,6 +144,18 @@ __device__ __forceinline__ void lds_sync() {
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+
+// s_setprio takes an immediate: p is wave-uniform
+__device__ __forceinline__ void set_prio(int p) {
+  if (p >= 3) __builtin_amdgcn_s_setprio(3);
+  else if (p == 2) __builtin_amdgcn_s_setprio(2);
+  else if (p == 1) __builtin_amdgcn_s_setprio(1);
+  else __builtin_amdgcn_s_setprio(0);
+}
+
+#ifndef WG_K1_PRIO_MODE
+#define WG_K1_PRIO_MODE 0
+#endif
 
 __device__ __forceinline__ int clamp255(int v) { return min(max(v, 0), 255); }
 // byte 0 of v in all four bytes: one v_perm_b32 (a multiply by 0x01010101 is a quarter-rate
@@ -473,6 +501,7 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
   // vmcnt(0) drained the record/coefficient prefetch every MB.
   __shared__ uint32_t progress[kWaves];
   __shared__ uint32_t recon_done, next_unit;  // K1 tail (emit_tail): waves done, units claimed
+  __shared__ uint32_t quads_done;
   const FrameDesc* F = frames + blockIdx.x;
   if (!F->valid || (F->cols != nullptr) != kGlobalCols) return;
   const int mb_w = F->mb_w, mb_h = F->mb_h;
@@ -506,7 +535,7 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
   else cols = lds + kHdrBytes + kMaxRecon * kRows * kSlotBytes;
   // per MB column c: cols + c*kColBytes: [0..15] ytop Y, [16..23] U, [24..31] V, [32..159] fbot
   if (threadIdx.x < kWaves) progress[threadIdx.x] = 0;
-  if (threadIdx.x == 0) recon_done = next_unit = 0;
+  if (threadIdx.x == 0) recon_done = next_unit = quads_done = 0;
   const bool emit = F->flags & kFrameEmitRgba;
   if (emit) __builtin_amdgcn_s_setprio(2);  // reconstruction is the critical path; the tail's conversion yields
   const int nquads = (mb_h + kRows - 1) / kRows;
@@ -515,6 +544,7 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
   // ring safe: quad k + 16 only starts on a wave that has completed a quad > k, so quad k
   // is complete whenever its slot holds a later quad's value.
   const int R = recon_waves_arg > 0 ? min(recon_waves_arg, kMaxRecon) : kMaxRecon;
+  if (WG_K1_PRIO_MODE == 1 && wave < R) set_prio(1 + (3 * wave) / R);
   for (int t = threadIdx.x; t < 160; t += blockDim.x) tab[t] = kPred4Table[t];
   K1_TIMELINE_START();
   __syncthreads();
@@ -525,8 +555,6 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
     const bool row_ok = y < mb_h;
     const bool has_next = kRows * (k + 1) < mb_h;  // a later quad waits on this one's last row
     const bool last_row = y == mb_h - 1;
-    const int nrows_y = last_row ? 16 : 13;  // luma rows of this MB row final after its pass
-    const int nrows_c = last_row ? 8 : 5;
     uint32_t blk = row_ok ? row_block0[y] : 0u;
     MbRec rc = load_rec(recs, mb_w, y, row_ok, -2 * g);
     MbRec rn = load_rec(recs, mb_w, y, row_ok, -2 * g + 1);
@@ -541,30 +569,24 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
     // conservatively drain the NEXT MB's prefetch with a vmcnt(0).
     __builtin_amdgcn_s_waitcnt(0x0F70);
     uint32_t top_carry = 0;  // see "top samples"
-    // Plane offsets of the five HBM store slots (see "final pixels to HBM") of both roles at
-    // MB column 0, once per quad: per MB only `x << shift` is added.  A slot that never
-    // stores for this row/role starts at kDrop, and kDrop + 16x stays beyond the planes.
-    uint32_t sbA0[2], sbA1[2], sbB[2], sbC[2], sbE[2];
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int l0 = (lane & 15) + 16 * s, q0 = l0 & 3, b00 = l0 >> 2;
-      sbA0[s] = b00 < nrows_y ? (uint32_t)__mul24(16 * y + b00, ys) - 4u + 4u * q0 : kDrop;
-      sbA1[s] = b00 + 8 < nrows_y ? (uint32_t)__mul24(16 * y + b00 + 8, ys) - 4u + 4u * q0 : kDrop;
-      const int bk = l0 - 12, bp = bk >= 6, brem = bk - 6 * bp;
-      const int brr = l0 < 12 ? (l0 >> 2) - 3 : (brem >> 1) - 3;
-      const int bd = l0 < 12 ? (l0 & 3) : (brem & 1);
-      sbB[s] = !(y > 0 && l0 < 24) ? kDrop
-               : l0 < 12 ? (uint32_t)__mul24(16 * y + brr, ys) + 4u * bd
-                         : (bp ? voff : uoff) + (uint32_t)__mul24(8 * y + brr, uvs) + 4u * bd;
-      const bool cl = l0 >= 16;
-      const uint32_t cpoff = ((l0 >> 3) & 1) ? voff : uoff;
-      sbC[s] = cl ? ((l0 & 7) < nrows_c ? cpoff + (uint32_t)__mul24(8 * y + (l0 & 7), uvs) + 4u : kDrop)
-                  : (l0 < nrows_y ? (uint32_t)__mul24(16 * y + l0, ys) + 12u : kDrop);
-      const int ep = l0 >> 4, er = (l0 >> 1) & 7, ed = l0 & 1;
-      sbE[s] = er < nrows_c ? (ep ? voff : uoff) + (uint32_t)__mul24(8 * y + er, uvs) - 4u + 4u * ed : kDrop;
+    // Plane offsets (at MB column 0) of the lane's two row-segment stores, once per quad (see
+    // "final pixels to HBM"); per MB only `x << 4` / `x << 3` is added.  Luma: lanes 0..12
+    // row m, cols -4..11; lanes 13..15 rows 13..15 of the MB above, cols 0..15.  Chroma
+    // (U lanes 0..7, V 8..15): rows 0..4 cols -4..3; lanes 5..7 rows 5..7 above, cols 0..7.
+    // Rows above exist for y > 0 only: kDrop + 16x stays beyond the planes.
+    uint32_t sb_y, sb_c;
+    {
+      const int m0 = lane & 15, rc = m0 & 7;
+      // (minus 4: the per-MB offset adds the segment's window column, 0 or 4)
+      sb_y = m0 >= 13 ? (y > 0 ? (uint32_t)__mul24(16 * y - 16 + m0, ys) - 4u : kDrop)
+                      : (uint32_t)__mul24(16 * y + m0, ys) - 4u;
+      const uint32_t cp = m0 >= 8 ? voff : uoff;
+      sb_c = rc >= 5 ? (y > 0 ? cp + (uint32_t)__mul24(8 * y - 8 + rc, uvs) - 4u : kDrop)
+                     : cp + (uint32_t)__mul24(8 * y + rc, uvs) - 4u;
     }
 
     K1_SECT_START();
+    K1_QUAD_MARK(k, 0);
 
     for (int i = 0; i < mb_w + 2 * (kRows - 1); ++i) {
       // Lane roles, recomputed every iteration from an opaque lane id: hoisted out of the
@@ -599,6 +621,11 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
       //      and the timeout does not leave the loop: any path reaching the loop latch without
       //      this iteration's plane stores makes the waitcnt pass extend the latch's prefetch
       //      wait over those stores (a vmcnt that waits for store acks every MB).
+      if (WG_K1_PRIO_MODE == 2 && (i & 15) == 0) {
+        const int d = k - (int)__builtin_amdgcn_readfirstlane(
+                              __hip_atomic_load(&quads_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        set_prio(1 + min(2, (3 * d) / R));
+      }
       if (k > 0 && i < mb_w) {
         const uint32_t need = ((uint32_t)(k - 1) << 16) | (uint32_t)min(i + lead, mb_w);
         uint32_t* pr = progress + ((k - 1) & (kWaves - 1));
@@ -676,14 +703,19 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
       int ry0[2][4], ry1[2][4], rcr[2][4];
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
+#ifndef WG_ABL_IDCT
         idct_pass(q, cc[s].y0, ry0[s]);
         idct_pass(q, cc[s].y1, ry1[s]);
         idct_pass(q, cc[s].c, rcr[s]);
+#else
+        for (int t = 0; t < 4; ++t) ry0[s][t] = ry1[s][t] = rcr[s][t] = (int)(cc[s].y0.x + cc[s].y1.y + cc[s].c.x) >> 20;
+#endif
       }
 
       K1_SECT(4);
       // ---- luma prediction + residual (role r: block column (r>>2)&3, pixel rows
       //      4*((r>>2)>>2)+q and that + 8)
+#ifndef WG_ABL_PRED
       if (act && !i4) {
         const uint32_t oh = 1u << check_mode(x, y, (fl >> kYModeShift) & 3);
         const int tl = ws[Y_OFF - BPS - 1];
@@ -740,8 +772,10 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
           st32(ws + coff + row * BPS + 4 * cbx, add_res(pred, rcr[s]));
         }
       }
+#endif
       lds_sync();
       K1_SECT(5);
+#ifndef WG_ABL_I4
       if (__any(act && i4)) {
         // recipe words and residuals of all sixteen blocks fetched up front (independent loads)
         const uint32_t im_lo = rc.imodes_lo, im_hi = rc.imodes_hi;
@@ -781,6 +815,7 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
           if (j == 15 || kI4Step[j + 1] != kI4Step[j]) lds_sync();
         }
       }
+#endif
 
       K1_SECT(6);
       K1_SECT(7);
@@ -815,7 +850,11 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
         const uint32_t fi = rc.finfo;
         const int limit = fi & 0xff;
         const bool on = act && limit > 0;
+#ifdef WG_ABL_FILTER
+        if (false) {
+#else
         if (ftype > 0 && __any(on)) {
+#endif
           const int ilevel = (fi >> 8) & 0xff, inner = (fi >> 16) & 0xff, hev_t = (fi >> 24) & 0xff;
           if (ftype == 2) filter_mb<true>(fw, m, on, x > 0, y > 0, inner != 0, limit, ilevel, hev_t);
           else filter_mb<false>(fw, m, on, x > 0, y > 0, inner != 0, limit, ilevel, hev_t);
@@ -849,43 +888,48 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
         }
       }
       K1_SECT(10);
-      // ---- final pixels to HBM (each byte written once).  Five dword slots per role, all
-      //      buffer stores against one descriptor spanning the frame's Y|U|V planes; an idle
-      //      slot gets an out-of-range offset and the hardware bounds check drops it, so the
-      //      section is branch-free and its LDS reads issue back to back.
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const int l = m + 16 * s, b0 = l >> 2;
-        const bool cl = s == 1;  // chroma role (slots C, E by plane)
-        const int pl = (l >> 3) & 1;
-        const uint8_t* cwin = fw + (pl ? kFwV : kFwU);
-        const int er = (l >> 1) & 7, ed = l & 1;  // slot E
-        const uint8_t* ewin = fw + (s ? kFwV : kFwU);
-        // slot B: roles 0..11 luma rows -3..-1 of the MB above (cols 0..15),
-        //         roles 12..23 chroma rows -3..-1 (cols 0..7), U then V
-        const int bk = l - 12, bp = bk >= 6, brem = bk - 6 * bp;
-        const int brr = l < 12 ? (l >> 2) - 3 : (brem >> 1) - 3;
-        const int bd = l < 12 ? (l & 3) : (brem & 1);
-        const uint8_t* bsrc = l < 12 ? fw + kFwY + (brr + 4) * FWY + 4 + 4 * bd
-                                     : fw + (bp ? kFwV : kFwU) + (brr + 4) * FWC + 4 + 4 * bd;
-        const uint32_t vA0 = ld32(fw + kFwY + (b0 + 4) * FWY + 4 * q);
-        const uint32_t vA1 = ld32(fw + kFwY + (b0 + 12) * FWY + 4 * q);
-        const uint32_t vB = ld32(bsrc);
-        const uint32_t vC = cl ? ld32(cwin + ((l & 7) + 4) * FWC + 8) : ld32(fw + kFwY + (l + 4) * FWY + 16);
-        const uint32_t vE = ld32(ewin + (er + 4) * FWC + 4 * ed);
+      // ---- final pixels to HBM.  After this MB's filter, its rows 0..12 (chroma 0..4) are final
+      //      in cols 0..11 (0..3), and so are the left neighbour's cols 12..15 (4..7) and the
+      //      bottom rows 13..15 (5..7) of the MB above: one 16-byte (8-byte chroma) row segment
+      //      per lane, two buffer stores per MB step, against one descriptor spanning the
+      //      frame's Y|U|V planes.  At x = 0 the segment starts at col 0 instead of -4: its
+      //      last 4 (chroma 4) bytes are not final yet and are rewritten, final, by the same
+      //      lane at x = 1 (same-address stores of a lane stay in order) or by the last-column
+      //      store below.  The bottom MB row and the last MB column add their rows 13..15
+      //      (5..7) and cols 12..15 (4..7) under branches.
+      {
+        const bool tl = m >= 13, tc = (m & 7) >= 5;
+        const int wcy = (tl || x == 0) ? 4 : 0, wcc = (tc || x == 0) ? 4 : 0;
+        const uint8_t* sy = fw + kFwY + (tl ? m - 12 : m + 4) * FWY + wcy;
+        const uint8_t* sc = fw + (m >= 8 ? kFwV : kFwU) + (tc ? (m & 7) - 4 : (m & 7) + 4) * FWC + wcc;
+        const u32x4 vy = {ld32(sy), ld32(sy + 4), ld32(sy + 8), ld32(sy + 12)};
+        const u32x2 vc = {ld32(sc), ld32(sc + 4)};
         const uint32_t ux = (uint32_t)x;
-        const bool aok = act && (q > 0 || x > 0);
-        const int shB = l < 12 ? 4 : 3, shC = cl ? 3 : 4;
-        const uint32_t oA0 = aok ? sbA0[s] + (ux << 4) : kDrop;
-        const uint32_t oA1 = aok ? sbA1[s] + (ux << 4) : kDrop;
-        const uint32_t oB = act ? sbB[s] + (ux << shB) : kDrop;
-        const uint32_t oC = act && last_x ? sbC[s] + (ux << shC) : kDrop;
-        const uint32_t oE = act && (ed > 0 || x > 0) ? sbE[s] + (ux << 3) : kDrop;
-        __builtin_amdgcn_raw_buffer_store_b32(vA0, planes, (int)oA0, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(vA1, planes, (int)oA1, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(vB, planes, (int)oB, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(vC, planes, (int)oC, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(vE, planes, (int)oE, 0, 0);
+        const uint32_t oy = act ? sb_y + (ux << 4) + wcy : kDrop;
+        const uint32_t oc = act ? sb_c + (ux << 3) + wcc : kDrop;
+        __builtin_amdgcn_raw_buffer_store_b128(vy, planes, (int)oy, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(vc, planes, (int)oc, 0, 0);
+        const int w0 = x == 0 ? 4 : 0;  // the own-row segments' window column
+        if (act && last_row && tl) {  // rows 13..15 of the bottom MB row (no MB below)
+          const uint8_t* s2 = fw + kFwY + (m + 4) * FWY + w0;
+          const u32x4 v2 = {ld32(s2), ld32(s2 + 4), ld32(s2 + 8), ld32(s2 + 12)};
+          __builtin_amdgcn_raw_buffer_store_b128(v2, planes, __mul24(16 * y + m, ys) + 16 * x + w0 - 4, 0, 0);
+        }
+        if (act && last_row && tc) {  // chroma rows 5..7 of the bottom MB row
+          const uint8_t* s2 = fw + (m >= 8 ? kFwV : kFwU) + ((m & 7) + 4) * FWC + w0;
+          const u32x2 v2 = {ld32(s2), ld32(s2 + 4)};
+          __builtin_amdgcn_raw_buffer_store_b64(
+              v2, planes, (int)((m >= 8 ? voff : uoff) + __mul24(8 * y + (m & 7), uvs)) + 8 * x + w0 - 4, 0, 0);
+        }
+        if (act && last_x) {  // the last MB column's cols 12..15 (chroma 4..7) of its own rows
+          if (m < 13 || last_row)
+            __builtin_amdgcn_raw_buffer_store_b32(ld32(fw + kFwY + (m + 4) * FWY + 16), planes,
+                                                  __mul24(16 * y + m, ys) + 16 * x + 12, 0, 0);
+          if ((m & 7) < 5 || last_row)
+            __builtin_amdgcn_raw_buffer_store_b32(
+                ld32(fw + (m >= 8 ? kFwV : kFwU) + ((m & 7) + 4) * FWC + 8), planes,
+                (int)((m >= 8 ? voff : uoff) + __mul24(8 * y + (m & 7), uvs)) + 8 * x + 4, 0, 0);
+        }
       }
       lds_sync();
 
@@ -919,9 +963,16 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
       cc[1] = cn[1];
       blk = blk_next;
     }
+    K1_QUAD_MARK(k, 1);
+    if (WG_K1_PRIO_MODE == 2 && lane == 0)
+      __hip_atomic_fetch_add(&quads_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
   K1_SECT_FLUSH();
+#ifdef WG_ABL_TAIL
+  if (false) {
+#else
   if (emit) {
+#endif
     // Own plane stores complete before announcing the wave done: converters may read the
     // bottom rows right after the last wave's increment, with no row of margin left.
     // (Workgroup-scope release alone emits no vmcnt wait; this costs one wait per wave.)
@@ -931,6 +982,7 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
     if (F->flags & kFrameNoFancy) emit_tail<false>(*F, progress, &recon_done, &next_unit, lane, err);
     else emit_tail<true>(*F, progress, &recon_done, &next_unit, lane, err);
   }
+  K1_TIMELINE_END();
 }
 
 #ifdef WG_K1_SECTION_TIMING
@@ -944,11 +996,19 @@ extern "C" int wg_debug_k1_sections(unsigned long long* out, int n, int reset) {
   return n;
 }
 
-// per frame: start, then the exit time of each of the 16 waves (memrealtime ticks, 100 MHz)
+// per frame: start, each wave's exit from reconstruction, each wave's exit from the kernel
+// (memrealtime ticks, 100 MHz)
 extern "C" int wg_debug_k1_timeline(unsigned long long* out, int n_frames) {
   if (n_frames > kTimelineFrames) n_frames = kTimelineFrames;
-  const size_t bytes = (size_t)n_frames * (1 + kWaves) * sizeof(unsigned long long);
+  const size_t bytes = (size_t)n_frames * (1 + 2 * kWaves) * sizeof(unsigned long long);
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_k1_timeline), bytes) != hipSuccess) return -1;
+  return n_frames;
+}
+
+extern "C" int wg_debug_k1_quads(unsigned long long* out, int n_frames) {
+  if (n_frames > kTimelineFrames) n_frames = kTimelineFrames;
+  const size_t bytes = (size_t)n_frames * kTimelineQuads * 2 * sizeof(unsigned long long);
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_k1_quads), bytes) != hipSuccess) return -1;
   return n_frames;
 }
 #endif

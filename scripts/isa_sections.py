@@ -25,6 +25,21 @@ MARKS = [("// ---- software pipeline", "prefetch"), ("// ---- wait for the previ
          ("// ---- rotate for the next MB", "rotate"), ("rc = rn;", "end")]
 
 
+# Issue cost of a VALU instruction in SIMD-throughput units, measured by
+# scripts/probes/valu_rate.hip (4 waves per SIMD): plain 2-operand integer ALU ops issue at
+# one per ~1.07 ns per SIMD (1 unit); 3-operand ops, min/max, multiplies, compares,
+# cndmask, DPP, SDWA and packed 16-bit ops at one per ~2.1 ns (2 units); v_ashr_pk_u8_i32 3.4.
+FULL_RATE = re.compile(r"v_(add|sub|subrev)_(u32|co_u32|i32)(_e32|_e64)?$|v_(and|or|xor|not)_b32(_e32|_e64)?$|"
+                       r"v_(lshrrev|lshlrev)_b32(_e32|_e64)?$|v_ashrrev_i32(_e32|_e64)?$|v_mov_b32(_e32|_e64)?$|"
+                       r"v_(add|sub)_u16(_e32|_e64)?$|v_mul_lo_u16(_e32|_e64)?$")
+
+
+def valu_units(op):
+    if op.startswith("v_ashr_pk_u8"):
+        return 3.4
+    return 1.0 if FULL_RATE.match(op) else 2.0
+
+
 def main():
     src = sys.argv[1] if len(sys.argv) > 1 else SRC
     d = os.path.dirname(os.path.abspath(src))
@@ -62,11 +77,13 @@ def main():
             cls = ("valu" if op.startswith("v_") else "salu" if op.startswith("s_") else "lds" if op.startswith("ds_")
                    else "vmem" if op.startswith(("global_", "buffer_", "flat_")) else "other")
             cnt.setdefault(cur, collections.Counter())[cls] += 1
+            if cls == "valu":
+                cnt[cur]["units"] += valu_units(op)
     tot = collections.Counter()
     for k, v in cnt.items():
-        print(f"{k:10s} " + " ".join(f"{c}={v[c]}" for c in ("valu", "salu", "lds", "vmem")))
+        print(f"{k:10s} " + " ".join(f"{c}={v[c]:g}" for c in ("valu", "units", "salu", "lds", "vmem")))
         tot += v
-    print("total      " + " ".join(f"{c}={tot[c]}" for c in ("valu", "salu", "lds", "vmem")), meta)
+    print("total      " + " ".join(f"{c}={tot[c]:g}" for c in ("valu", "units", "salu", "lds", "vmem")), meta)
 
 
 if __name__ == "__main__":

@@ -11,7 +11,7 @@ import ctypes as C
 import os
 import sys
 
-os.environ["WG_LIB_VARIANT"] = "timing"
+os.environ["WG_LIB_VARIANT"] = os.environ.get("K1_TIMING_VARIANT", "timing")
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "go-webp_amd"), os.path.join(ROOT, "tests")]
 
@@ -53,11 +53,11 @@ def main():
     L.wg_debug_k1_timeline.restype = C.c_int
     L.wg_debug_k1_timeline.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
     nf = min(args.batch, 1024)
-    tl = (C.c_ulonglong * (nf * 17))()
+    tl = (C.c_ulonglong * (nf * 33))()
     L.wg_debug_k1_timeline(tl, nf)
     import numpy as np
-    t = np.frombuffer(tl, dtype=np.uint64).reshape(nf, 17).astype(np.int64)
-    start, ends = t[:, :1], t[:, 1:]
+    t = np.frombuffer(tl, dtype=np.uint64).reshape(nf, 33).astype(np.int64)
+    start, ends, kend = t[:, :1], t[:, 1:17], t[:, 17:]
     dur = ends.max(1) - start[:, 0]
     idle = (ends.max(1, keepdims=True) - ends).sum(1) / (16.0 * dur)
     srt = np.sort(ends - start, axis=1)
@@ -65,6 +65,20 @@ def main():
           f"max {dur.max() / 100:.1f}); idle wave-time after exit {100 * idle.mean():.1f}%")
     print("  mean exit time of the k-th wave to finish, % of frame span:",
           " ".join(f"{100 * (srt[:, k] / dur).mean():.0f}" for k in range(16)))
+    print("  mean reconstruction exit per wave index, % of span:",
+          " ".join(f"{100 * ((ends[:, w] - start[:, 0]) / dur).mean():.0f}" for w in range(16)))
+    fend = kend.max(1) - start[:, 0]
+    print(f"  frame end (last wave leaves the kernel) {100 * (fend / dur).mean():.1f}% of the reconstruction span "
+          f"({fend.mean() / 100:.1f} us)")
+    L.wg_debug_k1_quads.restype = C.c_int
+    L.wg_debug_k1_quads.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
+    qb = (C.c_ulonglong * (nf * 64 * 2))()
+    L.wg_debug_k1_quads(qb, nf)
+    q = np.frombuffer(qb, dtype=np.uint64).reshape(nf, 64, 2).astype(np.int64)
+    nq = int((q[0, :, 1] > 0).sum())
+    rel = lambda v: 100 * ((v - start) / dur[:, None]).mean(0)
+    qs, qe = rel(q[:, :nq, 0]), rel(q[:, :nq, 1])
+    print("  quad start/end, % of span:", " ".join(f"{k}:{a:.0f}-{b:.0f}" for k, (a, b) in enumerate(zip(qs, qe))))
     st = start[:, 0] - start.min()
     print(f"  frame start spread {st.max() / 100:.1f} us; kernel span {(ends.max() - start.min()) / 100:.1f} us")
     b.close()
