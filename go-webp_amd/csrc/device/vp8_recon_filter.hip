@@ -145,17 +145,6 @@ __device__ __forceinline__ void lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// s_setprio takes an immediate: p is wave-uniform
-__device__ __forceinline__ void set_prio(int p) {
-  if (p >= 3) __builtin_amdgcn_s_setprio(3);
-  else if (p == 2) __builtin_amdgcn_s_setprio(2);
-  else if (p == 1) __builtin_amdgcn_s_setprio(1);
-  else __builtin_amdgcn_s_setprio(0);
-}
-
-#ifndef WG_K1_PRIO_MODE
-#define WG_K1_PRIO_MODE 0
-#endif
 
 __device__ __forceinline__ int clamp255(int v) { return min(max(v, 0), 255); }
 // byte 0 of v in all four bytes: one v_perm_b32 (a multiply by 0x01010101 is a quarter-rate
@@ -501,7 +490,6 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
   // vmcnt(0) drained the record/coefficient prefetch every MB.
   __shared__ uint32_t progress[kWaves];
   __shared__ uint32_t recon_done, next_unit;  // K1 tail (emit_tail): waves done, units claimed
-  __shared__ uint32_t quads_done;
   const FrameDesc* F = frames + blockIdx.x;
   if (!F->valid || (F->cols != nullptr) != kGlobalCols) return;
   const int mb_w = F->mb_w, mb_h = F->mb_h;
@@ -535,7 +523,7 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
   else cols = lds + kHdrBytes + kMaxRecon * kRows * kSlotBytes;
   // per MB column c: cols + c*kColBytes: [0..15] ytop Y, [16..23] U, [24..31] V, [32..159] fbot
   if (threadIdx.x < kWaves) progress[threadIdx.x] = 0;
-  if (threadIdx.x == 0) recon_done = next_unit = quads_done = 0;
+  if (threadIdx.x == 0) recon_done = next_unit = 0;
   const bool emit = F->flags & kFrameEmitRgba;
   if (emit) __builtin_amdgcn_s_setprio(2);  // reconstruction is the critical path; the tail's conversion yields
   const int nquads = (mb_h + kRows - 1) / kRows;
@@ -544,7 +532,6 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
   // ring safe: quad k + 16 only starts on a wave that has completed a quad > k, so quad k
   // is complete whenever its slot holds a later quad's value.
   const int R = recon_waves_arg > 0 ? min(recon_waves_arg, kMaxRecon) : kMaxRecon;
-  if (WG_K1_PRIO_MODE == 1 && wave < R) set_prio(1 + (3 * wave) / R);
   for (int t = threadIdx.x; t < 160; t += blockDim.x) tab[t] = kPred4Table[t];
   K1_TIMELINE_START();
   __syncthreads();
@@ -621,11 +608,6 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
       //      and the timeout does not leave the loop: any path reaching the loop latch without
       //      this iteration's plane stores makes the waitcnt pass extend the latch's prefetch
       //      wait over those stores (a vmcnt that waits for store acks every MB).
-      if (WG_K1_PRIO_MODE == 2 && (i & 15) == 0) {
-        const int d = k - (int)__builtin_amdgcn_readfirstlane(
-                              __hip_atomic_load(&quads_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-        set_prio(1 + min(2, (3 * d) / R));
-      }
       if (k > 0 && i < mb_w) {
         const uint32_t need = ((uint32_t)(k - 1) << 16) | (uint32_t)min(i + lead, mb_w);
         uint32_t* pr = progress + ((k - 1) & (kWaves - 1));
@@ -964,8 +946,6 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
       blk = blk_next;
     }
     K1_QUAD_MARK(k, 1);
-    if (WG_K1_PRIO_MODE == 2 && lane == 0)
-      __hip_atomic_fetch_add(&quads_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
   K1_SECT_FLUSH();
 #ifdef WG_ABL_TAIL
