@@ -162,8 +162,37 @@ __device__ __forceinline__ void st32(gptr<uint8_t> p, uint32_t v) { *(gptr<uint3
 __device__ __forceinline__ int mul1(int a) { return (__mul24(a, 20091) >> 16) + a; }
 __device__ __forceinline__ int mul2(int a) { return __mul24(a, 35468) >> 16; }
 
-__device__ __forceinline__ int dpp_swap1(int v) { return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, true); }
-__device__ __forceinline__ int dpp_swap2(int v) { return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, true); }
+
+// 4x4 transpose across a lane quad (lane q holds row q in t[0..3], ends with column q):
+// two DPP exchange stages, each pair as two v_cndmask_b32_dpp (the swapped operand through
+// DPP, the kept one selected by a lane-parity mask in VCC) -- 8 VALU instead of 4 DPP moves
+// plus 12 selects.  Hardware hazard: DPP reading a VGPR written by the previous VALU needs
+// two wait states (the leading s_nop 1; the second stage's inputs are >= 2 instructions
+// old).  Checked on the device by scripts/probes/quad_transpose.hip.
+__device__ __forceinline__ void quad_transpose(int t[4]) {
+  int n0, n1, n2, n3, m0, m1, m2, m3;
+  asm volatile(
+      "s_nop 1\n\t"
+      "s_mov_b32 vcc_lo, 0xaaaaaaaa\n\ts_mov_b32 vcc_hi, 0xaaaaaaaa\n\t"
+      "v_cndmask_b32_dpp %1, %8, %9, vcc quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+      "v_cndmask_b32_dpp %3, %10, %11, vcc quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+      "s_mov_b32 vcc_lo, 0x55555555\n\ts_mov_b32 vcc_hi, 0x55555555\n\t"
+      "v_cndmask_b32_dpp %0, %9, %8, vcc quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+      "v_cndmask_b32_dpp %2, %11, %10, vcc quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+      "s_mov_b32 vcc_lo, 0xcccccccc\n\ts_mov_b32 vcc_hi, 0xcccccccc\n\t"
+      "v_cndmask_b32_dpp %6, %0, %2, vcc quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+      "v_cndmask_b32_dpp %7, %1, %3, vcc quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+      "s_mov_b32 vcc_lo, 0x33333333\n\ts_mov_b32 vcc_hi, 0x33333333\n\t"
+      "v_cndmask_b32_dpp %4, %2, %0, vcc quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+      "v_cndmask_b32_dpp %5, %3, %1, vcc quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf"
+      : "=&v"(n0), "=&v"(n1), "=&v"(n2), "=&v"(n3), "=&v"(m0), "=&v"(m1), "=&v"(m2), "=&v"(m3)
+      : "v"(t[0]), "v"(t[1]), "v"(t[2]), "v"(t[3])
+      : "vcc");
+  t[0] = m0;
+  t[1] = m1;
+  t[2] = m2;
+  t[3] = m3;
+}
 
 // TransformOne (dec.c.go:49-88) of a 4x4 block spread over a lane quad.  In: column q of
 // the coefficients (c0..c3 = in[q], in[4+q], in[8+q], in[12+q]).  Out: residuals
@@ -182,18 +211,7 @@ __device__ __forceinline__ void idct_quad(int q, uint2 cv, int r[4]) {
     t[2] = b - c;
     t[3] = a - d;
   }
-  {  // quad transpose: lane q ends with u[c] = tmp[4c + q]
-    const bool o1 = q & 1;
-    int g = dpp_swap1(o1 ? t[0] : t[1]);
-    if (o1) t[0] = g; else t[1] = g;
-    g = dpp_swap1(o1 ? t[2] : t[3]);
-    if (o1) t[2] = g; else t[3] = g;
-    const bool o2 = q & 2;
-    g = dpp_swap2(o2 ? t[0] : t[2]);
-    if (o2) t[0] = g; else t[2] = g;
-    g = dpp_swap2(o2 ? t[1] : t[3]);
-    if (o2) t[1] = g; else t[3] = g;
-  }
+  quad_transpose(t);  // lane q ends with t[c] = tmp[4c + q]
   const int dc = t[0] + 4;
   const int a = dc + t[2];
   const int b = dc - t[2];
