@@ -655,6 +655,20 @@ LOSSY_CASES = [
     ("wide_16383x17_simple", lambda: smooth(17, 16383, 23), {"filter_type": 0, "quality": 50}),
 ]
 
+# Narrow and tall frames for K1's quad geometry (4 MB rows per wave, 12 waves): one MB column
+# (the first MB is also the last), partial last quads (mb_h % 4 = 1..3), more quads than waves
+# (the progress ring wraps), i4-heavy content under both filters.  Generated by the
+# "lossy_extra" section, which adds to the lossy fixtures without re-encoding the others.
+LOSSY_EXTRA_CASES = [
+    ("synth_16x200", lambda: synth(200, 16, 24, 6), {}),
+    ("noise_9x300_complex", lambda: noise(300, 9, 25), {"filter_strength": 80}),
+    ("noise_40x336", lambda: noise(336, 40, 26), {"sharpness": 2}),
+    ("smooth_24x1000_simple", lambda: smooth(1000, 24, 27), {"filter_type": 0, "filter_strength": 70}),
+    ("noise_33x1000", lambda: noise(1000, 33, 28, 40), {"filter_strength": 60}),
+    ("synth_600x70", lambda: synth(70, 600, 29, 10), {}),
+    ("noise_250x100_q30", lambda: noise(100, 250, 30, 50), {"quality": 30, "filter_strength": 90}),
+]
+
 LOSSLESS_CASES = [
     ("ll_corr_64x64", lambda: corr_luma(64, 64, 1), {"method": 4}),
     ("ll_corr_123x77", lambda: corr_luma(77, 123, 2), {"method": 6, "quality": 100}),
@@ -703,9 +717,9 @@ def sha(a):
 
 
 def main(argv):
-    """argv: sections to (re)generate among lossy, lossless, alpha, bench (default: all);
+    """argv: sections to (re)generate among lossy, lossy_extra, lossless, alpha, modes, anim, bench (default: all);
     the manifest entries of the other sections are kept."""
-    sections = set(argv) or {"lossy", "lossless", "alpha", "modes", "anim", "bench"}
+    sections = set(argv) or {"lossy", "lossy_extra", "lossless", "alpha", "modes", "anim", "bench"}
     os.makedirs(os.path.join(HERE, "lossy"), exist_ok=True)
     os.makedirs(os.path.join(HERE, "lossless"), exist_ok=True)
     os.makedirs(os.path.join(HERE, "bench"), exist_ok=True)
@@ -716,7 +730,10 @@ def main(argv):
         manifest[sec] = {}
     if "alpha" in sections:
         manifest["alpha_errors"] = {}
-    for name, fn, kw in LOSSY_CASES if "lossy" in sections else []:
+    extra = LOSSY_EXTRA_CASES if "lossy_extra" in sections else []
+    manifest.pop("lossy_extra", None)
+    manifest.setdefault("lossy", {})
+    for name, fn, kw in (LOSSY_CASES if "lossy" in sections else []) + extra:
         img = fn()
         data = encode(img, **kw)
         r = decode_all(data, lossy=True)
