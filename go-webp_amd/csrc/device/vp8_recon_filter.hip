@@ -805,8 +805,11 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
               const uint32_t s = __builtin_amdgcn_sad_u8(ld32(org - BPS), 0, 0);
               v = (int)(s + org[-1] + org[BPS - 1] + org[2 * BPS - 1] + org[3 * BPS - 1] + 4) >> 3;
             } else {
-              const int avg3 = (a + 2 * b + c + 2) >> 2;
-              const int avg2 = (a + b + 1) >> 1;
+              // v_lerp_u8 averages bytes, rounding up where its third operand's bit is set:
+              // AVG2 = (a + b + 1) >> 1 in one instruction, AVG3 = (a + 2b + c + 2) >> 2 =
+              // (((a + c) >> 1) + b + 1) >> 1 in two (exact: tests/test_oracle.py::test_avg3_lerp_identity)
+              const int avg3 = (int)__builtin_amdgcn_lerp(__builtin_amdgcn_lerp(a, c, 0u), b, 1u);
+              const int avg2 = (int)__builtin_amdgcn_lerp(a, b, 1u);
               const int tm = clamp255(a + b - c);
               v = (kind & 2) ? tm : (kind & 1) ? avg2 : avg3;
             }

@@ -82,6 +82,13 @@ def _transform(coeffs, code, pred):
     return dst[:, :4].copy()
 
 
+def test_avg3_lerp_identity():
+    """K1's i4 AVG3 (dec.c.go AVG3, (a + 2b + c + 2) >> 2) as two v_lerp_u8 byte averages:
+    floor average of a and c, then the rounding-up average with b -- exact for all bytes."""
+    a, b, c = np.meshgrid(np.arange(256), np.arange(256), np.arange(256), indexing="ij")
+    np.testing.assert_array_equal((((a + c) >> 1) + b + 1) >> 1, (a + 2 * b + c + 2) >> 2)
+
+
 def test_transform_shortcuts_exact():
     """TransformAC3 / TransformDC == TransformOne on their coefficient patterns
     (dec.c.go:49-126): the device may always run TransformOne."""
