@@ -57,6 +57,19 @@ typedef uint32_t uint32x4_t __attribute__((ext_vector_type(4)));
 [[maybe_unused]] constexpr int kK3Sections = 10;
 #ifdef WG_K3_SECTION_TIMING
 __device__ unsigned long long g_k3_sections[kK3Sections];
+// per frame (workgroup) and band: start and end of the band's predictor loop (s_memrealtime)
+constexpr int kK3TimelineFrames = 1024, kK3TimelineBands = 64;
+__device__ unsigned long long g_k3_bands[kK3TimelineFrames][kK3TimelineBands + 1][2];
+#define K3_BAND_MARK(b, which)                                                              \
+  do {                                                                                      \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < kK3TimelineFrames && (b) < kK3TimelineBands) \
+      g_k3_bands[blockIdx.x][1 + (b)][which] = __builtin_amdgcn_s_memrealtime();           \
+  } while (0)
+#define K3_START_MARK()                                                                     \
+  do {                                                                                      \
+    if (threadIdx.x == 0 && blockIdx.x < kK3TimelineFrames)                                 \
+      g_k3_bands[blockIdx.x][0][0] = __builtin_amdgcn_s_memrealtime();                     \
+  } while (0)
 #define K3_SECT_DECL() uint64_t sect_acc[kK3Sections] = {}, sect_t = __builtin_amdgcn_s_memtime()
 #define K3_SECT(id)                                       \
   do {                                                    \
@@ -73,6 +86,8 @@ __device__ unsigned long long g_k3_sections[kK3Sections];
 #define K3_SECT_DECL() (void)0
 #define K3_SECT(id) (void)0
 #define K3_SECT_FLUSH() (void)0
+#define K3_BAND_MARK(b, which) (void)0
+#define K3_START_MARK() (void)0
 #endif
 
 // Per-byte a + b mod 256: add the low 7 bits of every byte (no carry can leave a byte),
@@ -273,6 +288,7 @@ __device__ __forceinline__ bool pred_wavefront(const Pass& P, int W, int H, int 
   uint8_t* my_lds = slot + lane * kSlotStride;
   K3_SECT_DECL();
   for (int b = wave; b < nbands; b += kWaves) {
+    K3_BAND_MARK(b, 0);
     const int y = b * kBand + lane;
     const bool row0 = y == 0;
     const int yc = min(y, H - 1);
@@ -469,6 +485,7 @@ __device__ __forceinline__ bool pred_wavefront(const Pass& P, int W, int H, int 
       }
       K3_SECT(9);
     }
+    K3_BAND_MARK(b, 1);
   }
   K3_SECT_FLUSH();
   return !aborted;
@@ -487,6 +504,7 @@ __global__ void __launch_bounds__(1024) vp8l_transforms_kernel(const LLDesc* __r
   uint32_t* cc_tab = reinterpret_cast<uint32_t*>(lds + kRingBytes + kModeTabMax);
   uint8_t* slots = lds + kRingBytes + kModeTabMax + kCCTabMax * 4;
   const int W = F.width, H = F.height, n = F.n_stages;
+  K3_START_MARK();
 
   int i = 0, w_in = F.coded_width;
   const uint32_t* src = F.coded;
@@ -594,6 +612,13 @@ __global__ void __launch_bounds__(1024) vp8l_transforms_kernel(const LLDesc* __r
 size_t vp8l_lds_bytes() { return kLdsBytes; }
 
 #ifdef WG_K3_SECTION_TIMING
+extern "C" int wg_debug_k3_bands(unsigned long long* out, int n_frames) {
+  if (n_frames > kK3TimelineFrames) n_frames = kK3TimelineFrames;
+  const size_t bytes = (size_t)n_frames * (kK3TimelineBands + 1) * 2 * sizeof(unsigned long long);
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_k3_bands), bytes) != hipSuccess) return -1;
+  return n_frames;
+}
+
 extern "C" int wg_debug_k3_sections(unsigned long long* out, int n, int reset) {
   if (n > kK3Sections) n = kK3Sections;
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_k3_sections), n * sizeof(unsigned long long)) != hipSuccess) return -1;

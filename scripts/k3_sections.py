@@ -48,6 +48,21 @@ def main():
     print(f"workload {args.workload} batch {args.batch} runs {args.runs}: K3 {ms[2]:.3f} ms")
     for n, v in sorted(zip(NAMES, buf), key=lambda t: -t[1]):
         print(f"  {n:10s} {100.0 * v / tot:6.2f}%  {v / args.runs / 1e6:10.1f} Mcyc/run")
+    # per band: start / end of its loop, % of the frame span (last run, mean over frames)
+    import numpy as np
+    L.wg_debug_k3_bands.restype = C.c_int
+    L.wg_debug_k3_bands.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
+    nf = min(args.batch, 1024)
+    buf2 = (C.c_ulonglong * (nf * 65 * 2))()
+    L.wg_debug_k3_bands(buf2, nf)
+    t = np.frombuffer(buf2, dtype=np.uint64).reshape(nf, 65, 2).astype(np.int64)
+    t0 = t[:, 0, 0]
+    nb = int((t[0, 1:, 1] > 0).sum())
+    st, en = t[:, 1:1 + nb, 0] - t0[:, None], t[:, 1:1 + nb, 1] - t0[:, None]
+    span = en.max(1)
+    print(f"  frame span {span.mean() / 100:.1f} us; band start-end, % of span:")
+    print("   " + " ".join(f"{k}:{100 * (st[:, k] / span).mean():.0f}-{100 * (en[:, k] / span).mean():.0f}"
+                          for k in range(nb)))
     b.close()
     ctx.close()
 
