@@ -25,6 +25,7 @@
 // predictor output).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <type_traits>
 
 #include "../device_format.h"
 #include "kernels.h"
@@ -387,8 +388,10 @@ __device__ __forceinline__ bool pred_wavefront(const Pass& P, int W, int H, int 
 
     uint32_t o_prev = 0, t1 = 0, t2 = 0, first = 0;  // L; TR of the last two steps (= T, TL)
     // one chunk (cl = 0/1 within its group): inputs from the slot, outputs back to it
-    auto chunk = [&](const int c, const int cl) {
-      const bool interior = c >= c_lo && c <= c_hi;
+    // kInterior (std::true_type / false_type): every lane's columns inside [1, W-2], so the
+    // per-step frame-edge logic compiles out (two instantiations of the chunk)
+    auto chunk_impl = [&](const int c, const int cl, auto kInterior) {
+      constexpr bool interior = decltype(kInterior)::value;
       const uint32x4_t in0 = *reinterpret_cast<const uint32x4_t*>(my_lds + 32 * cl);
       const uint32x4_t in1 = *reinterpret_cast<const uint32x4_t*>(my_lds + 32 * cl + 16);
       uint32_t ccw[kChunk];
@@ -467,6 +470,10 @@ __device__ __forceinline__ bool pred_wavefront(const Pass& P, int W, int H, int 
         __hip_atomic_store(prog + (b & (kWaves - 1)), ((uint32_t)b << 16) | (uint32_t)min(c * kChunk + kChunk, steps),
                            __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       K3_SECT(5);
+    };
+    auto chunk = [&](const int c, const int cl) {
+      if (c >= c_lo && c <= c_hi) chunk_impl(c, cl, std::true_type{});
+      else chunk_impl(c, cl, std::false_type{});
     };
     load_pair(0);
     stage_half(false);
