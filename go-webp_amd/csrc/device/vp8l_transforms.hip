@@ -169,13 +169,24 @@ __device__ __forceinline__ int cdelta(int t, int c) {  // ColorTransformDelta on
 __device__ __forceinline__ uint32_t cross_color_inv(uint32_t argb, uint32_t m) {
   const int g = (int)((argb >> 8) & 0xff);
   int r = (int)((argb >> 16) & 0xff), b = (int)(argb & 0xff);
-  r = (r + cdelta((int)(m & 0xff), g)) & 0xff;
-  b = (b + cdelta((int)((m >> 8) & 0xff), g) + cdelta((int)((m >> 16) & 0xff), r)) & 0xff;
-  return (argb & 0xff00ff00u) | ((uint32_t)r << 16) | (uint32_t)b;
+  r = r + cdelta((int)(m & 0xff), g);  // only the low byte is kept
+  b = b + cdelta((int)((m >> 8) & 0xff), g) + cdelta((int)((m >> 16) & 0xff), r & 0xff);
+  // the low bytes of r and b into bytes 2 and 0 of argb: two v_perm instead of masks + shifts
+  const uint32_t t = __builtin_amdgcn_perm((uint32_t)r, argb, 0x03040100u);
+  return __builtin_amdgcn_perm((uint32_t)b, t, 0x03020104u);
 }
 __device__ __forceinline__ uint32_t add_green(uint32_t argb) {
   const uint32_t g = (argb >> 8) & 0xff;
   return (argb & 0xff00ff00u) | (((argb & 0x00ff00ffu) + ((g << 16) | g)) & 0x00ff00ffu);
+}
+// VP8LAddGreenToBlueAndRed of one pixel with the output byte order folded into the final
+// v_perm: bytes 0 and 2 of x are blue + green and red + green (the 0x00ff00ff mask keeps a
+// byte-0 carry out of byte 2), bytes 1 and 3 (green, alpha) come from the input.  sel =
+// 0x03060104 keeps ARGB (B,G,R,A in memory), 0x03040106 swaps to R,G,B,A.
+__device__ __forceinline__ uint32_t add_green_emit(uint32_t argb, uint32_t sel) {
+  const uint32_t gg = __builtin_amdgcn_perm(argb, argb, 0x0c010c01u);  // green in bytes 0 and 2
+  const uint32_t x = (argb & 0x00ff00ffu) + gg;
+  return __builtin_amdgcn_perm(x, argb, sel);
 }
 __device__ __forceinline__ uint32_t bgra_to_rgba(uint32_t c) {
   return __builtin_amdgcn_perm(c, c, 0x07040506u);  // bytes B,G,R,A -> R,G,B,A
@@ -387,6 +398,10 @@ __device__ __forceinline__ bool pred_wavefront(const Pass& P, int W, int H, int 
     };
 
     uint32_t o_prev = 0, t1 = 0, t2 = 0, first = 0;  // L; TR of the last two steps (= T, TL)
+    // v_perm selectors of the chunk outputs: add-green's result bytes with RGBA (last pass)
+    // or ARGB (scratch) order, and the plain RGBA / identity swizzle
+    const uint32_t out_sel = last ? 0x03040106u : 0x03060104u;
+    const uint32_t out_sel0 = last ? 0x07040506u : 0x07060504u;
     // one chunk (cl = 0/1 within its group): inputs from the slot, outputs back to it
     // kInterior (std::true_type / false_type): every lane's columns inside [1, W-2], so the
     // per-step frame-edge logic compiles out (two instantiations of the chunk)
@@ -460,9 +475,15 @@ __device__ __forceinline__ bool pred_wavefront(const Pass& P, int W, int H, int 
       uint32_t f[kChunk];
 #pragma unroll
       for (int k = 0; k < kChunk; ++k) {
-        f[k] = GENERIC ? post_ops(P, cc_tab, ov[k], min(max(c * kChunk + k - 2 * lane, 0), W - 1), yc)
-                       : ops_ct<POST>(ov[k], ccw[k]);
-        if (last) f[k] = bgra_to_rgba(f[k]);
+        if constexpr (!GENERIC && POST == 2) {
+          f[k] = add_green_emit(ov[k], out_sel);  // add-green and the output byte order in one
+        } else if constexpr (!GENERIC && POST == 0) {
+          f[k] = __builtin_amdgcn_perm(ov[k], ov[k], out_sel0);
+        } else {
+          f[k] = GENERIC ? post_ops(P, cc_tab, ov[k], min(max(c * kChunk + k - 2 * lane, 0), W - 1), yc)
+                         : ops_ct<POST>(ov[k], ccw[k]);
+          if (last) f[k] = bgra_to_rgba(f[k]);
+        }
       }
       *reinterpret_cast<uint32x4_t*>(my_lds + 32 * cl) = uint32x4_t{f[0], f[1], f[2], f[3]};
       *reinterpret_cast<uint32x4_t*>(my_lds + 32 * cl + 16) = uint32x4_t{f[4], f[5], f[6], f[7]};
