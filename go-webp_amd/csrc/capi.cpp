@@ -1256,7 +1256,8 @@ int wg_yuv420_to_rgba_device(const uint8_t* y, const uint8_t* u, const uint8_t* 
   if (!y || !u || !v || !rgba || width <= 0 || height <= 0 || rgba_stride < 4 * width ||
       y_stride < ((width + 15) & ~15) || uv_stride < ((((width + 1) >> 1) + 7) & ~7) || (y_stride & 15) ||
       (uv_stride & 3) || (reinterpret_cast<uintptr_t>(y) & 15) || (reinterpret_cast<uintptr_t>(u) & 3) ||
-      (reinterpret_cast<uintptr_t>(v) & 3))
+      (reinterpret_cast<uintptr_t>(v) & 3) ||
+      (int64_t)rgba_stride * height > INT32_MAX)  // the emitter addresses the RGBA with 32-bit offsets
     return WG_STATUS_INVALID_PARAM;
   FrameDesc d{};
   d.y = const_cast<uint8_t*>(y);

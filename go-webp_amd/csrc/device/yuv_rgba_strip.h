@@ -167,15 +167,21 @@ __device__ __forceinline__ u32x4 convert_group(uint32_t nu, uint32_t fu, uint32_
   return u32x4{a.x, a.y, b.x, b.y};
 }
 
-__device__ __forceinline__ void store_group(gptr<uint8_t> dst, u32x4 px, int nvalid, bool aligned) {
+// RGBA stores go through a buffer descriptor over the frame's RGBA (32-bit offsets: no 64-bit
+// address arithmetic per store).  kAux = cache policy of the full 16-byte stores (buffer aux
+// bits): K2 streams them non-temporally (2 = nt; sc1 measured 2.43 vs 2.36 ms on c3), K1's
+// tail writes them through (16 = sc1: the lines leave the L2 at once instead of competing
+// with the reconstruction's working set; c3 K1 7.71 vs 7.77 ms, same call).
+constexpr int kAuxNt = 2, kAuxSc1 = 16;
+template <int kAux>
+__device__ __forceinline__ void store_group(__amdgpu_buffer_rsrc_t o, uint32_t off, u32x4 px, int nvalid, bool aligned) {
   if (aligned && nvalid >= 4) {
-    __builtin_nontemporal_store(px, reinterpret_cast<gptr<u32x4>>(dst));
+    __builtin_amdgcn_raw_buffer_store_b128(px, o, off, 0, kAux);
   } else {
-    gptr<uint32_t> d = reinterpret_cast<gptr<uint32_t>>(dst);
-    if (nvalid > 0) d[0] = px.x;
-    if (nvalid > 1) d[1] = px.y;
-    if (nvalid > 2) d[2] = px.z;
-    if (nvalid > 3) d[3] = px.w;
+    if (nvalid > 0) __builtin_amdgcn_raw_buffer_store_b32(px.x, o, off, 0, 0);
+    if (nvalid > 1) __builtin_amdgcn_raw_buffer_store_b32(px.y, o, off + 4, 0, 0);
+    if (nvalid > 2) __builtin_amdgcn_raw_buffer_store_b32(px.z, o, off + 8, 0, 0);
+    if (nvalid > 3) __builtin_amdgcn_raw_buffer_store_b32(px.w, o, off + 12, 0, 0);
   }
 }
 
@@ -188,7 +194,7 @@ __device__ __forceinline__ int n_bands(int H, bool fancy) {
   return (npairs + kPairs - 1) / kPairs;
 }
 
-template <bool kFancy>
+template <bool kFancy, int kAux>
 __device__ __forceinline__ void convert_strip(const FrameDesc& F, int tx, int band, int lane) {
   const int W = F.width, H = F.height;
   const int uv_w = (W + 1) >> 1, uv_h = (H + 1) >> 1;
@@ -198,8 +204,8 @@ __device__ __forceinline__ void convert_strip(const FrameDesc& F, int tx, int ba
   const gptr<const uint8_t> Y = as_global(static_cast<const uint8_t*>(F.y));
   const gptr<const uint8_t> U = as_global(static_cast<const uint8_t*>(F.u));
   const gptr<const uint8_t> V = as_global(static_cast<const uint8_t*>(F.v));
-  const gptr<uint8_t> out = as_global(F.rgba);
   const int ys = F.y_stride, uvs = F.uv_stride, os = F.rgba_stride;
+  const __amdgpu_buffer_rsrc_t out = __builtin_amdgcn_make_buffer_rsrc(F.rgba, 0, os * H, 0x00020000);
 
   auto load_luma = [&](int row, uint32_t yw[kGroups]) {
 #pragma unroll
@@ -232,10 +238,10 @@ __device__ __forceinline__ void convert_strip(const FrameDesc& F, int tx, int ba
         const int nvalid = W - x;
         if (nvalid <= 0) continue;
         if (ya >= 0)  // near = chroma row p-1, far = row p
-          store_group(out + (size_t)ya * os + 4 * x, convert_group(wp.u[k], wc.u[k], wp.v[k], wc.v[k], yA[k]), nvalid,
+          store_group<kAux>(out, (uint32_t)(ya * os + 4 * x), convert_group(wp.u[k], wc.u[k], wp.v[k], wc.v[k], yA[k]), nvalid,
                       aligned);
         if (yb < H)  // near = chroma row p, far = row p-1
-          store_group(out + (size_t)yb * os + 4 * x, convert_group(wc.u[k], wp.u[k], wc.v[k], wp.v[k], yB[k]), nvalid,
+          store_group<kAux>(out, (uint32_t)(yb * os + 4 * x), convert_group(wc.u[k], wp.u[k], wc.v[k], wp.v[k], yB[k]), nvalid,
                       aligned);
       }
       wp = wc;
@@ -267,7 +273,7 @@ __device__ __forceinline__ void convert_strip(const FrameDesc& F, int tx, int ba
           const uint32_t yw = r ? yB[k] : yA[k];
           const uint2 a = yuv_to_rgba2(bytes2(yw, 0, 1), u0, v0), b = yuv_to_rgba2(bytes2(yw, 2, 3), u1, v1);
           const u32x4 px{a.x, a.y, b.x, b.y};
-          store_group(out + (size_t)yr * os + 4 * x, px, nvalid, aligned);
+          store_group<kAux>(out, (uint32_t)(yr * os + 4 * x), px, nvalid, aligned);
         }
       }
     }

@@ -24,7 +24,7 @@ __global__ void __launch_bounds__(64 * kWavesPerWG) yuv_to_rgba_kernel(const Fra
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int sx = strip::strips_x(F.width);
   const int tx = blockIdx.x % sx, ty = blockIdx.x / sx;
-  strip::convert_strip<kFancy>(F, tx, ty * kWavesPerWG + wave, lane);
+  strip::convert_strip<kFancy, strip::kAuxNt>(F, tx, ty * kWavesPerWG + wave, lane);
 }
 
 }  // namespace
