@@ -376,10 +376,12 @@ __device__ __forceinline__ bool pred_wavefront(const Pass& P, int W, int H, int 
     };
     // modes and cross-color words of chunk c: all reads issued back to back (column
     // clamped into the frame), the fixed modes of row 0 / column 0 applied afterwards
-    auto fetch_tables = [&](int c, int* md, uint32_t* cw) {
+    // (interior chunks: every lane's columns lie inside the frame, no clamp)
+    auto fetch_tables = [&](int c, int* md, uint32_t* cw, auto kInterior) {
 #pragma unroll
       for (int k = 0; k < kChunk; ++k) {
-        const int x = min(max(c * kChunk + k - 2 * lane, 0), W - 1);
+        const int xr = c * kChunk + k - 2 * lane;
+        const int x = decltype(kInterior)::value ? xr : min(max(xr, 0), W - 1);
         if (GENERIC && !P.m_in_lds)
           md[k] = (int)((P.m_g[mrow + (x >> P.m_bits)] >> 8) & 0xf);
         else
@@ -411,7 +413,7 @@ __device__ __forceinline__ bool pred_wavefront(const Pass& P, int W, int H, int 
       const uint32x4_t in1 = *reinterpret_cast<const uint32x4_t*>(my_lds + 32 * cl + 16);
       uint32_t ccw[kChunk];
       int md[kChunk];
-      fetch_tables(c, md, ccw);
+      fetch_tables(c, md, ccw, kInterior);
       K3_SECT(0);
       // band b-1 must be 135 steps ahead of this chunk's end (its last row, lane 63, then
       // covers column x+1 of lane 0); band b+1 must have consumed the ring columns this
