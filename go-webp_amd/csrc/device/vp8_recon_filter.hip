@@ -908,8 +908,17 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
         const u32x4 vy = {ld32(sy), ld32(sy + 4), ld32(sy + 8), ld32(sy + 12)};
         const u32x2 vc = {ld32(sc), ld32(sc + 4)};
         const uint32_t ux = (uint32_t)x;
+        // (measurement builds WG_ABL_PLANES_Y / _C drop the luma / chroma stores: DESIGN.md §4)
+#ifndef WG_ABL_PLANES_Y
         const uint32_t oy = act ? sb_y + (ux << 4) + wcy : kDrop;
+#else
+        const uint32_t oy = kDrop;
+#endif
+#ifndef WG_ABL_PLANES_C
         const uint32_t oc = act ? sb_c + (ux << 3) + wcc : kDrop;
+#else
+        const uint32_t oc = kDrop;
+#endif
         __builtin_amdgcn_raw_buffer_store_b128(vy, planes, (int)oy, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b64(vc, planes, (int)oc, 0, 0);
         const int w0 = x == 0 ? 4 : 0;  // the own-row segments' window column
