@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Soak check of K1's RGBA tail (cross-wave plane hand-off): a full c3 batch (256 x 4K, the
-R = 12 path) run many times; after every run a sample of frames' RGBA is hashed against the
+R = 12 path; `soak_fused.py <runs> c2_1080p` for 1080p, whose last quad is full) run many times; after every run a sample of frames' RGBA is hashed against the
 libwebp 1.6.0 SHA-256 in the manifest.  Any mismatch (a converter reading a plane row before
 its stores landed) fails the script."""
 import hashlib
@@ -16,7 +16,7 @@ def main():
     import webp_amd
     from oracle_lib import bench_files, manifest
     runs = int(sys.argv[1]) if len(sys.argv) > 1 else 30
-    paths = bench_files("c3_4k")
+    paths = bench_files(sys.argv[2] if len(sys.argv) > 2 else "c3_4k")  # or c2_1080p
     m = manifest()["bench"]
     want = [m[os.path.basename(p)]["sha256"]["rgba"] for p in paths]
     datas = [open(p, "rb").read() for p in paths]
