@@ -56,18 +56,29 @@ __device__ __forceinline__ u16x2 sat_sub(u16x2 a, unsigned short c) { return __b
 __device__ __forceinline__ u16x2 sat_sub(u16x2 a, u16x2 b) { return __builtin_elementwise_sub_sat(a, b); }
 __device__ __forceinline__ u16x2 min255(u16x2 a) { return __builtin_elementwise_min(a, splat(255)); }
 
+// (a * 4) saturated at 0xffff, two 16-bit lanes in one v_pk_mad_u16 with clamp: its HIGH byte is
+// min(a >> 6, 255) -- the final `>> 6` + Clip8 in one instruction instead of a shift and a min
+// (tests/test_oracle.py::test_packed_yuv_formulas; on the device over all 2^24 (y, u, v):
+// tests/test_gpu_parity.py::test_yuv_to_rgba_device_every_yuv_triple).
+__device__ __forceinline__ uint32_t sat_x4(u16x2 a) {
+  uint32_t r;
+  asm("v_pk_mad_u16 %0, %1, %2, 0 clamp" : "=v"(r) : "v"(as_u32(a)), "s"(0x00040004u));
+  return r;
+}
+
 // VP8YuvToRgba (conversion.go:28-49, A = 0xff) of two pixels; y, u, v hold one 8-bit
 // sample per 16-bit half.  Returns the two RGBA dwords.
 __device__ __forceinline__ uint2 yuv_to_rgba2(u16x2 y, u16x2 u, u16x2 v) {
-  const u16x2 y1 = y * splat(74) + ((y * splat(133)) >> 8);                              // MultHi(y, 19077)
-  const u16x2 r = min255(sat_sub(y1 + v * splat(102) + ((v * splat(37)) >> 8), 14234) >> 6);  // + MultHi(v, 26149)
-  const u16x2 gu = u * splat(25) + ((u * splat(19)) >> 8);                               // MultHi(u, 6419)
-  const u16x2 gv = v * splat(52) + (v >> 5);                                             // MultHi(v, 13320)
-  const u16x2 g = min255(sat_sub(sat_sub(y1 + splat(8708), gu), gv) >> 6);
-  const u16x2 b = min255(sat_sub(y1 + u * splat(129) + ((u * splat(26)) >> 8), 17685) >> 6);  // + MultHi(u, 33050)
-  // bytes: t = R0 G0 R1 G1; px = R G B 0xff (perm selector 0x0d = 0xff)
-  const uint32_t t = __builtin_amdgcn_perm(as_u32(g), as_u32(r), 0x06020400u);
-  return make_uint2(__builtin_amdgcn_perm(as_u32(b), t, 0x0d040100u), __builtin_amdgcn_perm(as_u32(b), t, 0x0d060302u));
+  const u16x2 y1 = y * splat(74) + ((y * splat(133)) >> 8);                            // MultHi(y, 19077)
+  const uint32_t r = sat_x4(sat_sub(y1 + v * splat(102) + ((v * splat(37)) >> 8), 14234));  // + MultHi(v, 26149)
+  const u16x2 gu = u * splat(25) + ((u * splat(19)) >> 8);                             // MultHi(u, 6419)
+  const u16x2 gv = v * splat(52) + (v >> 5);                                           // MultHi(v, 13320)
+  const uint32_t g = sat_x4(sat_sub(sat_sub(y1 + splat(8708), gu), gv));
+  const uint32_t b = sat_x4(sat_sub(y1 + u * splat(129) + ((u * splat(26)) >> 8), 17685));  // + MultHi(u, 33050)
+  // the channel values are the high bytes of the 16-bit lanes: t = R0 G0 R1 G1; px = R G B 0xff
+  // (perm selector 0x0d = 0xff)
+  const uint32_t t = __builtin_amdgcn_perm(g, r, 0x07030501u);
+  return make_uint2(__builtin_amdgcn_perm(b, t, 0x0d050100u), __builtin_amdgcn_perm(b, t, 0x0d070302u));
 }
 
 // bytes i and j of w as the two 16-bit halves
@@ -205,7 +216,15 @@ __device__ __forceinline__ void convert_strip(const FrameDesc& F, int tx, int ba
   const gptr<const uint8_t> U = as_global(static_cast<const uint8_t*>(F.u));
   const gptr<const uint8_t> V = as_global(static_cast<const uint8_t*>(F.v));
   const int ys = F.y_stride, uvs = F.uv_stride, os = F.rgba_stride;
-  const __amdgpu_buffer_rsrc_t out = __builtin_amdgcn_make_buffer_rsrc(F.rgba, 0, os * H, 0x00020000);
+  // (the descriptor from readfirstlane'd values: F is one frame per workgroup, but where the
+  // compiler cannot prove it uniform (K2 picks `single` or frames[y]) a VGPR descriptor
+  // would wrap every store in a readfirstlane waterfall loop)
+  const uint64_t ob = reinterpret_cast<uint64_t>(F.rgba);
+  const uint32_t ob_hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(ob >> 32));
+  const uint32_t ob_lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)ob);  // (unsigned: no sign extension)
+  uint8_t* const obase = reinterpret_cast<uint8_t*>(((uint64_t)ob_hi << 32) | ob_lo);
+  const __amdgpu_buffer_rsrc_t out =
+      __builtin_amdgcn_make_buffer_rsrc(obase, 0, __builtin_amdgcn_readfirstlane(os * H), 0x00020000);
 
   auto load_luma = [&](int row, uint32_t yw[kGroups]) {
 #pragma unroll

@@ -86,3 +86,22 @@ def test_no_cpu_fallback_without_gpu():
     assert e.value.status == webp_amd.Status.UNSUPPORTED_FEATURE
     with pytest.raises(webp_amd.WebPError):
         webp_amd.Context(0)
+
+
+def test_yuv_stage_entry_rejects_bad_geometry_before_any_device_call():
+    """wg_yuv420_to_rgba_device validates its arguments on the host (no device access, so it
+    runs without a GPU): strides below the row sizes, misaligned planes, and an RGBA extent
+    beyond the emitter's 32-bit offsets are INVALID_PARAM."""
+    p = 1 << 20  # aligned dummy addresses: never dereferenced on these paths
+    bad = [
+        dict(w=16, h=16, ys=8, uvs=8, rs=64),           # y_stride < width
+        dict(w=16, h=16, ys=16, uvs=4, rs=64),          # uv_stride < chroma width
+        dict(w=16, h=16, ys=16, uvs=8, rs=32),          # rgba_stride < 4 * width
+        dict(w=16, h=16, ys=24, uvs=8, rs=64),          # y_stride not a multiple of 16
+        dict(w=4096, h=16383, ys=4096, uvs=2048, rs=1 << 17),  # rgba_stride * height > INT32_MAX
+        dict(w=0, h=16, ys=16, uvs=8, rs=64),
+    ]
+    for a in bad:
+        with pytest.raises(webp_amd.WebPError) as e:
+            webp_amd.yuv420_to_rgba_device(p, p, p, a["ys"], a["uvs"], p, a["rs"], a["w"], a["h"], True, None)
+        assert e.value.status == webp_amd.Status.INVALID_PARAM, a

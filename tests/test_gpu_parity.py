@@ -158,6 +158,48 @@ def test_yuv_to_rgba_device_stage_vs_oracle():
             np.testing.assert_array_equal(out.cpu().numpy(), ref, err_msg=f"{h}x{w} fancy={fancy}")
 
 
+def test_yuv_to_rgba_device_every_yuv_triple():
+    """The device's packed 16-bit VP8YuvToRgba over ALL 2^24 (y, u, v): a 4096 x 4096 frame
+    whose 2x2 blocks hold every (u, v) pair 64 times and, across those 64 blocks, every y.
+    Point sampling gives each pixel exactly its block's (u, v), so the RGBA must equal
+    conversion.go:28-49 (MultHi, Clip8) evaluated in numpy; the same planes fancy-upsampled
+    must equal the oracle."""
+    import torch
+    n = 4096
+    b = np.arange((n // 2) * (n // 2), dtype=np.int64).reshape(n // 2, n // 2)  # block index
+    U = ((b >> 14) & 255).astype(np.uint8)
+    V = ((b >> 6) & 255).astype(np.uint8)
+    Y = np.empty((n, n), np.uint8)
+    for dy in range(2):
+        for dx in range(2):
+            Y[dy::2, dx::2] = (((b & 63) << 2) + 2 * dy + dx).astype(np.uint8)
+    dY, dU, dV = (torch.from_numpy(a).cuda() for a in (Y, U, V))
+    out = torch.zeros((n, n, 4), dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    webp_amd.yuv420_to_rgba_device(dY.data_ptr(), dU.data_ptr(), dV.data_ptr(), n, n // 2, out.data_ptr(), 4 * n, n,
+                                   n, False, stream)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    y = Y.astype(np.int64)
+    u = np.repeat(np.repeat(U, 2, 0), 2, 1).astype(np.int64)
+    v = np.repeat(np.repeat(V, 2, 0), 2, 1).astype(np.int64)
+    seen = np.zeros(1 << 24, bool)
+    seen[(y << 16 | u << 8 | v).ravel()] = True
+    assert seen.all()  # every (y, u, v) occurs
+
+    def clip8(x):
+        return np.clip(x >> 6, 0, 255)
+    y1 = (y * 19077) >> 8
+    np.testing.assert_array_equal(got[..., 0], clip8(y1 + ((v * 26149) >> 8) - 14234))
+    np.testing.assert_array_equal(got[..., 1], clip8(y1 - ((u * 6419) >> 8) - ((v * 13320) >> 8) + 8708))
+    np.testing.assert_array_equal(got[..., 2], clip8(y1 + ((u * 33050) >> 8) - 17685))
+    assert (got[..., 3] == 255).all()
+    webp_amd.yuv420_to_rgba_device(dY.data_ptr(), dU.data_ptr(), dV.data_ptr(), n, n // 2, out.data_ptr(), 4 * n, n,
+                                   n, True, stream)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out.cpu().numpy(), oracle_yuv_to_rgba(Y, U, V, fancy=True))
+
+
 def test_wide_frames_global_column_store(ctx):
     """Frames wider than K1's LDS column store (mb_w > 600, up to VP8's 16383 px) take the
     global-store K1 variant: alone, interleaved with narrow frames (both variants launched on

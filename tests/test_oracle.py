@@ -188,6 +188,9 @@ def test_packed_yuv_formulas():
     np.testing.assert_array_equal(b, B)
     a = 3 * 255 + 255
     assert 3 * a + a + 8 < 65536
+    # the final `>> 6` + Clip8 as the high byte of a saturating x4 (v_pk_mad_u16 ... clamp)
+    x = np.arange(65536)
+    np.testing.assert_array_equal(np.minimum(4 * x, 65535) >> 8, np.minimum(x >> 6, 255))
 
 
 def test_bench_c1_frame_sha256():
