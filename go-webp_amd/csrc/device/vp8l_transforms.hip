@@ -152,7 +152,11 @@ __device__ __forceinline__ uint32_t predict(int mode, uint32_t L, uint32_t T, ui
 // modes, skipped when none is.
 __device__ __forceinline__ uint32_t predict_fast(int m, uint32_t L, uint32_t T, uint32_t TL, uint32_t TR) {
   uint32_t p = avg2(avg2(L, TL), avg2(T, TR));
+#ifdef WG_ABL_K3_FAST  // measurement only: every pixel takes the mode-10 predictor (output wrong)
+  if (false) {
+#else
   if (__any(m != 10)) {
+#endif
     const uint32_t cp = (m & 1) ? ((m & 2) ? TR : L) : ((m & 2) ? T : TL);  // 1 L, 2 T, 3 TR, 4 TL
     p = (unsigned)(m - 1) < 4u ? cp : p;
     const bool rest = ((unsigned)(m - 1) >= 4u) & (m != 10);
@@ -254,6 +258,10 @@ __device__ __forceinline__ uint32_t post_ops(const Pass& P, const uint32_t* cc_l
 // cross-color tile word.
 template <int OPS>
 __device__ __forceinline__ uint32_t ops_ct(uint32_t v, uint32_t ccw) {
+#ifdef WG_ABL_K3_NOCC  // measurement only: cross-color skipped (output wrong)
+  if (OPS == 1) return v;
+  if (OPS == 3) return add_green(v);
+#endif
   if (OPS == 1) return cross_color_inv(v, ccw);
   if (OPS == 2) return add_green(v);
   if (OPS == 3) return add_green(cross_color_inv(v, ccw));
