@@ -146,22 +146,46 @@ __device__ __forceinline__ uint32_t predict(int mode, uint32_t L, uint32_t T, ui
   }
 }
 
-// Per-lane predictor with the common modes cheap: ClampedAverage of four (mode 10, most
-// tiles of a natural image) for every lane; the copies 1..4 by a two-level select on the
-// mode bits when some lane uses them; the per-lane switch only for lanes on the remaining
-// modes, skipped when none is.
-__device__ __forceinline__ uint32_t predict_fast(int m, uint32_t L, uint32_t T, uint32_t TL, uint32_t TR) {
+// Predictor modes as staged for the steps (enc_mode): 0 = mode 10 (ClampedAverage of four, most
+// tiles of a natural image); the copies 1..4 = 4 | sel with sel's bits choosing
+// b1 ? (b0 ? TR : T) : (b0 ? L : TL); every other mode = 0x80 | mode << 3.
+__device__ __forceinline__ int enc_mode(int m) {
+  if (m == 10) return 0;
+  if (m >= 1 && m <= 4) return 4 | (m & 3);
+  return 0x80 | (m << 3);
+}
+// v_bfi_b32: bitwise mask ? a : b.  One-bit field of e sign-extended to a full mask: v_bfe_i32.
+// (Inline asm: written as C, the compiler turns the masks back into compares + v_cndmask.)
+__device__ __forceinline__ uint32_t bitsel(uint32_t mask, uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(mask), "v"(a), "v"(b));
+  return r;
+}
+template <int kBit>
+__device__ __forceinline__ uint32_t bitmask(int e) {
+  uint32_t r;
+  asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(r) : "v"(e), "i"(kBit));
+  return r;
+}
+
+// Per-lane predictor with the common modes cheap: the ClampedAverage of four for every lane;
+// when some lane is on another mode, the copies by three bitwise selects on masks taken
+// straight from the encoded mode's bits (no compares: 7 instructions, the compare-and-select
+// form took 14), and the per-lane switch only on lanes with the remaining modes, skipped when
+// none is.
+__device__ __forceinline__ uint32_t predict_fast(int e, uint32_t L, uint32_t T, uint32_t TL, uint32_t TR) {
   uint32_t p = avg2(avg2(L, TL), avg2(T, TR));
 #ifdef WG_ABL_K3_FAST  // measurement only: every pixel takes the mode-10 predictor (output wrong)
   if (false) {
 #else
-  if (__any(m != 10)) {
+  if (__any(e != 0)) {
 #endif
-    const uint32_t cp = (m & 1) ? ((m & 2) ? TR : L) : ((m & 2) ? T : TL);  // 1 L, 2 T, 3 TR, 4 TL
-    p = (unsigned)(m - 1) < 4u ? cp : p;
-    const bool rest = ((unsigned)(m - 1) >= 4u) & (m != 10);
+    const uint32_t b0 = bitmask<0>(e);
+    const uint32_t cp = bitsel(bitmask<1>(e), bitsel(b0, TR, T), bitsel(b0, L, TL));
+    p = bitsel(bitmask<2>(e), cp, p);
+    const bool rest = (unsigned)e >= 0x80u;
     if (__any(rest)) {
-      if (rest) p = predict(m, L, T, TL, TR);
+      if (rest) p = predict((e >> 3) & 0xf, L, T, TL, TR);
     }
   }
   return p;
@@ -391,7 +415,7 @@ __device__ __forceinline__ bool pred_wavefront(const Pass& P, int W, int H, int 
         const int xr = c * kChunk + k - 2 * lane;
         const int x = decltype(kInterior)::value ? xr : min(max(xr, 0), W - 1);
         if (GENERIC && !P.m_in_lds)
-          md[k] = (int)((P.m_g[mrow + (x >> P.m_bits)] >> 8) & 0xf);
+          md[k] = enc_mode((int)((P.m_g[mrow + (x >> P.m_bits)] >> 8) & 0xf));
         else
           md[k] = mode_tab[mrow + (x >> P.m_bits)];
         if (kCC) cw[k] = cc_tab[crow + (x >> P.cc_bits)];
@@ -402,7 +426,7 @@ __device__ __forceinline__ bool pred_wavefront(const Pass& P, int W, int H, int 
 #pragma unroll
         for (int k = 0; k < kChunk; ++k) {
           const int xr = c * kChunk + k - 2 * lane;
-          md[k] = row0 ? (xr == 0 ? 0 : 1) : (xr == 0 ? 2 : md[k]);
+          md[k] = row0 ? (xr == 0 ? enc_mode(0) : enc_mode(1)) : (xr == 0 ? enc_mode(2) : md[k]);
         }
       }
     };
@@ -589,7 +613,7 @@ __global__ void __launch_bounds__(1024) vp8l_transforms_kernel(const LLDesc* __r
       const int nt = P.m_tpr * ((H + (1 << P.m_bits) - 1) >> P.m_bits);
       P.m_in_lds = nt <= kModeTabMax;
       if (P.m_in_lds)
-        for (int t = threadIdx.x; t < nt; t += blockDim.x) mode_tab[t] = (uint8_t)((P.m_g[t] >> 8) & 0xf);
+        for (int t = threadIdx.x; t < nt; t += blockDim.x) mode_tab[t] = (uint8_t)enc_mode((int)((P.m_g[t] >> 8) & 0xf));
     }
     if (threadIdx.x < kWaves) prog[threadIdx.x] = 0;
     __syncthreads();
