@@ -184,7 +184,11 @@ __device__ __forceinline__ uint32_t predict_fast(int e, uint32_t L, uint32_t T, 
     const uint32_t cp = bitsel(bitmask<1>(e), bitsel(b0, TR, T), bitsel(b0, L, TL));
     p = bitsel(bitmask<2>(e), cp, p);
     const bool rest = (unsigned)e >= 0x80u;
+#ifdef WG_ABL_K3_NOREST  // measurement only: modes other than 1..4 and 10 not predicted (output wrong)
+    if (false) {
+#else
     if (__any(rest)) {
+#endif
       if (rest) p = predict((e >> 3) & 0xf, L, T, TL, TR);
     }
   }
