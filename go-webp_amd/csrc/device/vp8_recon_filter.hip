@@ -909,7 +909,20 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
         const u32x2 vc = {ld32(sc), ld32(sc + 4)};
         const uint32_t ux = (uint32_t)x;
         // (measurement builds WG_ABL_PLANES_Y / _C drop the luma / chroma stores: DESIGN.md §4)
-#ifndef WG_ABL_PLANES_Y
+#if defined(WG_ABL_PLANES_Y64)  // measurement only: own luma rows as full 64-byte chunks (data wrong)
+        const uint32_t oy = act && tl ? sb_y + (ux << 4) + wcy : kDrop;
+        {
+          const bool fl = act && (x & 3) == 0 && x >= 4;
+          if (__any(fl)) {
+#pragma unroll
+            for (int A = 0; A < 4; ++A) {
+              const int r = 4 * A + (m >> 2);
+              const uint32_t o = fl && r < 13 ? (uint32_t)__mul24(16 * y + r, ys) + 16u * (ux - 4u) + 16u * (m & 3) : kDrop;
+              __builtin_amdgcn_raw_buffer_store_b128(vy, planes, (int)o, 0, 0);
+            }
+          }
+        }
+#elif !defined(WG_ABL_PLANES_Y)
         const uint32_t oy = act ? sb_y + (ux << 4) + wcy : kDrop;
 #else
         const uint32_t oy = kDrop;
