@@ -610,15 +610,10 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
       const bool act = row_ok && x >= 0 && x < mb_w;
       const bool last_x = x == mb_w - 1;
       K1_SECT(13);
-      // ---- software pipeline: record x+2 and coefficients x+1 in flight during MB x
+      // ---- software pipeline: record x+2 in flight during MB x; the coefficients of x+1 are
+      //      loaded into cc as soon as the IDCT has consumed x's (below)
       const MbRec rnn = load_rec(recs, mb_w, y, row_ok, x + 2);
       const uint32_t blk_next = blk + __builtin_popcount(rc.flags & kNzMask);
-      Coefs cn[2];
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const int r = m + 16 * s;
-        cn[s] = load_coefs(blks, rn.flags & kNzMask, blk_next, r >> 2, 16 + (r >> 2), q);
-      }
 
       K1_SECT(0);
       // ---- wait for the previous quad's last row (t = x + 2y wavefront)
@@ -712,6 +707,15 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
 #endif
       }
 
+      // coefficients of x+1 into the registers the IDCT just freed: no rotation copies at the loop
+      // latch (which waited there for these loads), and the loads are issued ahead of this step's
+      // plane stores -- gfx950's single in-order vmcnt makes a load complete only after every
+      // store issued before it, so issuing them here gives the previous step's stores more slack
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int r = m + 16 * s;
+        cc[s] = load_coefs(blks, rn.flags & kNzMask, blk_next, r >> 2, 16 + (r >> 2), q);
+      }
       K1_SECT(4);
       // ---- luma prediction + residual (role r: block column (r>>2)&3, pixel rows
       //      4*((r>>2)>>2)+q and that + 8)
@@ -984,8 +988,6 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
       K1_SECT(12);
       rc = rn;
       rn = rnn;
-      cc[0] = cn[0];
-      cc[1] = cn[1];
       blk = blk_next;
     }
     K1_QUAD_MARK(k, 1);
