@@ -6,7 +6,7 @@ TAG=${TAG:-r01}
 WL=${WL:-c3}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
-BENCH="python3 bench.py --workload $WL --steps ${STEPS:-3} --warmup 1 --no-cpu-baseline"
+BENCH="python3 bench.py --workload $WL --steps ${STEPS:-3} --warmup 1 --no-cpu-baseline --no-e2e"
 run() {  # run <name> <timeout> <rocprofv3 args...>
   local name=$1 to=$2; shift 2
   echo "=== $name"
