@@ -54,7 +54,6 @@ __device__ __forceinline__ uint32_t as_u32(u16x2 v) { return __builtin_bit_cast(
 __device__ __forceinline__ u16x2 splat(unsigned short c) { return u16x2{c, c}; }
 __device__ __forceinline__ u16x2 sat_sub(u16x2 a, unsigned short c) { return __builtin_elementwise_sub_sat(a, splat(c)); }
 __device__ __forceinline__ u16x2 sat_sub(u16x2 a, u16x2 b) { return __builtin_elementwise_sub_sat(a, b); }
-__device__ __forceinline__ u16x2 min255(u16x2 a) { return __builtin_elementwise_min(a, splat(255)); }
 
 // (a * 4) saturated at 0xffff, two 16-bit lanes in one v_pk_mad_u16 with clamp: its HIGH byte is
 // min(a >> 6, 255) -- the final `>> 6` + Clip8 in one instruction instead of a shift and a min
