@@ -130,6 +130,30 @@ def test_bad_frames_do_not_poison_batch(ctx):
     np.testing.assert_array_equal(outs[4], g["rgba"])
 
 
+def test_decode_batch_hundred_frames_with_bad_ones(ctx):
+    """wg_decode_rgba_batch over 100 frames (every opaque lossy fixture and the alpha frame, cycled,
+    with truncated frames in between): every good frame equals libwebp's RGBA and the statuses
+    land on the right frames."""
+    names = OPAQUE + ["alpha_64x48"]
+    good = [load_lossy(n) for n in names]
+    datas, want = [], []
+    for k in range(100):
+        if k % 23 == 7:
+            datas.append(good[0][0][: len(good[0][0]) // 3])  # truncated: fails in its chunk only
+            want.append(None)
+        else:
+            d, g = good[k % len(good)]
+            datas.append(d)
+            want.append(g["rgba"])
+    outs, status = ctx.decode_batch(datas)
+    for k, (o, w, s) in enumerate(zip(outs, want, status)):
+        if w is None:
+            assert s != 0, k
+        else:
+            assert s == 0, (k, s)
+            np.testing.assert_array_equal(o, w, err_msg=str(k))
+
+
 def test_lossy_alpha_frame_in_the_lossy_set(ctx):
     """VP8+ALPH: the lossy set's alpha frame decodes to libwebp's RGBA."""
     al, g = load_lossy("alpha_64x48")
