@@ -58,7 +58,10 @@ namespace {
 
 constexpr int kWaves = 16;
 constexpr int kRows = 4;       // MB rows per wave (a quad); 16 lanes per MB
-constexpr int kMaxRecon = 12;  // waves that may reconstruct: LDS slots for 4 x 12 MB rows
+#ifndef WG_K1_MAX_RECON
+#define WG_K1_MAX_RECON 12
+#endif
+constexpr int kMaxRecon = WG_K1_MAX_RECON;  // waves that may reconstruct: LDS slots for 4 x 12 MB rows
 constexpr int BPS = 32;        // libwebp workspace stride (vp8/constants.go BPS)
 constexpr int Y_OFF = BPS * 1 + 8;
 constexpr int U_OFF = Y_OFF + BPS * 16 + BPS;
