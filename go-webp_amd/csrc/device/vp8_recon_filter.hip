@@ -41,7 +41,7 @@
 // (VP8TopSamples), the final bottom rows `fbot` of each MB column for the next row's
 // top-edge filter, progress counters.  Every HBM byte of the Y/U/V planes is written
 // exactly once, when final.  MB records and coefficients are software-pipelined: record
-// x+2 and coefficients x+1 are in flight while MB x is processed.
+// x+2 is loaded at the top of MB x's step, the coefficients of x+1 right after x's IDCT.
 #include <hip/hip_runtime.h>
 #include <type_traits>
 #include <stdint.h>
