@@ -796,11 +796,14 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
           e[j] = tab[mode * 16 + m];
           rs[j] = res[bi * 16 + m];
         }
-        // blocks of equal t are independent: one LDS hand-off per t
+        // blocks of equal t are independent: one LDS hand-off per t.  The lane mask is set once
+        // for the whole walk (one exec save/restore instead of one per block: the chain is paced
+        // by each wave's instruction count, SALU included)
+        if (act && i4) {
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
           const int bi = kI4Order[j], bx = bi & 3, by = bi >> 2;
-          if (act && i4) {
+          {
             uint8_t* org = ws + Y_OFF + 4 * by * BPS + 4 * bx;
             const uint32_t ew = e[j];
             const int kind = ew >> 24;
@@ -823,6 +826,7 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
             org[ppy * BPS + ppx] = (uint8_t)clamp255(v + rs[j]);
           }
           if (j == 15 || kI4Step[j + 1] != kI4Step[j]) lds_sync();
+        }
         }
       }
 #endif
