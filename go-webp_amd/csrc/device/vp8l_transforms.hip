@@ -173,23 +173,32 @@ __device__ __forceinline__ uint32_t bitmask(int e) {
 // straight from the encoded mode's bits (no compares: 7 instructions, the compare-and-select
 // form took 14), and the per-lane switch only on lanes with the remaining modes, skipped when
 // none is.
+// kSel (chosen per chunk, see chunk_impl): 0 = every lane of the chunk on mode 10, 1 = mode 10 or
+// copies only (selects without the per-step checks), 2 = anything (per-step checks).  kMS: bit
+// position of the encoded mode in e (24 when it shares a word with the cross-color multipliers).
+template <int kSel, int kMS>
 __device__ __forceinline__ uint32_t predict_fast(int e, uint32_t L, uint32_t T, uint32_t TL, uint32_t TR) {
   uint32_t p = avg2(avg2(L, TL), avg2(T, TR));
+  if (kSel == 1) {
+    const uint32_t b0 = bitmask<kMS>(e);
+    const uint32_t cp = bitsel(bitmask<kMS + 1>(e), bitsel(b0, TR, T), bitsel(b0, L, TL));
+    return bitsel(bitmask<kMS + 2>(e), cp, p);
+  }
 #ifdef WG_ABL_K3_FAST  // measurement only: every pixel takes the mode-10 predictor (output wrong)
   if (false) {
 #else
-  if (__any(e != 0)) {
+  if (kSel == 2 && __any((unsigned)e >= (1u << kMS))) {
 #endif
-    const uint32_t b0 = bitmask<0>(e);
-    const uint32_t cp = bitsel(bitmask<1>(e), bitsel(b0, TR, T), bitsel(b0, L, TL));
-    p = bitsel(bitmask<2>(e), cp, p);
-    const bool rest = (unsigned)e >= 0x80u;
+    const uint32_t b0 = bitmask<kMS>(e);
+    const uint32_t cp = bitsel(bitmask<kMS + 1>(e), bitsel(b0, TR, T), bitsel(b0, L, TL));
+    p = bitsel(bitmask<kMS + 2>(e), cp, p);
+    const bool rest = (unsigned)e >= (0x80u << kMS);
 #ifdef WG_ABL_K3_NOREST  // measurement only: modes other than 1..4 and 10 not predicted (output wrong)
     if (false) {
 #else
     if (__any(rest)) {
 #endif
-      if (rest) p = predict((e >> 3) & 0xf, L, T, TL, TR);
+      if (rest) p = predict((int)(((unsigned)e >> (kMS + 3)) & 0xf), L, T, TL, TR);
     }
   }
   return p;
@@ -261,6 +270,7 @@ struct Pass {
   gptr<const uint32_t> cc_g;
   int m_bits, m_tpr, m_in_lds;
   gptr<const uint32_t> m_g;
+  int joint;               // modes staged in byte 3 of the cross-color words (pred_wavefront kMS)
 };
 
 __device__ __forceinline__ uint32_t cc_word(const Pass& P, const uint32_t* cc_lds, int x, int y) {
@@ -315,7 +325,11 @@ constexpr bool ops_cc(int ops) { return ops == 1 || ops == 3 || ops == 4; }
 // instead of 64 and every 64-byte row segment moves in one request.  The steps read
 // and overwrite the slot transposed (lane = row).  Inputs of group g+1 are in flight in
 // registers while group g computes.
-template <int PRE, int POST, bool GENERIC>
+//
+// kMS = 24: the pass's predictor modes share the cross-color table's words (equal tile
+// sizes, both staged in LDS; encoded mode in byte 3, which cross-color does not read), so a
+// step reads one table word instead of two and computes one address.
+template <int PRE, int POST, bool GENERIC, int kMS = 0>
 __device__ __forceinline__ bool pred_wavefront(const Pass& P, int W, int H, int w_in, bool last, __amdgpu_buffer_rsrc_t in_rs,
                                __amdgpu_buffer_rsrc_t out_rs, int dst_stride, uint32_t* ring, const uint8_t* mode_tab,
                                const uint32_t* cc_tab, uint8_t* slots, uint32_t* prog, int* err) {
@@ -418,11 +432,16 @@ __device__ __forceinline__ bool pred_wavefront(const Pass& P, int W, int H, int 
       for (int k = 0; k < kChunk; ++k) {
         const int xr = c * kChunk + k - 2 * lane;
         const int x = decltype(kInterior)::value ? xr : min(max(xr, 0), W - 1);
-        if (GENERIC && !P.m_in_lds)
-          md[k] = enc_mode((int)((P.m_g[mrow + (x >> P.m_bits)] >> 8) & 0xf));
-        else
-          md[k] = mode_tab[mrow + (x >> P.m_bits)];
-        if (kCC) cw[k] = cc_tab[crow + (x >> P.cc_bits)];
+        if constexpr (kMS != 0) {
+          cw[k] = cc_tab[crow + (x >> P.cc_bits)];
+          md[k] = (int)cw[k];
+        } else {
+          if (GENERIC && !P.m_in_lds)
+            md[k] = enc_mode((int)((P.m_g[mrow + (x >> P.m_bits)] >> 8) & 0xf));
+          else
+            md[k] = mode_tab[mrow + (x >> P.m_bits)];
+          if (kCC) cw[k] = cc_tab[crow + (x >> P.cc_bits)];
+        }
       }
     };
     auto fix_modes = [&](int c, int* md) {
@@ -430,7 +449,8 @@ __device__ __forceinline__ bool pred_wavefront(const Pass& P, int W, int H, int 
 #pragma unroll
         for (int k = 0; k < kChunk; ++k) {
           const int xr = c * kChunk + k - 2 * lane;
-          md[k] = row0 ? (xr == 0 ? enc_mode(0) : enc_mode(1)) : (xr == 0 ? enc_mode(2) : md[k]);
+          const int fixed = row0 ? (xr == 0 ? enc_mode(0) : enc_mode(1)) : enc_mode(2);
+          if (row0 || xr == 0) md[k] = kMS ? (int)(((uint32_t)md[k] & 0xffffffu) | ((uint32_t)fixed << kMS)) : fixed;
         }
       }
     };
@@ -479,6 +499,8 @@ __device__ __forceinline__ bool pred_wavefront(const Pass& P, int W, int H, int 
       const uint32_t cin[kChunk] = {in0[0], in0[1], in0[2], in0[3], in1[0], in1[1], in1[2], in1[3]};
       K3_SECT(3);
       uint32_t ov[kChunk];
+      auto run_steps = [&](auto kSelC) {
+      constexpr int kSel = decltype(kSelC)::value;
 #pragma unroll
       for (int k = 0; k < kChunk; ++k) {
         const int x = c * kChunk + k - 2 * lane;
@@ -487,12 +509,28 @@ __device__ __forceinline__ bool pred_wavefront(const Pass& P, int W, int H, int 
         // (generic: tables may be in HBM, so the column is clamped into the frame)
         const uint32_t v =
             GENERIC ? pre_ops(P, cc_tab, cin[k], min(max(x, 0), W - 1), yc) : ops_ct<PRE>(cin[k], ccw[k]);
-        const uint32_t o = add_pixels(v, predict_fast(md[k], o_prev, t1, t2, TR));
+        const uint32_t o = add_pixels(v, predict_fast<kSel, kMS>(md[k], o_prev, t1, t2, TR));
         if (!interior && x == 0) first = o;
         t2 = t1;
         t1 = tr;
         o_prev = o;
         ov[k] = o;
+      }
+      };
+      // interior chunks pick the step code once for the chunk: the per-step checks of
+      // predict_fast<2> (a compare and a branch each, two when some lane is off mode 10)
+      // are only needed where some lane of the chunk is on a mode other than 10 and 1-4
+      if constexpr (interior) {
+        const int any_mode = (md[0] | md[1] | md[2] | md[3]) | (md[4] | md[5] | md[6] | md[7]);
+#ifdef WG_ABL_K3_FAST
+        run_steps(std::integral_constant<int, 0>{});
+#else
+        if (!__any((unsigned)any_mode >= (1u << kMS))) run_steps(std::integral_constant<int, 0>{});
+        else if (!__any((unsigned)any_mode >= (0x80u << kMS))) run_steps(std::integral_constant<int, 1>{});
+        else run_steps(std::integral_constant<int, 2>{});
+#endif
+      } else {
+        run_steps(std::integral_constant<int, 2>{});
       }
       K3_SECT(4);
       // band b's last row into the ring (lane 63)
@@ -616,7 +654,12 @@ __global__ void __launch_bounds__(1024) vp8l_transforms_kernel(const LLDesc* __r
       P.m_g = as_global(ps.data);
       const int nt = P.m_tpr * ((H + (1 << P.m_bits) - 1) >> P.m_bits);
       P.m_in_lds = nt <= kModeTabMax;
-      if (P.m_in_lds)
+      P.joint = (VARIANT == 1 || VARIANT == 3) && cc_stage >= 0 && P.cc_in_lds && nt <= kModeTabMax &&
+                P.cc_bits == P.m_bits && P.cc_tpr == P.m_tpr;
+      if (P.joint)  // same thread, same t as the cross-color staging above
+        for (int t = threadIdx.x; t < nt; t += blockDim.x)
+          cc_tab[t] = (cc_tab[t] & 0xffffffu) | ((uint32_t)enc_mode((int)((P.m_g[t] >> 8) & 0xf)) << 24);
+      else if (P.m_in_lds)
         for (int t = threadIdx.x; t < nt; t += blockDim.x) mode_tab[t] = (uint8_t)enc_mode((int)((P.m_g[t] >> 8) & 0xf));
     }
     if (threadIdx.x < kWaves) prog[threadIdx.x] = 0;
@@ -633,13 +676,14 @@ __global__ void __launch_bounds__(1024) vp8l_transforms_kernel(const LLDesc* __r
       // ---------------- predictor wavefront: compile-time op variants for the common
       // transform orders (all tables in LDS), the generic one otherwise
       bool ok;
-#define WG_PRED(PRE, POST, GEN) \
-  pred_wavefront<PRE, POST, GEN>(P, W, H, w_in, last, in_rs, out_rs, dst_stride, ring, mode_tab, cc_tab, slots, prog, err)
-      if (VARIANT == 1) ok = WG_PRED(1, 2, false);       // CC | PRED | AG (libwebp's usual order)
-      else if (VARIANT == 2) ok = WG_PRED(0, 2, false);  // PRED | AG
-      else if (VARIANT == 3) ok = WG_PRED(1, 0, false);  // CC | PRED
-      else if (VARIANT == 4) ok = WG_PRED(0, 0, false);  // PRED
-      else ok = WG_PRED(0, 0, true);
+#define WG_PRED(PRE, POST, GEN, MS) \
+  pred_wavefront<PRE, POST, GEN, MS>(P, W, H, w_in, last, in_rs, out_rs, dst_stride, ring, mode_tab, cc_tab, slots, prog, err)
+      // CC | PRED | AG (libwebp's usual order)
+      if (VARIANT == 1) ok = P.joint ? WG_PRED(1, 2, false, 24) : WG_PRED(1, 2, false, 0);
+      else if (VARIANT == 2) ok = WG_PRED(0, 2, false, 0);  // PRED | AG
+      else if (VARIANT == 3) ok = P.joint ? WG_PRED(1, 0, false, 24) : WG_PRED(1, 0, false, 0);  // CC | PRED
+      else if (VARIANT == 4) ok = WG_PRED(0, 0, false, 0);  // PRED
+      else ok = WG_PRED(0, 0, true, 0);
 #undef WG_PRED
       if (!ok) return;
     } else {
