@@ -18,9 +18,8 @@
 // so the row above is lane i-1 two steps earlier: T, TL, TR are lane i-1's last three
 // outputs, moved one lane up with DPP wave_shr:1 (no LDS).  Lane 0 takes them from the
 // previous band's last row through an LDS ring (kRing columns per band, flow-controlled
-// by per-wave progress counters).  Pixels move in 8-step chunks: at step 8c every lane
-// loads/stores the 8 columns it will touch next (aligned to its own skew), so memory
-// instructions are wave-uniform.  Cross-color / add-green before the predictor are
+// by per-wave progress counters).  Pixels move in 8-step chunks through a per-row
+// LDS column ring; HBM sees row-wise loads and whole aligned 64-byte row blocks.  Cross-color / add-green before the predictor are
 // applied to its input, those after it to its output (the recurrence keeps the raw
 // predictor output).
 #include <hip/hip_runtime.h>
@@ -36,14 +35,14 @@ namespace {
 constexpr int kWaves = 16;
 constexpr int kBand = 64;
 constexpr int kChunk = 8;
-constexpr int kRing = 512;  // columns per inter-band ring slot (power of two)
+constexpr int kRing = 256;  // columns per inter-band ring slot (power of two; 512 measured the same)
 constexpr int kRingBytes = kWaves * kRing * 4;
 constexpr int kModeTabMax = 16384;  // predictor tiles staged in LDS (1 byte each)
 constexpr int kCCTabMax = 4096;     // cross-color tiles staged in LDS (4 bytes each)
-// Per-wave staging slot: the band's 64 rows x 16 columns of one group (two chunks), row
-// stride padded to 80 B so the row-per-lane b128 accesses are bank-conflict free.
+// Per-wave staging slot: the band's 64 rows x a 24-column ring (see pred_wavefront).
 constexpr int kGroup = 2 * kChunk;
-constexpr int kSlotStride = 4 * kGroup + 16;
+constexpr int kOutCols = 24;  // per-row column ring: column x at position x mod 24
+constexpr int kSlotStride = 4 * kOutCols;
 constexpr int kSlotBytes = kBand * kSlotStride;
 constexpr int kLdsBytes = kRingBytes + kModeTabMax + kCCTabMax * 4 + kWaves * kSlotBytes;
 constexpr uint32_t kDrop = 0x80000000u;
@@ -51,6 +50,7 @@ constexpr int T_PRED = 0, T_CC = 1, T_AG = 2;  // 3 = color indexing
 
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t uint32x4_t __attribute__((ext_vector_type(4)));
+typedef uint32_t uint32x2_t __attribute__((ext_vector_type(2)));
 
 // Opt-in per-section cycle accounting (make VARIANT=timing, read back by
 // scripts/k3_sections.py): s_memtime deltas summed per chunk section in registers,
@@ -319,12 +319,12 @@ constexpr bool ops_cc(int ops) { return ops == 1 || ops == 3 || ops == 4; }
 // issue together at its start and are waited on once.  Row 0 / column 0 use fixed modes
 // (L / T, black at the origin), folded into the fetched modes.
 //
-// HBM traffic goes through the wave's staging slot, one group (two chunks, 16 columns
-// of the band's skewed rows) at a time: row-wise 16-byte loads/stores with four lanes per
-// row segment (16 rows per instruction), so an instruction touches ~24 cache lines
-// instead of 64 and every 64-byte row segment moves in one request.  The steps read
-// and overwrite the slot transposed (lane = row).  Inputs of group g+1 are in flight in
-// registers while group g computes.
+// HBM traffic goes through the wave's staging slot, a 24-column ring per row: each chunk's
+// inputs are loaded row-wise (two lanes per row) two chunks ahead and staged into the ring,
+// the steps read and overwrite them transposed (lane = row), and every row's output leaves
+// in whole aligned 64-byte blocks as soon as it completes one.  (Writing each group's
+// 64 bytes per row where the skew puts them, 8 bytes off alignment, left HBM sectors half
+// written between groups: 3.93 vs 3.47 ms on C5, see DESIGN.md.)
 //
 // kMS = 24: the pass's predictor modes share the cross-color table's words (equal tile
 // sizes, both staged in LDS; encoded mode in byte 3, which cross-color does not read), so a
@@ -341,12 +341,7 @@ __device__ __forceinline__ bool pred_wavefront(const Pass& P, int W, int H, int 
   const int ngroups = (steps + kGroup - 1) / kGroup;
   // interior chunks: 8c - 2*63 >= 1 and 8c + 7 <= W - 2
   const int c_lo = (2 * (kBand - 1) + kChunk) / kChunk, c_hi = (W - 1 - kChunk) / kChunk;
-  // groups whose columns all lie in [0, W-1]: 16g - 126 >= 0 and 16g + 15 <= W - 1
-  const int g_lo = (2 * (kBand - 1) + kGroup - 1) / kGroup, g_hi = (W - kGroup) / kGroup;
   uint8_t* slot = slots + wave * kSlotBytes;
-  // row-wise I/O mapping: lane -> rows io_r + 16q (q = 0..3), 16-byte quad io_p
-  const int io_r = lane >> 2, io_p = lane & 3;
-  uint8_t* io_lds = slot + io_r * kSlotStride + 16 * io_p;
   uint8_t* my_lds = slot + lane * kSlotStride;
   K3_SECT_DECL();
   for (int b = wave; b < nbands; b += kWaves) {
@@ -364,62 +359,61 @@ __device__ __forceinline__ bool pred_wavefront(const Pass& P, int W, int H, int 
     K3_SECT(6);
     const int mrow = (yc >> P.m_bits) * P.m_tpr;
     const int crow = (yc >> P.cc_bits) * P.cc_tpr;
-    // byte offsets of the I/O lane's quad in group 0 for q = 0 (row io_r, column
-    // -2*io_r + 4*io_p); +64 per group, +q*(16 rows - 32 columns) per q.  Rows past the
-    // frame get kDrop.  Columns left of the frame read the previous row (ignored) or, in
-    // row 0, wrap to an out-of-range offset (reads 0).
+    // Rows past the frame get kDrop.  Columns left of the frame read the previous row
+    // (ignored) or, in row 0, wrap to an out-of-range offset (reads 0).
     const int rows_left = H - b * kBand;
-    const uint32_t out_q = 16u * (uint32_t)dst_stride - 128u;
-    const uint32_t out_base = (uint32_t)((b * kBand + io_r) * dst_stride) + 16u * io_p - 8u * io_r;
-    const int x_io = 4 * io_p - 2 * io_r;  // column of the quad (group 0, q = 0)
-
-    // Inputs are loaded two groups at a time: 128 contiguous bytes per row (groups 2p and
-    // 2p+1), 8 lanes per row, rows io_r2 + 8q (q = 0..7), so each row's line is requested
-    // once per pair instead of once per group (the 64-byte-per-group loads re-fetched lines
-    // the L2 had evicted in between).  Quads 0..3 of a row are group 2p, 4..7 group 2p+1;
-    // a group's staging has the other half's lanes write into the slot's row padding.
-    const int io_r2 = lane >> 3, io_p2 = lane & 7;
-    const uint32_t in_q2 = 8u * (uint32_t)w_in * 4u - 64u;  // +8 rows, -16 columns of skew
-    const uint32_t in_base2 = (uint32_t)((b * kBand + io_r2) * w_in * 4) + 16u * io_p2 - 8u * io_r2;
-    uint8_t* const io_lds2 = slot + io_r2 * kSlotStride + 16 * (io_p2 & 3);
-    uint8_t* const io_pad2 = slot + io_r2 * kSlotStride + 4 * kGroup;  // row padding (never read)
-    uint32x4_t R[8];  // the current pair of groups' inputs
-    auto load_pair = [&](int p) {
+    // Row ring of 24 columns (column x at position x mod 24), inputs staged and outputs
+    // emitted per chunk.  Loads: chunk c's 8 columns of a row (32 B) by two lanes, rows
+    // lane/2 and lane/2 + 32, issued two chunks ahead.  Stores: whenever a row completes an
+    // aligned 16-column block (64 B, every other chunk per row; 32 rows per chunk, 4 lanes
+    // each) it goes out whole, so no HBM sector is left half written between groups.
+    // Occupancy: at most 14 un-emitted columns + the chunk's 8 <= 24.
+    auto ring_pos = [](int v) { return v >= kOutCols ? v - kOutCols : v; };
+    const int cpos0 = (kOutCols - (2 * lane) % kOutCols) % kOutCols;  // column -2*lane
+    const int l_row0 = lane >> 1, l_piece = lane & 1;
+    const int spos0 = ((4 * l_piece - 2 * l_row0) % kOutCols + kOutCols) % kOutCols;  // h = 0, c = 0
+    const int spos1 = ((4 * l_piece - 2 * (l_row0 + 32)) % kOutCols + kOutCols) % kOutCols;
+    const uint32_t l_off0 = (uint32_t)((b * kBand + l_row0) * w_in * 4) + 16u * l_piece - 8u * l_row0;
+    const uint32_t l_off1 = l_off0 + 32u * (uint32_t)w_in * 4u - 256u;  // +32 rows, -64 columns
+    auto load_chunk = [&](int c, uint32x4_t* L) {
+      L[0] = __builtin_amdgcn_raw_buffer_load_b128(in_rs, l_row0 < rows_left ? l_off0 + 32u * c : kDrop, 0, 0);
+      L[1] = __builtin_amdgcn_raw_buffer_load_b128(in_rs, l_row0 + 32 < rows_left ? l_off1 + 32u * c : kDrop, 0, 0);
+    };
+    auto stage_chunk = [&](int c, const uint32x4_t* L) {
+      const int c8 = 8 * (c % 3);
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const uint32_t off = io_r2 + 8 * q < rows_left ? in_base2 + q * in_q2 + 128u * p : kDrop;
-        R[q] = __builtin_amdgcn_raw_buffer_load_b128(in_rs, off, 0, 0);
+      for (int h = 0; h < 2; ++h) {
+        const int pa = ring_pos((h ? spos1 : spos0) + c8);
+        const int pb = pa + 2 == kOutCols ? 0 : pa + 2;
+        uint8_t* const row = slot + (l_row0 + 32 * h) * kSlotStride;
+        *reinterpret_cast<uint32x2_t*>(row + 4 * pa) = uint32x2_t{L[h][0], L[h][1]};
+        *reinterpret_cast<uint32x2_t*>(row + 4 * pb) = uint32x2_t{L[h][2], L[h][3]};
       }
     };
-    auto stage_half = [&](bool upper) {
-      uint8_t* const dst = (io_p2 >= 4) == upper ? io_lds2 : io_pad2;
+    // rows completing a block after chunk c (a multiple of 16 in (8c - 2r, 8c + 8 - 2r]):
+    // r mod 8 in {1..4} (c even) or {5, 6, 7, 0} (c odd); lane -> (i = lane/4 + 16h,
+    // quad = lane & 3), row = (8(i/4) + (i&3) + 1 + 4(c&1)) mod 64
+    const int e_quad = lane & 3;
+    auto emit_chunk = [&](int c) {
+      const int K_hi = ((kChunk * c + kChunk) >> 4) - 1;  // row 0's block
+      const bool inner = 8 * c >= 2 * (kBand - 1) + 16 && 16 * K_hi + 16 <= W;
 #pragma unroll
-      for (int q = 0; q < 8; ++q) *reinterpret_cast<uint32x4_t*>(dst + 8 * q * kSlotStride) = R[q];
-    };
-    auto emit_group = [&](int g) {
-      uint32x4_t S[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) S[q] = *reinterpret_cast<const uint32x4_t*>(io_lds + 16 * q * kSlotStride);
-      // full quads with one 16-byte store each (always issued, so the wait before the
-      // next staging keeps them in flight); edge groups add per-pixel stores for the
-      // quads that straddle a frame edge
-      const bool inner = g >= g_lo && g <= g_hi;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int x = x_io + kGroup * g - 32 * q;
-        const bool full = io_r + 16 * q < rows_left && (inner || (x >= 0 && x + 3 < W));
-        __builtin_amdgcn_raw_buffer_store_b128(S[q], out_rs, full ? out_base + q * out_q + 64u * g : kDrop, 0, 0);
-      }
-      if (!inner) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int x = x_io + kGroup * g - 32 * q;
-          const bool part = io_r + 16 * q < rows_left && !(x >= 0 && x + 3 < W);
-          const uint32_t off = out_base + q * out_q + 64u * g;
+      for (int h = 0; h < 2; ++h) {
+        const int i = (lane >> 2) + 16 * h;
+        const int row = (8 * (i >> 2) + (i & 3) + 1 + 4 * (c & 1)) & (kBand - 1);
+        const int K = ((kChunk * c + kChunk - 2 * row) >> 4) - 1;  // floor
+        const int km3 = K >= 0 ? K % 3 : 0;
+        const int pos = ring_pos(16 * km3 - (km3 == 2 ? 24 : 0) + 4 * e_quad);
+        const uint32x4_t d = *reinterpret_cast<const uint32x4_t*>(slot + row * kSlotStride + 4 * pos);
+        const int x0 = 16 * K + 4 * e_quad;
+        const uint32_t off = (uint32_t)((b * kBand + row) * dst_stride) + 4u * (uint32_t)x0;
+        const bool rok = row < rows_left && K >= 0;
+        __builtin_amdgcn_raw_buffer_store_b128(d, out_rs, rok && x0 + 3 < W ? off : kDrop, 0, 0);
+        if (!inner) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            const bool ok = part && x + j >= 0 && x + j < W;
-            __builtin_amdgcn_raw_buffer_store_b32(S[q][j], out_rs, ok ? off + 4 * j : kDrop, 0, 0);
+            const bool ok = rok && x0 + 3 >= W && x0 + j < W;
+            __builtin_amdgcn_raw_buffer_store_b32(d[j], out_rs, ok ? off + 4 * j : kDrop, 0, 0);
           }
         }
       }
@@ -465,8 +459,18 @@ __device__ __forceinline__ bool pred_wavefront(const Pass& P, int W, int H, int 
     // per-step frame-edge logic compiles out (two instantiations of the chunk)
     auto chunk_impl = [&](const int c, const int cl, auto kInterior) {
       constexpr bool interior = decltype(kInterior)::value;
-      const uint32x4_t in0 = *reinterpret_cast<const uint32x4_t*>(my_lds + 32 * cl);
-      const uint32x4_t in1 = *reinterpret_cast<const uint32x4_t*>(my_lds + 32 * cl + 16);
+      int cp[4];
+      {
+        const int p0 = ring_pos(cpos0 + 8 * (c % 3));
+#pragma unroll
+        for (int j = 0; j < 4; ++j) cp[j] = ring_pos(p0 + 2 * j);
+      }
+      const uint32x2_t i0 = *reinterpret_cast<const uint32x2_t*>(my_lds + 4 * cp[0]);
+      const uint32x2_t i1 = *reinterpret_cast<const uint32x2_t*>(my_lds + 4 * cp[1]);
+      const uint32x2_t i2 = *reinterpret_cast<const uint32x2_t*>(my_lds + 4 * cp[2]);
+      const uint32x2_t i3 = *reinterpret_cast<const uint32x2_t*>(my_lds + 4 * cp[3]);
+      const uint32x4_t in0 = uint32x4_t{i0[0], i0[1], i1[0], i1[1]};
+      const uint32x4_t in1 = uint32x4_t{i2[0], i2[1], i3[0], i3[1]};
       uint32_t ccw[kChunk];
       int md[kChunk];
       fetch_tables(c, md, ccw, kInterior);
@@ -561,8 +565,8 @@ __device__ __forceinline__ bool pred_wavefront(const Pass& P, int W, int H, int 
           if (last) f[k] = bgra_to_rgba(f[k]);
         }
       }
-      *reinterpret_cast<uint32x4_t*>(my_lds + 32 * cl) = uint32x4_t{f[0], f[1], f[2], f[3]};
-      *reinterpret_cast<uint32x4_t*>(my_lds + 32 * cl + 16) = uint32x4_t{f[4], f[5], f[6], f[7]};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) *reinterpret_cast<uint32x2_t*>(my_lds + 4 * cp[j]) = uint32x2_t{f[2 * j], f[2 * j + 1]};
       if (lane == 0)
         __hip_atomic_store(prog + (b & (kWaves - 1)), ((uint32_t)b << 16) | (uint32_t)min(c * kChunk + kChunk, steps),
                            __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -572,23 +576,24 @@ __device__ __forceinline__ bool pred_wavefront(const Pass& P, int W, int H, int 
       if (c >= c_lo && c <= c_hi) chunk_impl(c, cl, std::true_type{});
       else chunk_impl(c, cl, std::false_type{});
     };
-    load_pair(0);
-    stage_half(false);
-    for (int g = 0; g < ngroups; ++g) {
-      chunk(2 * g, 0);
-      chunk(2 * g + 1, 1);
-      emit_group(g);
+    uint32x4_t LA[2], LB[2];  // chunk inputs in flight: even chunks in LA, odd in LB
+    load_chunk(0, LA);
+    load_chunk(1, LB);
+    const int nch = 2 * ngroups;
+    for (int c = 0; c < nch; c += 2) {
+      stage_chunk(c, LA);
+      load_chunk(c + 2, LA);
+      chunk(c, 0);
+      emit_chunk(c);
       K3_SECT(7);
-      if ((g & 1) == 0) {
-        stage_half(true);     // group g+1: the resident pair's upper half
-        K3_SECT(8);
-        load_pair(g / 2 + 1);  // groups g+2, g+3 in flight (past the end: out of range, reads 0)
-      } else {
-        stage_half(false);    // group g+1: lower half of the pair loaded one group ago
-        K3_SECT(8);
-      }
-      K3_SECT(9);
+      stage_chunk(c + 1, LB);
+      load_chunk(c + 3, LB);
+      chunk(c + 1, 1);
+      emit_chunk(c + 1);
+      K3_SECT(7);
     }
+    // blocks still open after the last chunk (row 63 completes one more, two chunks on)
+    for (int c = nch; c < nch + 3; ++c) emit_chunk(c);
     K3_BAND_MARK(b, 1);
   }
   K3_SECT_FLUSH();
