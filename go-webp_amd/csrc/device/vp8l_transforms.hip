@@ -582,12 +582,16 @@ __device__ __forceinline__ bool pred_wavefront(const Pass& P, int W, int H, int 
     const int nch = 2 * ngroups;
     for (int c = 0; c < nch; c += 2) {
       stage_chunk(c, LA);
+      K3_SECT(8);
       load_chunk(c + 2, LA);
+      K3_SECT(9);
       chunk(c, 0);
       emit_chunk(c);
       K3_SECT(7);
       stage_chunk(c + 1, LB);
+      K3_SECT(8);
       load_chunk(c + 3, LB);
+      K3_SECT(9);
       chunk(c + 1, 1);
       emit_chunk(c + 1);
       K3_SECT(7);
