@@ -397,6 +397,11 @@ __device__ __forceinline__ bool pred_wavefront(const Pass& P, int W, int H, int 
     auto emit_chunk = [&](int c) {
       const int K_hi = ((kChunk * c + kChunk) >> 4) - 1;  // row 0's block
       const bool inner = 8 * c >= 2 * (kBand - 1) + 16 && 16 * K_hi + 16 <= W;
+      // both halves' LDS reads first, then both stores: one LDS round trip per chunk
+      uint32x4_t d[2];
+      uint32_t off[2];
+      int x0[2];
+      bool rok[2];
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int i = (lane >> 2) + 16 * h;
@@ -404,16 +409,21 @@ __device__ __forceinline__ bool pred_wavefront(const Pass& P, int W, int H, int 
         const int K = ((kChunk * c + kChunk - 2 * row) >> 4) - 1;  // floor
         const int km3 = K >= 0 ? K % 3 : 0;
         const int pos = ring_pos(16 * km3 - (km3 == 2 ? 24 : 0) + 4 * e_quad);
-        const uint32x4_t d = *reinterpret_cast<const uint32x4_t*>(slot + row * kSlotStride + 4 * pos);
-        const int x0 = 16 * K + 4 * e_quad;
-        const uint32_t off = (uint32_t)((b * kBand + row) * dst_stride) + 4u * (uint32_t)x0;
-        const bool rok = row < rows_left && K >= 0;
-        __builtin_amdgcn_raw_buffer_store_b128(d, out_rs, rok && x0 + 3 < W ? off : kDrop, 0, 0);
-        if (!inner) {
+        d[h] = *reinterpret_cast<const uint32x4_t*>(slot + row * kSlotStride + 4 * pos);
+        x0[h] = 16 * K + 4 * e_quad;
+        off[h] = (uint32_t)((b * kBand + row) * dst_stride) + 4u * (uint32_t)x0[h];
+        rok[h] = row < rows_left && K >= 0;
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        __builtin_amdgcn_raw_buffer_store_b128(d[h], out_rs, rok[h] && x0[h] + 3 < W ? off[h] : kDrop, 0, 0);
+      if (!inner) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            const bool ok = rok && x0 + 3 >= W && x0 + j < W;
-            __builtin_amdgcn_raw_buffer_store_b32(d[j], out_rs, ok ? off + 4 * j : kDrop, 0, 0);
+            const bool ok = rok[h] && x0[h] + 3 >= W && x0[h] + j < W;
+            __builtin_amdgcn_raw_buffer_store_b32(d[h][j], out_rs, ok ? off[h] + 4 * j : kDrop, 0, 0);
           }
         }
       }
