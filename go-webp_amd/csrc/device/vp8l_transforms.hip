@@ -45,6 +45,8 @@ constexpr int kOutCols = 24;  // per-row column ring: column x at position x mod
 constexpr int kSlotStride = 4 * kOutCols;
 constexpr int kSlotBytes = kBand * kSlotStride;
 constexpr int kLdsBytes = kRingBytes + kModeTabMax + kCCTabMax * 4 + kWaves * kSlotBytes;
+static_assert(kLdsBytes + 4 * kWaves <= 160 * 1024, "K3 LDS (dynamic + the progress counters) exceeds gfx950's 160 KB");
+static_assert(kOutCols >= 14 + kChunk && kOutCols % 4 == 0, "row ring: 14 open columns + a chunk; 16-byte pieces never wrap");
 constexpr uint32_t kDrop = 0x80000000u;
 constexpr int T_PRED = 0, T_CC = 1, T_AG = 2;  // 3 = color indexing
 
