@@ -3,19 +3,26 @@
 
 Metric (BASELINE.json): "decoded MPixels/sec at 1/2/4/8 GPUs; % HBM roofline (YUV->RGBA)".
 
-A step = one pass of the device decode path (K1 reconstruct+deblock, K2 YUV420->RGBA)
-over one resident batch of frames: by default config C3, 256 x 3840x2160
-VP8-lossy frames with the in-loop deblocking filter, 8 distinct libwebp-encoded synthetic
-bitstreams cycled (each frame has its own HBM buffers).  The entropy stage (host) and the
-H2D upload happen before the timed region: `value` is device throughput with inputs
-resident in HBM.  With N GPUs each rank decodes its own 256 frames (weak scaling, no
-collectives on the data path; C4 = 2048 frames over 8 GPUs).
+A step = one pass of the device decode path over one resident batch of frames: by default
+config C3, 256 x 3840x2160 VP8-lossy frames with the in-loop deblocking
+filter (K1: Y2 WHT + IDCT + reconstruction + deblocking + YUV420->RGBA in its tail), 8
+distinct libwebp-encoded synthetic bitstreams cycled (each frame has its own HBM buffers).
+The entropy stage (host) and the H2D upload happen before the timed region: `value` is
+device throughput with inputs resident in HBM.
+
+Multi-GPU: every rank decodes its own `--batch` frames on its own GPU
+(weak scaling); ranks exchange nothing on the data path.  `--gpus N` without a launcher
+spawns N rank processes itself (before anything touches a GPU); under torch.distributed.run
+the launcher's RANK / LOCAL_RANK / WORLD_SIZE are used.  The timing barrier and the
+max-time / sum-pixels reduction go over gloo (host sockets), not RCCL.
 
 Prints ONE JSON line on rank 0.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -65,8 +72,7 @@ def shard_frames(datas, rank, batch):
 
 def reduce_job(dist, device, dt, pixels):
     """Whole-job figures over all ranks: (max elapsed seconds, total pixels).  `dist` None =
-    single process; otherwise any initialised torch.distributed backend (nccl on the GPU
-    box, gloo in tests/test_multi_rank.py)."""
+    single process; otherwise an initialised torch.distributed gloo group (CPU tensors)."""
     if dist is None:
         return dt, pixels
     import torch
@@ -77,6 +83,48 @@ def reduce_job(dist, device, dt, pixels):
     return float(t.item()), int(p.item())
 
 
+# ------------------------------------------------------------------------------- launcher
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n, argv, timeout=None):
+    """Run `bench.py argv` as n rank processes (RANK = LOCAL_RANK = r, WORLD_SIZE = n, gloo
+    rendezvous on 127.0.0.1) and return the worst exit code.  The parent never touches a GPU:
+    each rank initialises only its own device.  If a rank fails, the others are stopped (their
+    exact PIDs) instead of waiting at the barrier."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    t0 = time.time()
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0:
+                rc = rc or code
+                for q in live:
+                    q.kill()
+        if timeout is not None and time.time() - t0 > timeout:
+            for q in live:
+                q.kill()
+            return 124
+        time.sleep(0.05)
+    for p in procs:
+        p.wait()
+    return rc
+
+
+# ------------------------------------------------------------------------------- CPU legs
 def _cpu_decode_one(d):
     """One frame through the CPU path (host entropy stage + oracle); returns its pixels."""
     import webp_amd
@@ -93,8 +141,6 @@ def _cpu_decode_one(d):
 def cpu_baseline(datas, seconds):
     """CPU oracle (C restatement, 1 thread): host entropy stage + reconstruct + filter +
     fancy RGBA, frames decoded serially until `seconds` elapse."""
-    import webp_amd
-    from oracle_lib import oracle_decode
     pix, n, t0 = 0, 0, time.perf_counter()
     while True:
         d = datas[n % len(datas)]
@@ -106,6 +152,35 @@ def cpu_baseline(datas, seconds):
     return dict(value=pix / el / 1e6, unit="MPix/s", cores=1, kind="port",
                 sample=f"{n} frames of the same workload decoded serially on 1 host core "
                        f"(host entropy stage + oracle/ CPU restatement of the device path), {el:.1f}s")
+
+
+def cpu_baseline_dsp(datas, seconds):
+    """The same CPU restatement on pre-parsed frames (entropy stage outside the timing): the
+    work the device kernels do, timed on 1 host core -- the like-for-like baseline for
+    `value`."""
+    import webp_amd
+    from oracle_lib import oracle_decode, oracle_vp8l_decode
+    parsed = []
+    for d in datas:
+        if webp_amd.features(d).format == 2:
+            parsed.append(("ll", webp_amd.vp8l_parse(d)))
+        else:
+            parsed.append(("vp8", webp_amd.vp8_parse(d)))
+    pix, n, t0 = 0, 0, time.perf_counter()
+    while True:
+        kind, p = parsed[n % len(parsed)]
+        if kind == "ll":
+            oracle_vp8l_decode(*p)
+        else:
+            oracle_decode(*p)
+        pix += p[0].width * p[0].height
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return dict(value=pix / el / 1e6, unit="MPix/s", cores=1, kind="port",
+                sample=f"{n} pre-parsed frames through the oracle/ CPU restatement of the device path "
+                       f"(reconstruct + filter + RGBA, or the VP8L inverse transforms) on 1 host core, {el:.1f}s")
 
 
 def cpu_baseline_parallel(datas, seconds, threads):
@@ -140,6 +215,26 @@ def cpu_baseline_parallel(datas, seconds, threads):
                        f"(entropy stage + oracle/ CPU restatement), {el:.1f}s")
 
 
+# ------------------------------------------------------------------------------- one rank
+class _MockBatch:
+    """--mock (CPU tests of the launcher): a stand-in for webp_amd.Batch that sleeps instead of
+    decoding, so the rank / reduction / JSON plumbing runs without a GPU."""
+    n = 4
+    pixels = 4 * 1000
+
+    def run(self, stream=None):
+        time.sleep(0.002)
+
+    def kernel_ms(self):
+        return (0.0, 0.0, 0.0, 0.0)
+
+    def kernel_bytes(self):
+        return (0.0, 0.0, 0.0, 0.0)
+
+    def close(self):
+        pass
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -153,48 +248,61 @@ def main():
     ap.add_argument("--emit", choices=("fused", "separate"), default="fused",
                     help="lossy RGBA from K1's tail (default) or a separate K2 launch")
     ap.add_argument("--host-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
+    ap.add_argument("--mock", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no launcher: start one rank per GPU ourselves, before anything touches a GPU
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0 and args.gpus != 1:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}", file=sys.stderr)
     import torch
-    import webp_amd
-
-    torch.cuda.set_device(local)
     dist = None
     if world > 1:
+        import datetime
         import torch.distributed as dist
-        dist.init_process_group("nccl")
+        dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=600))
 
     def barrier():
         if dist is not None:
             dist.barrier()
 
     wl = WORKLOADS[args.workload]
-    datas, bpp = _load_frames(wl["prefix"])
-    frames = shard_frames(datas, rank, args.batch)
-    ctx_threads = max(1, min(args.host_threads, 64))
-    ctx = webp_amd.Context(local, host_threads=ctx_threads)
-    t_prep = time.perf_counter()
-    b = ctx.batch(frames)
-    t_prep = time.perf_counter() - t_prep
-    if not (b.status == 0).all():
-        raise SystemExit(f"rank {rank}: frames failed to parse: {b.status}")
-    stream = torch.cuda.current_stream().cuda_stream
-    b.set_emit(args.emit == "separate")
+    if args.mock:
+        datas, bpp = [b"mock"], 0.0
+        b, ctx, t_prep, stream = _MockBatch(), None, 0.0, None
+        sync = lambda: None  # noqa: E731
+    else:
+        import webp_amd
+        torch.cuda.set_device(local)
+        datas, bpp = _load_frames(wl["prefix"])
+        frames = shard_frames(datas, rank, args.batch)
+        ctx_threads = max(1, min(args.host_threads, 64))
+        ctx = webp_amd.Context(local, host_threads=ctx_threads)
+        t_prep = time.perf_counter()
+        b = ctx.batch(frames)
+        t_prep = time.perf_counter() - t_prep
+        if not (b.status == 0).all():
+            raise SystemExit(f"rank {rank}: frames failed to parse: {b.status}")
+        stream = torch.cuda.current_stream().cuda_stream
+        b.set_emit(args.emit == "separate")
+        sync = torch.cuda.synchronize
 
     for _ in range(args.warmup):
         b.run(stream)
-    torch.cuda.synchronize()
+    sync()
     b.kernel_ms()  # drop warmup timings
 
     barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         b.run(stream)
-    torch.cuda.synchronize()
+    sync()
     barrier()
     dt = time.perf_counter() - t0
     kms = list(b.kernel_ms())  # per-launch averages over the timed steps (HIP events): K1..K4
@@ -205,14 +313,19 @@ def main():
         # alone (K2 over the same reconstructed planes) for its own roofline figure
         for _ in range(2):
             b.run_emit(stream)
-        torch.cuda.synchronize()
+        sync()
         b.kernel_ms()
         for _ in range(args.steps):
             b.run_emit(stream)
         stage_ms = b.kernel_ms()[1]
     px_rank = b.pixels
-    dt, total_px = reduce_job(dist, "cuda", dt, px_rank * args.steps)
+    dt, total_px = reduce_job(dist, "cpu", dt, px_rank * args.steps)
     value = total_px / dt / 1e6
+    ranks = [(rank, local, os.getpid())]
+    if dist is not None:
+        gathered = [None] * world
+        dist.all_gather_object(gathered, (rank, local, os.getpid()))
+        ranks = gathered
 
     if rank == 0:
         def roof(bytes_, ms, kernel):
@@ -224,10 +337,10 @@ def main():
                     "avg_launch_ms": round(ms, 4)}
         ran = [k for k in range(len(KERNELS)) if kms[k] > 0]
         roofs = {KERNELS[k]: roof(kby[k], kms[k], KERNELS[k]) for k in ran}
-        dominant = roofs[KERNELS[max(ran, key=lambda k: kms[k])]]
-        if dominant["kernel"] == "vp8_recon_filter_kernel":
-            # measured limiter: VALU issue on the frame's CU, not HBM
-            dominant["limiter"] = "VALU issue per CU (each added VALU op per MB step costs ~2.5 SIMD cycles)"
+        dominant = roofs[KERNELS[max(ran, key=lambda k: kms[k])]] if ran else None
+        if dominant and dominant["kernel"] == "vp8_recon_filter_kernel":
+            # measured limiter: instruction issue / latency on the frame's CU, not HBM
+            dominant["limiter"] = "per-wave issue and latency on the frame's CU (DESIGN.md §4)"
         if stage_ms > 0:
             roofs["yuv_to_rgba_kernel"] = dict(roof(kby[1], stage_ms, "yuv_to_rgba_kernel"),
                                                note="stage timed alone over the same planes; in the "
@@ -248,39 +361,53 @@ def main():
             "config": {"workload": wl["name"], "description": wl["desc"], "frames_per_gpu": args.batch,
                        "frames_total": args.batch * world,
                        "distinct_bitstreams": len(datas), "input_bpp": round(bpp, 3),
-                       "parallelism": f"frame-sharded over {world} GPU(s), no collectives",
+                       "parallelism": f"frame-sharded over {world} GPU(s), one process each, no collectives "
+                                      f"(gloo barrier + timing reduction only)",
                        "inputs": "resident in HBM (host entropy stage + H2D outside the timed region)"},
             "roofline": dominant,
             "kernel_ms": {KERNELS[k]: round(kms[k], 4) for k in ran},
             "lossy_emit": args.emit if kms[0] > 0 else None,
             "host_prepare_s": round(t_prep, 3),
+            "ranks": [{"rank": r, "local_rank": lr, "pid": pid} for r, lr, pid in sorted(ranks)],
         }
+        if args.mock:
+            out["mock"] = True
         if "yuv_to_rgba_kernel" in roofs:
             out["roofline_yuv_to_rgba"] = roofs["yuv_to_rgba_kernel"]
-        if not args.no_e2e:
-            # secondary figure: host bitstreams in, host RGBA out (entropy stage on host threads
-            # + H2D + K1 + K2 + D2H into pageable numpy buffers allocated outside the timing)
+        if not args.no_e2e and not args.mock:
+            # secondary figure: host bitstreams in, host RGBA out (entropy stage on the context's
+            # host threads + H2D + kernels + D2H into pageable numpy buffers allocated outside the
+            # timing).  The first call also grows the context's pinned staging and device buffers.
             outs = [np.empty((b.dims(i)[1], b.dims(i)[0], 4), np.uint8) for i in range(b.n)]
-            ctx.decode_batch(frames[:2], out=outs[:2])
-            t_e = time.perf_counter()
-            ctx.decode_batch(frames, out=outs)
-            t_e = time.perf_counter() - t_e
+            runs = []
+            for _ in range(2):
+                t_e = time.perf_counter()
+                ctx.decode_batch(frames, out=outs)
+                runs.append(time.perf_counter() - t_e)
+            t_e = min(runs)
             out["end_to_end"] = {"value": round(px_rank / t_e / 1e6, 1), "unit": "MPix/s", "n_gpus": 1,
-                                 "seconds": round(t_e, 3), "host_threads": ctx_threads,
+                                 "seconds": round(t_e, 3), "seconds_first_call": round(runs[0], 3),
+                                 "host_threads": ctx_threads,
                                  "note": "one batch: host entropy stage + H2D + kernels + D2H (pageable), "
                                          "host-bound; not the headline value"}
             del outs
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and not args.mock:
             cb = cpu_baseline(datas, args.cpu_seconds)
             out["cpu_baseline"] = cb
             out["speedup_vs_cpu_baseline"] = round(value / cb["value"], 1)
+            cbd = cpu_baseline_dsp(datas, max(2.0, args.cpu_seconds / 2))
+            out["cpu_baseline_dsp"] = cbd
+            out["speedup_vs_cpu_dsp"] = round(value / cbd["value"], 1)
             threads = max(1, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)))
             cba = cpu_baseline_parallel(datas, max(2.0, args.cpu_seconds / 2), threads)
             out["cpu_baseline_all_cores"] = cba
             out["speedup_vs_cpu_all_cores"] = round(value / cba["value"], 1)
+            if "end_to_end" in out:
+                out["end_to_end"]["vs_cpu_all_cores"] = round(out["end_to_end"]["value"] / cba["value"], 2)
         print(json.dumps(out), flush=True)
     b.close()
-    ctx.close()
+    if ctx is not None:
+        ctx.close()
     if dist is not None:
         dist.destroy_process_group()
 

@@ -11,28 +11,128 @@
 #include <algorithm>
 #include <atomic>
 #include <climits>
-#include <new>
 #include <cstring>
+#include <memory>
 #include <mutex>
+#include <new>
+#include <system_error>
 #include <thread>
 #include <vector>
 
 #include "../../include/gowebp_amd.h"
 #include "device/kernels.h"
 #include "device_format.h"
+#include "host/batch.h"
 #include "host/host.h"
 
-using wg::FrameDesc;
-using wg::LLDesc;
 using wg::AlphaDesc;
 using wg::AnimFrameDesc;
+using wg::FrameDesc;
+using wg::FrameParse;
+using wg::LLDesc;
 using wg::MbRec;
+
+namespace {
+
+// Device buffers of finished batches, kept for the next batch of the context (the single-frame
+// and one-shot batch entry points create and destroy a batch per call).  Best fit among
+// buffers at most ~2x the request; beyond kMaxCached bytes the largest are freed.
+class DeviceCache {
+ public:
+  ~DeviceCache() { trim(0); }
+  void* get(size_t bytes) {
+    bytes = std::max<size_t>(bytes, 256);
+    {
+      std::lock_guard<std::mutex> lock(mu_);
+      size_t best = free_.size();
+      for (size_t i = 0; i < free_.size(); ++i) {
+        const size_t c = free_[i].cap;
+        if (c >= bytes && c <= 2 * bytes + (size_t(16) << 20) && (best == free_.size() || c < free_[best].cap)) best = i;
+      }
+      if (best < free_.size()) {
+        void* p = free_[best].p;
+        cached_ -= free_[best].cap;
+        free_.erase(free_.begin() + (ptrdiff_t)best);
+        return p;
+      }
+    }
+    void* p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) {
+      (void)hipGetLastError();
+      trim(0);  // make room and try once more
+      if (hipMalloc(&p, bytes) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+      }
+    }
+    std::lock_guard<std::mutex> lock(mu_);
+    caps_.push_back(Entry{p, bytes});
+    return p;
+  }
+  void put(void* p) {
+    if (!p) return;
+    std::lock_guard<std::mutex> lock(mu_);
+    for (size_t i = 0; i < caps_.size(); ++i)
+      if (caps_[i].p == p) {
+        free_.push_back(caps_[i]);
+        cached_ += caps_[i].cap;
+        break;
+      }
+    trim_locked(kMaxCached);
+  }
+  void trim(size_t keep) {
+    std::lock_guard<std::mutex> lock(mu_);
+    trim_locked(keep);
+  }
+
+ private:
+  struct Entry {
+    void* p;
+    size_t cap;
+  };
+  void trim_locked(size_t keep) {
+    while (cached_ > keep && !free_.empty()) {
+      auto it = std::max_element(free_.begin(), free_.end(), [](const Entry& a, const Entry& b) { return a.cap < b.cap; });
+      hipFree(it->p);
+      cached_ -= it->cap;
+      for (size_t i = 0; i < caps_.size(); ++i)
+        if (caps_[i].p == it->p) {
+          caps_.erase(caps_.begin() + (ptrdiff_t)i);
+          break;
+        }
+      free_.erase(it);
+    }
+  }
+  static constexpr size_t kMaxCached = size_t(64) << 30;
+  std::mutex mu_;
+  std::vector<Entry> free_, caps_;  // free list; every buffer this cache allocated (and its size)
+  size_t cached_ = 0;
+};
+
+void* pinned_alloc(size_t bytes) {
+  void* p = nullptr;
+  if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  return p;
+}
+void pinned_free(void* p) { hipHostFree(p); }
+
+}  // namespace
 
 struct wg_ctx {
   int device = 0;
   int host_threads = 1;
   hipStream_t stream = nullptr;
-  std::mutex mu;
+  std::mutex mu;  // one batch creation at a time (the arena and the pool are shared)
+  std::unique_ptr<wg::WorkerPool> pool;
+  std::unique_ptr<wg::StagingArena> arena;
+  DeviceCache cache;
+  wg::WorkerPool* workers() {
+    if (!pool) pool.reset(new wg::WorkerPool(host_threads));
+    return pool.get();
+  }
 };
 
 namespace {
@@ -40,194 +140,10 @@ namespace {
 constexpr size_t kAlign = 256;
 inline size_t align_up(size_t v) { return (v + kAlign - 1) & ~(kAlign - 1); }
 
-struct FrameParse {
-  int status = WG_STATUS_OK;
-  bool lossless = false;
-  wg::SparseFrame sf;  // lossy
-  wg::VP8LFrame lf;    // lossless
-  size_t off_recs = 0, off_rows = 0, off_blocks = 0;  // within the input buffer (lossy)
-  size_t off_coded = 0, off_tdata[4] = {0, 0, 0, 0};  // within the input buffer (lossless)
-  size_t off_y = 0, off_u = 0, off_v = 0;            // within the plane buffer
-  size_t off_cols = 0;                                // K1 global column store (wide frames)
-  bool wide = false;                                  // mb_w > vp8_recon_max_mb_w()
-  size_t off_scratch = 0;                             // lossless two-pass scratch (plane buffer)
-  size_t off_rgba = 0;                                // within the RGBA buffer
-  int width = 0, height = 0;
-  // ALPH plane of a lossy frame (f2): raw bytes, or a lossless stream K3 decodes
-  bool alpha = false;
-  wg::AlphaHeader ah;
-  wg::VP8LFrame af;
-  const uint8_t* alpha_raw = nullptr;  // into the caller's input (valid during batch creation)
-  size_t off_araw = 0, off_acoded = 0, off_atdata[4] = {0, 0, 0, 0};  // input buffer
-  size_t off_ascratch = 0, off_argba = 0, off_aplane = 0;            // plane buffer
-  // output (cropping, f4): out_w x out_h, taken at (win_x, win_y) of the frame's RGBA buffer
-  // (rgba_w x rgba_h: the window itself for lossy frames, the whole frame for lossless)
-  int out_w = 0, out_h = 0, win_x = 0, win_y = 0, rgba_w = 0, rgba_h = 0;
-  bool cropped = false;
-  size_t off_yc = 0, off_uc = 0, off_vc = 0;  // cropped lossy planes (plane buffer)
-  int yc_stride = 0, uvc_stride = 0;
-};
-
 struct Timing {
   hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
   bool ran[4] = {false, false, false, false};  // K1, K2, K3, K4 launched in this run
 };
-
-// Does the lossless frame need a second pass (predictor and color indexing both present)?
-bool ll_two_pass(const wg::VP8LFrame& f) {
-  int cores = 0;
-  for (const auto& t : f.transforms) cores += (t.type == wg::kVP8LPredictor || t.type == wg::kVP8LColorIndexing);
-  return cores > 1;
-}
-
-// Allocation failure anywhere in the host stages (vectors sized by the bitstream) is
-// reported as WebPDecode does, never thrown across the C ABI or out of a parse thread.
-template <class F>
-int guarded(F&& f) {
-  try {
-    return f();
-  } catch (const std::bad_alloc&) {
-    return WG_STATUS_OUT_OF_MEMORY;
-  }
-}
-
-constexpr int kFilterExtraRows[3] = {0, 2, 8};  // frame_dec.c.go (VP8EnterCritical)
-
-// Output options (WebPIoInitFromOptions / WebPAllocateDecBuffer, webp.go): colorspace,
-// scaling (disabled in the reference, io_dec.c.go:540-541), cropping (WebPCheckCropDimensions
-// -> INVALID_PARAM).  Sets the frame's output window.
-int apply_output_options(const wg_decoder_options& opt, FrameParse* f) {
-  if (!wg::output_bpp(opt.colorspace))
-    return (opt.colorspace == 11 || opt.colorspace == 12) ? WG_STATUS_UNSUPPORTED_FEATURE : WG_STATUS_INVALID_PARAM;
-  if (opt.use_scaling) return WG_STATUS_UNSUPPORTED_FEATURE;
-  f->out_w = f->width;
-  f->out_h = f->height;
-  if (opt.use_cropping) {
-    // WebPAllocateDecBuffer checks the window with its origin snapped to even
-    // (buffer_dec.c.go:201-209); the decoder's window (WebPIoInitFromOptions, webp.go:922-945)
-    // snaps only for YUV sources: lossy frames use the snapped origin, lossless the exact one
-    const int cw = opt.crop_width, ch = opt.crop_height;
-    auto inside = [&](int x, int y) {
-      return x >= 0 && y >= 0 && cw > 0 && ch > 0 && x < f->width && y < f->height && cw <= f->width - x &&
-             ch <= f->height - y;
-    };
-    const int x = f->lossless ? opt.crop_left : (opt.crop_left & ~1);
-    const int y = f->lossless ? opt.crop_top : (opt.crop_top & ~1);
-    if (!inside(opt.crop_left & ~1, opt.crop_top & ~1) || !inside(x, y)) return WG_STATUS_INVALID_PARAM;
-    f->cropped = x != 0 || y != 0 || cw != f->width || ch != f->height;
-    f->out_w = cw;
-    f->out_h = ch;
-    f->win_x = f->lossless ? x : 0;  // lossy: K2 writes the window itself
-    f->win_y = f->lossless ? y : 0;
-  }
-  f->rgba_w = f->lossless ? f->width : f->out_w;
-  f->rgba_h = f->lossless ? f->height : f->out_h;
-  return WG_STATUS_OK;
-}
-
-// The MB row at whose FinishRow libwebp's lazy alpha decode fails, INT_MAX if never.
-// FinishRow(m) (frame_dec.c.go) requests alpha rows [y_start, y_end): 16m minus the filter
-// delay, the last parsed row (m = rows - 1) through its bottom, clamped to the crop bottom;
-// the first request runs ALPHInit (header + lossless stream header), pre-processed
-// (quantized) alpha is decoded whole at that first request (VP8DecompressAlphaRows).  A
-// lossless pixel failure is hit once the requested rows reach it.
-int alpha_fail_row(int rows, int extra, int bottom, bool init_fails, size_t fail_pixel, int coded_width,
-                   bool whole_plane) {
-  for (int m = 0; m < rows; ++m) {
-    const int y_start = m ? 16 * m - extra : 0;
-    const int y_end = std::min(m == rows - 1 ? 16 * (m + 1) : 16 * (m + 1) - extra, bottom);
-    if (y_start >= y_end) continue;
-    if (init_fails) return m;
-    const uint64_t last = (uint64_t)(whole_plane ? bottom : y_end);
-    if (last * (uint64_t)coded_width > (uint64_t)fail_pixel) return m;
-    if (whole_plane) break;
-  }
-  return INT_MAX;
-}
-
-// One frame's host stages and its WebPDecode status, in DecodeInto's order (webp.go:483-556):
-// container, bitstream headers, output options, then the image data -- bounded, like
-// libwebp's, to the rows a crop window needs, with a lossy frame's ALPH data decoded
-// lazily per MB row (its failure wins over a token failure further down).
-int parse_one(const uint8_t* data, size_t size, const wg_decoder_options& opt, FrameParse* fp) {
-  wg::Container c;
-  wg_features feat{};
-  // WebPDecode first runs GetFeatures; its NOT_ENOUGH_DATA is "treated as error"
-  int st = wg::parse_container(data, size, &c, &feat, /*have_all_data=*/false);
-  if (st != WG_STATUS_OK) return st == WG_STATUS_NOT_ENOUGH_DATA ? WG_STATUS_BITSTREAM_ERROR : st;
-  st = wg::parse_container(data, size, &c, &feat);  // DecodeInto's WebPParseHeaders
-  if (st != WG_STATUS_OK) return st;
-  if (c.is_lossless) {  // VP8L: host entropy stage, K3 on device
-    fp->lossless = true;
-    st = wg::vp8l_parse(data + c.payload_off, c.payload_size, &fp->lf);
-    if (st != WG_STATUS_OK && fp->lf.fail_pixel == SIZE_MAX) return st;  // VP8LDecodeHeader
-    fp->width = fp->lf.width;
-    fp->height = fp->lf.height;
-    const int ost = apply_output_options(opt, fp);
-    if (ost != WG_STATUS_OK) return ost;
-    if (st != WG_STATUS_OK) {  // DecodeImageData stops at the crop bottom (io->crop_bottom)
-      const int bottom = opt.use_cropping ? opt.crop_top + opt.crop_height : fp->height;
-      if ((uint64_t)bottom * (uint64_t)fp->lf.coded_width > (uint64_t)fp->lf.fail_pixel) return st;
-    }
-    return WG_STATUS_OK;
-  }
-  const int flags = opt.bypass_filtering ? WG_FLAG_BYPASS_FILTERING : 0;
-  const int crop_bottom = opt.use_cropping ? (opt.crop_top & ~1) + opt.crop_height : -1;
-  st = wg::vp8_parse(data, size, flags, nullptr, nullptr, &fp->sf, crop_bottom);
-  if (st != WG_STATUS_OK && fp->sf.fail_row < 0) return st;  // VP8GetHeaders
-  fp->width = fp->sf.info.width;
-  fp->height = fp->sf.info.height;
-  const int ost = apply_output_options(opt, fp);
-  if (ost != WG_STATUS_OK) return ost;
-  if (c.alpha_size > 0) {  // ALPH (VP8DecompressAlphaRows, alpha_dec.go:164-213)
-    const uint8_t* ad = data + c.alpha_off;
-    fp->alpha = true;
-    int ast = WG_STATUS_OK;
-    bool init_fails = false;
-    if (!wg::parse_alpha_header(ad, c.alpha_size, fp->width, fp->height, &fp->ah)) {
-      ast = WG_STATUS_OUT_OF_MEMORY;  // ALPHInit failure without a VP8L decoder
-      init_fails = true;
-    } else if (fp->ah.method == 1) {
-      ast = wg::vp8l_parse_alpha(ad + 1, c.alpha_size - 1, fp->width, fp->height, &fp->af);
-      init_fails = ast == WG_STATUS_OUT_OF_MEMORY;
-    } else {
-      fp->alpha_raw = ad + 1;
-    }
-    if (ast != WG_STATUS_OK) {
-      const int bottom = crop_bottom >= 0 ? crop_bottom : fp->height;
-      const int arow = alpha_fail_row(fp->sf.br_mb_y, kFilterExtraRows[fp->sf.info.filter_type], bottom, init_fails,
-                                      fp->af.fail_pixel, fp->af.coded_width, fp->ah.pre_processing == 1);
-      if (arow < (st != WG_STATUS_OK ? fp->sf.fail_row : INT_MAX)) return ast;
-    }
-  }
-  return st;
-}
-
-void parse_all(const uint8_t* const* data, const size_t* sizes, int n, const wg_decoder_options& opt, int threads,
-               std::vector<FrameParse>& out) {
-  out.resize(n);
-  std::atomic<int> next{0};
-  auto work = [&]() {
-    for (;;) {
-      const int i = next.fetch_add(1);
-      if (i >= n) break;
-      if (data[i] == nullptr) {
-        out[i].status = WG_STATUS_INVALID_PARAM;
-        continue;
-      }
-      out[i].status = guarded([&] { return parse_one(data[i], sizes[i], opt, &out[i]); });
-      if (out[i].status != WG_STATUS_OK) out[i] = FrameParse{out[i].status};  // drop partial host data
-    }
-  };
-  const int t = std::max(1, std::min(threads, n));
-  if (t == 1) {
-    work();
-  } else {
-    std::vector<std::thread> pool;
-    for (int k = 0; k < t; ++k) pool.emplace_back(work);
-    for (auto& th : pool) th.join();
-  }
-}
 
 }  // namespace
 
@@ -263,17 +179,34 @@ struct wg_batch {
   double k1_fused_bytes = 0;  // K1 with its RGBA tail: inputs + RGBA (planes are an intermediate)
   std::vector<Timing> timings;  // one per run since the last query
   size_t n_runs_pending = 0;
+  hipEvent_t done = nullptr;    // recorded after the batch's latest work, on the stream it ran on
+  bool done_recorded = false;
 };
 
 namespace {
-void fill_vp8l_info(const wg::VP8LFrame& f, wg_vp8l_info* info, uint32_t* argb, uint32_t* const* transform_data);
-// The single-frame entry points share one lazily created context on device 0.
+// The single-frame entry points share one lazily created context (device 0 unless
+// wg_set_default_device chose another).
+std::mutex g_default_mu;
+wg_ctx* g_default_ctx = nullptr;
+int g_default_device = 0;
 wg_ctx* default_ctx() {
-  static std::mutex mu;
-  static wg_ctx* ctx = nullptr;
-  std::lock_guard<std::mutex> lock(mu);
-  if (!ctx) ctx = wg_ctx_create(0, 1);
-  return ctx;
+  std::lock_guard<std::mutex> lock(g_default_mu);
+  if (!g_default_ctx) g_default_ctx = wg_ctx_create(g_default_device, 0);
+  return g_default_ctx;
+}
+
+void fill_vp8l_info(const wg::VP8LFrame& f, wg_vp8l_info* info, uint32_t* argb, uint32_t* const* transform_data);
+
+// Errors never cross the C ABI as exceptions.
+template <class F>
+int guarded(F&& f) {
+  try {
+    return f();
+  } catch (const std::bad_alloc&) {
+    return WG_STATUS_OUT_OF_MEMORY;
+  } catch (const std::exception&) {
+    return WG_STATUS_OUT_OF_MEMORY;
+  }
 }
 }  // namespace
 
@@ -296,7 +229,7 @@ int wg_get_features(const uint8_t* data, size_t size, wg_features* out) {
 
 int wg_vp8_parse(const uint8_t* data, size_t size, int flags, wg_vp8_info* info, wg_vp8_mb* mbs) {
   if (data == nullptr) return WG_STATUS_INVALID_PARAM;
-  return guarded([&] { return wg::vp8_parse(data, size, flags, info, mbs, nullptr); });
+  return guarded([&] { return wg::vp8_parse(data, size, flags, info, mbs); });
 }
 
 int wg_decode_status(const uint8_t* data, size_t size, const wg_decoder_options* opt) {
@@ -305,8 +238,11 @@ int wg_decode_status(const uint8_t* data, size_t size, const wg_decoder_options*
   o.colorspace = 1;  // MODE_RGBA
   if (opt) o = *opt;
   return guarded([&] {
+    // host stages only; the staged device inputs go to plain heap memory and are dropped
+    wg::StagingArena heap([](size_t b) { return std::malloc(b); }, [](void* q) { std::free(q); });
+    wg::StagingArena::Cursor cur;
     FrameParse fp;
-    return parse_one(data, size, o, &fp);
+    return wg::parse_one(data, size, o, &heap, &cur, &fp);
   });
 }
 
@@ -386,7 +322,18 @@ void fill_vp8l_info(const wg::VP8LFrame& f, wg_vp8l_info* info, uint32_t* argb, 
 namespace {
 wg_batch* batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t* sizes, int n,
                        const wg_decoder_options* opt, int32_t* status);
+
+// Wait for everything the batch has queued (its latest run on whatever stream it ran on, and
+// the context stream) -- stream-scoped, so other contexts on the device are not serialised.
+hipError_t batch_wait(wg_batch* b) {
+  hipError_t e = hipStreamSynchronize(b->ctx->stream);
+  if (e == hipSuccess && b->done_recorded) e = hipEventSynchronize(b->done);
+  return e;
 }
+void batch_mark_done(wg_batch* b, hipStream_t s) {
+  if (b->done && hipEventRecord(b->done, s) == hipSuccess) b->done_recorded = true;
+}
+}  // namespace
 
 extern "C" {
 
@@ -394,10 +341,17 @@ wg_ctx* wg_ctx_create(int device, int host_threads) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return nullptr;
   if (hipSetDevice(device) != hipSuccess) return nullptr;
-  wg_ctx* c = new wg_ctx();
+  wg_ctx* c = new (std::nothrow) wg_ctx();
+  if (!c) return nullptr;
   c->device = device;
   c->host_threads = host_threads > 0 ? host_threads : (int)std::max(1u, std::thread::hardware_concurrency());
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return nullptr;
+  }
+  c->arena.reset(new (std::nothrow) wg::StagingArena(pinned_alloc, pinned_free));
+  if (!c->arena) {
+    hipStreamDestroy(c->stream);
     delete c;
     return nullptr;
   }
@@ -406,26 +360,52 @@ wg_ctx* wg_ctx_create(int device, int host_threads) {
 
 void wg_ctx_destroy(wg_ctx* c) {
   if (!c) return;
+  {
+    std::lock_guard<std::mutex> lock(g_default_mu);
+    if (c == g_default_ctx) g_default_ctx = nullptr;
+  }
   hipSetDevice(c->device);
+  if (c->stream) hipStreamSynchronize(c->stream);
+  c->pool.reset();
+  c->arena.reset();
+  c->cache.trim(0);
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
+}
+
+int wg_set_default_device(int device) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return WG_STATUS_INVALID_PARAM;
+  wg_ctx* old = nullptr;
+  {
+    std::lock_guard<std::mutex> lock(g_default_mu);
+    if (g_default_ctx && g_default_ctx->device != device) {
+      old = g_default_ctx;
+      g_default_ctx = nullptr;
+    }
+    g_default_device = device;
+  }
+  if (old) wg_ctx_destroy(old);
+  return WG_STATUS_OK;
 }
 
 void wg_batch_destroy(wg_batch* b) {
   if (!b) return;
   hipSetDevice(b->ctx->device);
-  hipStreamSynchronize(b->ctx->stream);
+  batch_wait(b);  // nothing may still use the buffers handed back to the cache
   for (auto& t : b->timings)
     for (auto& e : t.ev)
       if (e) hipEventDestroy(e);
-  if (b->d_desc) hipFree(b->d_desc);
-  if (b->d_lldesc) hipFree(b->d_lldesc);
-  if (b->d_adesc) hipFree(b->d_adesc);
-  if (b->d_desc2) hipFree(b->d_desc2);
-  if (b->d_err) hipFree(b->d_err);
-  if (b->d_in) hipFree(b->d_in);
-  if (b->d_planes) hipFree(b->d_planes);
-  if (b->d_rgba) hipFree(b->d_rgba);
+  if (b->done) hipEventDestroy(b->done);
+  DeviceCache& c = b->ctx->cache;
+  c.put(b->d_desc);
+  c.put(b->d_lldesc);
+  c.put(b->d_adesc);
+  c.put(b->d_desc2);
+  c.put(b->d_err);
+  c.put(b->d_in);
+  c.put(b->d_planes);
+  c.put(b->d_rgba);
   delete b;
 }
 
@@ -445,7 +425,7 @@ wg_batch* wg_batch_create_ex(wg_ctx* ctx, const uint8_t* const* data, const size
   if (!ctx || !data || !sizes || n <= 0 || !opt) return nullptr;
   try {
     return batch_create(ctx, data, sizes, n, opt, status);
-  } catch (const std::bad_alloc&) {  // host-side layout / descriptor vectors
+  } catch (const std::exception&) {  // host-side layout / descriptor vectors (batch_create frees its own)
     if (status)
       for (int i = 0; i < n; ++i)
         if (status[i] == WG_STATUS_OK) status[i] = WG_STATUS_OUT_OF_MEMORY;
@@ -456,45 +436,79 @@ wg_batch* wg_batch_create_ex(wg_ctx* ctx, const uint8_t* const* data, const size
 }  // extern "C"
 
 namespace {
+
+struct BatchDeleter {
+  void operator()(wg_batch* b) const { wg_batch_destroy(b); }
+};
+
+// The LLDesc of one lossless stream (transforms in application order = reverse of read
+// order); `d_in` + the arena's device offsets locate its staged coded image and data.
+LLDesc make_ll(const wg::LLMeta& m, const wg::StagingArena& arena, uint8_t* d_in, uint8_t* scratch, uint8_t* rgba,
+               int stride) {
+  LLDesc l{};
+  l.coded = reinterpret_cast<const uint32_t*>(d_in + arena.dev_offset(m.coded));
+  l.coded_bytes = (int32_t)m.coded.bytes;
+  l.scratch = m.two_pass() ? reinterpret_cast<uint32_t*>(scratch) : nullptr;
+  l.scratch_bytes = l.scratch ? m.width * m.height * 4 : 0;
+  l.rgba = rgba;
+  l.rgba_stride = stride;
+  l.width = m.width;
+  l.height = m.height;
+  l.coded_width = m.coded_width;
+  l.n_stages = m.n_transforms;
+  int types[4], bits[4], tiles[4];
+  for (int t = 0; t < l.n_stages; ++t) {
+    const int r = l.n_stages - 1 - t;  // read-order index
+    wg::LLStage& st = l.stages[t];
+    st.type = m.type[r];
+    st.bits = m.bits[r];
+    st.xsize = m.xsize[r];
+    st.tiles_per_row = (st.type == wg::kVP8LPredictor || st.type == wg::kVP8LCrossColor)
+                           ? (st.xsize + (1 << st.bits) - 1) >> st.bits
+                           : 0;
+    st.data = reinterpret_cast<const uint32_t*>(d_in + arena.dev_offset(m.tdata[r]));
+    types[t] = st.type;
+    bits[t] = st.bits;
+    tiles[t] = st.tiles_per_row ? st.tiles_per_row * ((m.height + (1 << st.bits) - 1) >> st.bits) : 0;
+  }
+  l.valid = 1;
+  l.pad1[0] = (uint64_t)wg::vp8l_variant(types, bits, tiles, l.n_stages);  // sort key
+  return l;
+}
+
+// algorithmic bytes of one lossless stream on K3: reads + RGBA write
+double ll_bytes(const wg::LLMeta& m) {
+  const double px = (double)m.width * m.height;
+  double bytes = (double)m.coded.bytes + 4.0 * px;
+  for (int t = 0; t < m.n_transforms; ++t) bytes += (double)m.tdata[t].bytes;
+  if (m.two_pass()) bytes += 8.0 * px;
+  return bytes;
+}
+
 wg_batch* batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t* sizes, int n,
                        const wg_decoder_options* opt, int32_t* status) {
   if (status)
     for (int i = 0; i < n; ++i) status[i] = WG_STATUS_OK;
   std::lock_guard<std::mutex> lock(ctx->mu);
   if (hipSetDevice(ctx->device) != hipSuccess) return nullptr;
-  wg_batch* b = new wg_batch();
+  std::unique_ptr<wg_batch, BatchDeleter> bp(new wg_batch());
+  wg_batch* b = bp.get();
   b->ctx = ctx;
   b->n = n;
   b->opt = *opt;
   const int32_t flags = (opt->bypass_filtering ? WG_FLAG_BYPASS_FILTERING : 0) |
                         (opt->no_fancy_upsampling ? WG_FLAG_NO_FANCY_UPSAMPLING : 0);
   b->flags = flags;
-  parse_all(data, sizes, n, *opt, ctx->host_threads, b->fp);
-  // layout
-  size_t in_b = 0, pl_b = 0, rg_b = 0;
+  if (hipEventCreateWithFlags(&b->done, hipEventDisableTiming) != hipSuccess) b->done = nullptr;
+  wg::StagingArena& arena = *ctx->arena;
+  arena.begin_batch();
+  wg::parse_all(data, sizes, n, *opt, ctx->workers(), &arena, b->fp);
+  b->in_bytes = std::max<size_t>(arena.layout(), kAlign);
+  // layout of the planes / RGBA, and the algorithmic bytes per kernel
+  size_t pl_b = 0, rg_b = 0;
   double k1 = 0, k2 = 0, k3 = 0, k4 = 0;
-  // K3 input (coded image + transform data) and two-pass scratch of one lossless stream;
-  // returns its algorithmic bytes (reads + RGBA write)
-  auto layout_ll = [&](const wg::VP8LFrame& lf, int w, int h, size_t* off_coded, size_t* off_tdata,
-                       size_t* off_scratch) {
-    const double px = (double)w * h;
-    *off_coded = in_b;
-    in_b = align_up(in_b + lf.argb.size() * 4);
-    double bytes = lf.argb.size() * 4.0 + 4.0 * px;
-    for (size_t t = 0; t < lf.transforms.size(); ++t) {
-      off_tdata[t] = in_b;
-      in_b = align_up(in_b + std::max<size_t>(lf.transforms[t].data.size(), 1) * 4);
-      bytes += lf.transforms[t].data.size() * 4.0;
-    }
-    if (ll_two_pass(lf)) {
-      *off_scratch = pl_b;
-      pl_b = align_up(pl_b + (size_t)w * h * 4);
-      bytes += 8.0 * px;
-    }
-    return bytes;
-  };
   for (int i = 0; i < n; ++i) {
-    FrameParse& f = b->fp[i];
+    FrameParse& f = b->fp[(size_t)i];
     if (status) status[i] = f.status;
     if (f.status != WG_STATUS_OK) continue;
     f.off_rgba = rg_b;
@@ -509,18 +523,16 @@ wg_batch* batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t* si
     if (f.lossless) {
       b->n_lossless++;
       b->n_k3++;
-      k3 += layout_ll(f.lf, f.width, f.height, &f.off_coded, f.off_tdata, &f.off_scratch);
+      if (f.ll.two_pass()) {
+        f.off_scratch = pl_b;
+        pl_b = align_up(pl_b + (size_t)f.width * f.height * 4);
+      }
+      k3 += ll_bytes(f.ll);
       continue;
     }
     b->n_lossy++;
-    const wg_vp8_info& inf = f.sf.info;
+    const wg_vp8_info& inf = f.info;
     const size_t nmb = (size_t)inf.mb_w * inf.mb_h;
-    f.off_recs = in_b;
-    in_b = align_up(in_b + nmb * sizeof(MbRec));
-    f.off_rows = in_b;
-    in_b = align_up(in_b + (size_t)inf.mb_h * 4);
-    f.off_blocks = in_b;
-    in_b = align_up(in_b + f.sf.blocks.size() * 2);
     f.off_y = pl_b;
     pl_b = align_up(pl_b + nmb * 256);
     f.off_u = pl_b;
@@ -546,28 +558,28 @@ wg_batch* batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t* si
       f.off_vc = pl_b;
       pl_b = align_up(pl_b + (size_t)f.uvc_stride * ((f.out_h + 1) >> 1));
     }
-    // algorithmic bytes: K1 reads records + coefficients, writes MB-padded
-    // planes; K2 reads cropped planes, writes RGBA.
-    const double uvpx = 2.0 * ((inf.width + 1) / 2) * (double)((inf.height + 1) / 2);
-    k1 += (double)nmb * sizeof(MbRec) + inf.mb_h * 4.0 + f.sf.blocks.size() * 2.0 + nmb * 384.0;
-    b->k1_fused_bytes += (double)nmb * sizeof(MbRec) + inf.mb_h * 4.0 + f.sf.blocks.size() * 2.0 +
-                         4.0 * inf.width * (double)inf.height;
+    // algorithmic bytes: K1 reads records + row index + coefficient blocks, writes
+    // MB-padded planes (or, with its RGBA tail, the RGBA); K2 reads cropped planes, writes RGBA.
+    const double k1_in = (double)nmb * sizeof(MbRec) + inf.mb_h * 4.0 + (double)f.n_blocks * 32.0;
+    k1 += k1_in + nmb * 384.0;
+    b->k1_fused_bytes += k1_in + 4.0 * inf.width * (double)inf.height;
     const double opx = (double)f.out_w * f.out_h;
     k2 += opx + 2.0 * ((f.out_w + 1) / 2) * (double)((f.out_h + 1) / 2) + 4.0 * opx;
-    (void)uvpx;
     if (f.alpha) {
       // K4 reads the filtered alpha (raw bytes, or K3's RGBA of the alpha stream) and
       // rewrites the RGBA A bytes (dword read-modify-write)
       b->n_alpha++;
       if (f.ah.method == 1) {
         b->n_k3++;
-        k3 += layout_ll(f.af, f.width, f.height, &f.off_acoded, f.off_atdata, &f.off_ascratch);
+        if (f.al.two_pass()) {
+          f.off_ascratch = pl_b;
+          pl_b = align_up(pl_b + (size_t)f.width * f.height * 4);
+        }
+        k3 += ll_bytes(f.al);
         f.off_argba = pl_b;
         pl_b = align_up(pl_b + (size_t)f.width * f.height * 4);
         k4 += 4.0 * px;
       } else {
-        f.off_araw = in_b;
-        in_b = align_up(in_b + (size_t)f.width * f.height);
         k4 += px;
       }
       f.off_aplane = pl_b;
@@ -579,97 +591,44 @@ wg_batch* batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t* si
   b->kbytes[2] = k3;
   b->kbytes[0] = k1;
   b->kbytes[1] = k2;
-  b->in_bytes = std::max<size_t>(in_b, kAlign);
   b->plane_bytes = std::max<size_t>(pl_b, kAlign);
   b->rgba_bytes = std::max<size_t>(rg_b, kAlign);
   auto fail = [&](int st) {
     if (status)
       for (int i = 0; i < n; ++i)
         if (status[i] == WG_STATUS_OK) status[i] = st;
-    wg_batch_destroy(b);
-    return (wg_batch*)nullptr;
+    return (wg_batch*)nullptr;  // bp's deleter hands every buffer back
   };
-  if (hipMalloc(&b->d_in, b->in_bytes) != hipSuccess || hipMalloc(&b->d_planes, b->plane_bytes) != hipSuccess ||
-      hipMalloc(&b->d_rgba, b->rgba_bytes) != hipSuccess ||
-      hipMalloc(&b->d_desc, sizeof(FrameDesc) * (size_t)n) != hipSuccess ||
-      hipMalloc(&b->d_lldesc, sizeof(LLDesc) * (size_t)std::max(b->n_k3, 1)) != hipSuccess ||
-      hipMalloc(&b->d_adesc, sizeof(AlphaDesc) * (size_t)std::max(b->n_alpha, 1)) != hipSuccess ||
-      hipMalloc(&b->d_err, sizeof(int)) != hipSuccess || hipMemset(b->d_err, 0, sizeof(int)) != hipSuccess)
+  DeviceCache& cache = ctx->cache;
+  b->d_in = static_cast<uint8_t*>(cache.get(b->in_bytes));
+  b->d_planes = static_cast<uint8_t*>(cache.get(b->plane_bytes));
+  b->d_rgba = static_cast<uint8_t*>(cache.get(b->rgba_bytes));
+  b->d_desc = static_cast<FrameDesc*>(cache.get(sizeof(FrameDesc) * (size_t)n));
+  b->d_lldesc = static_cast<LLDesc*>(cache.get(sizeof(LLDesc) * (size_t)std::max(b->n_k3, 1)));
+  b->d_adesc = static_cast<AlphaDesc*>(cache.get(sizeof(AlphaDesc) * (size_t)std::max(b->n_alpha, 1)));
+  b->d_err = static_cast<int*>(cache.get(sizeof(int)));
+  if (!b->d_in || !b->d_planes || !b->d_rgba || !b->d_desc || !b->d_lldesc || !b->d_adesc || !b->d_err ||
+      hipMemsetAsync(b->d_err, 0, sizeof(int), ctx->stream) != hipSuccess)
     return fail(WG_STATUS_OUT_OF_MEMORY);
-  // stage inputs in pinned memory, one H2D copy
-  uint8_t* h_in = nullptr;
-  if (hipHostMalloc(reinterpret_cast<void**>(&h_in), b->in_bytes, hipHostMallocDefault) != hipSuccess)
-    return fail(WG_STATUS_OUT_OF_MEMORY);
-  // Staging copies are collected first and run on the host threads afterwards (the
-  // parsed data they read is released only after that).
-  struct CopyJob {
-    uint8_t* dst;
-    const void* src;
-    size_t n;
-  };
-  std::vector<CopyJob> jobs;
-  auto stage = [&](size_t off, const void* src, size_t nbytes) {
-    if (nbytes) jobs.push_back(CopyJob{h_in + off, src, nbytes});
-  };
-  // the LLDesc of one lossless stream (transforms in application order = reverse of read
-  // order); its coded image and transform data go to the staging buffer
-  auto make_ll = [&](wg::VP8LFrame& lf, int w, int h, size_t off_coded, const size_t* off_tdata,
-                     size_t off_scratch, uint8_t* rgba, int stride) {
-    LLDesc l{};
-    stage(off_coded, lf.argb.data(), lf.argb.size() * 4);
-    l.coded = reinterpret_cast<const uint32_t*>(b->d_in + off_coded);
-    l.coded_bytes = (int32_t)(lf.argb.size() * 4);
-    l.scratch = ll_two_pass(lf) ? reinterpret_cast<uint32_t*>(b->d_planes + off_scratch) : nullptr;
-    l.scratch_bytes = l.scratch ? w * h * 4 : 0;
-    l.rgba = rgba;
-    l.rgba_stride = stride;
-    l.width = w;
-    l.height = h;
-    l.coded_width = lf.coded_width;
-    l.n_stages = (int32_t)lf.transforms.size();
-    int types[4], bits[4], tiles[4];
-    for (int t = 0; t < l.n_stages; ++t) {
-      const wg::VP8LTransform& tr = lf.transforms[(size_t)(l.n_stages - 1 - t)];
-      const size_t off = off_tdata[l.n_stages - 1 - t];
-      stage(off, tr.data.data(), tr.data.size() * 4);
-      wg::LLStage& st = l.stages[t];
-      st.type = tr.type;
-      st.bits = tr.bits;
-      st.xsize = tr.xsize;
-      st.tiles_per_row = (tr.type == wg::kVP8LPredictor || tr.type == wg::kVP8LCrossColor)
-                             ? (tr.xsize + (1 << tr.bits) - 1) >> tr.bits
-                             : 0;
-      st.data = reinterpret_cast<const uint32_t*>(b->d_in + off);
-      types[t] = st.type;
-      bits[t] = st.bits;
-      tiles[t] = st.tiles_per_row ? st.tiles_per_row * ((h + (1 << st.bits) - 1) >> st.bits) : 0;
-    }
-    l.valid = 1;
-    l.pad1[0] = (uint64_t)wg::vp8l_variant(types, bits, tiles, l.n_stages);  // sort key
-    return l;
-  };
-  b->desc.assign(n, FrameDesc{});
+  b->desc.assign((size_t)n, FrameDesc{});
   for (int i = 0; i < n; ++i) {
-    FrameParse& f = b->fp[i];
-    FrameDesc& d = b->desc[i];
+    FrameParse& f = b->fp[(size_t)i];
+    FrameDesc& d = b->desc[(size_t)i];
     if (f.status != WG_STATUS_OK) continue;
     d.rgba = b->d_rgba + f.off_rgba;
     d.width = f.width;
     d.height = f.height;
     d.rgba_stride = 4 * f.rgba_w;
     if (f.lossless) {  // K1/K2 skip it (valid = 0); K3 gets an LLDesc
-      b->lldesc.push_back(make_ll(f.lf, f.width, f.height, f.off_coded, f.off_tdata, f.off_scratch, d.rgba,
-                                  d.rgba_stride));
+      b->lldesc.push_back(make_ll(f.ll, arena, b->d_in, b->d_planes + f.off_scratch, d.rgba, d.rgba_stride));
       continue;
     }
-    const wg_vp8_info& inf = f.sf.info;
-    stage(f.off_recs, f.sf.mbs.data(), f.sf.mbs.size() * sizeof(MbRec));
-    stage(f.off_rows, f.sf.row_block0.data(), f.sf.row_block0.size() * 4);
-    stage(f.off_blocks, f.sf.blocks.data(), f.sf.blocks.size() * 2);
-    d.mbs = reinterpret_cast<const MbRec*>(b->d_in + f.off_recs);
-    d.row_block0 = reinterpret_cast<const uint32_t*>(b->d_in + f.off_rows);
-    d.blocks = reinterpret_cast<const int16_t*>(b->d_in + f.off_blocks);
-    d.blocks_bytes = (int32_t)(f.sf.blocks.size() * 2);
+    const wg_vp8_info& inf = f.info;
+    uint8_t* in = b->d_in + arena.dev_offset(f.input);
+    d.mbs = reinterpret_cast<const MbRec*>(in);
+    d.row_block0 = reinterpret_cast<const uint32_t*>(in + f.off_rows);
+    d.blocks = reinterpret_cast<const int16_t*>(in + f.off_blocks);
+    d.blocks_bytes = (int32_t)(f.n_blocks * 32);
     d.y = b->d_planes + f.off_y;
     d.cols = f.wide ? b->d_planes + f.off_cols : nullptr;
     d.u = b->d_planes + f.off_u;
@@ -684,12 +643,11 @@ wg_batch* batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t* si
     if (f.alpha) {
       AlphaDesc a{};
       if (f.ah.method == 1) {
-        b->lldesc.push_back(make_ll(f.af, f.width, f.height, f.off_acoded, f.off_atdata, f.off_ascratch,
-                                    b->d_planes + f.off_argba, 4 * f.width));
+        b->lldesc.push_back(make_ll(f.al, arena, b->d_in, b->d_planes + f.off_ascratch, b->d_planes + f.off_argba,
+                                    4 * f.width));
         a.green = b->d_planes + f.off_argba;
       } else {
-        stage(f.off_araw, f.alpha_raw, (size_t)f.width * f.height);
-        a.raw = b->d_in + f.off_araw;
+        a.raw = b->d_in + arena.dev_offset(f.araw);
       }
       a.plane = b->d_planes + f.off_aplane;
       a.rgba = d.rgba;
@@ -705,46 +663,17 @@ wg_batch* batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t* si
       b->adesc.push_back(a);
     }
   }
-  // run the staging copies on the host threads (large ones split into 4 MB pieces)
-  {
-    constexpr size_t kPiece = size_t(4) << 20;
-    std::vector<CopyJob> pieces;
-    for (const CopyJob& j : jobs)
-      for (size_t o = 0; o < j.n; o += kPiece)
-        pieces.push_back(CopyJob{j.dst + o, static_cast<const uint8_t*>(j.src) + o, std::min(kPiece, j.n - o)});
-    std::atomic<size_t> next{0};
-    auto work = [&]() {
-      for (size_t k; (k = next.fetch_add(1)) < pieces.size();) std::memcpy(pieces[k].dst, pieces[k].src, pieces[k].n);
-    };
-    const int t = (int)std::max<size_t>(1, std::min<size_t>((size_t)ctx->host_threads, pieces.size()));
-    std::vector<std::thread> pool;
-    for (int k = 1; k < t; ++k) pool.emplace_back(work);
-    work();
-    for (auto& th : pool) th.join();
-  }
-  // release host-side copies of the parsed data: the device owns them now
-  for (int i = 0; i < n; ++i) {
-    FrameParse& f = b->fp[i];
-    std::vector<MbRec>().swap(f.sf.mbs);
-    f.sf.blocks.release();
-    std::vector<uint32_t>().swap(f.sf.row_block0);
-    wg::VP8LFrame().transforms.swap(f.lf.transforms);
-    std::vector<uint32_t>().swap(f.lf.argb);
-    wg::VP8LFrame().transforms.swap(f.af.transforms);
-    std::vector<uint32_t>().swap(f.af.argb);
-    f.alpha_raw = nullptr;
-  }
   // Full-frame RGBA (no crop window anywhere in the batch): K1 converts each frame in its
   // own tail instead of a separate K2 launch (wg_batch_set_emit() switches back).
   b->fused = !b->any_crop;
   if (b->fused)
     for (int i = 0; i < n; ++i)
-      if (b->desc[i].valid) b->desc[i].flags |= wg::kFrameEmitRgba;
+      if (b->desc[(size_t)i].valid) b->desc[(size_t)i].flags |= wg::kFrameEmitRgba;
   if (b->any_crop) {  // K2's view: cropped lossy frames read their compact planes
     b->desc2 = b->desc;
     for (int i = 0; i < n; ++i) {
-      FrameParse& f = b->fp[i];
-      FrameDesc& d2 = b->desc2[i];
+      FrameParse& f = b->fp[(size_t)i];
+      FrameDesc& d2 = b->desc2[(size_t)i];
       if (f.status != WG_STATUS_OK || f.lossless || !f.cropped) continue;
       d2.y = b->d_planes + f.off_yc;
       d2.u = b->d_planes + f.off_uc;
@@ -755,12 +684,17 @@ wg_batch* batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t* si
       d2.height = f.out_h;
     }
   }
-  hipError_t e = hipMemcpyAsync(b->d_in, h_in, b->in_bytes, hipMemcpyHostToDevice, ctx->stream);
+  // the staged inputs: one copy per arena chunk, from pinned memory
+  hipError_t e = hipSuccess;
+  for (size_t c = 0; c < arena.n_chunks() && e == hipSuccess; ++c) {
+    const wg::StagingArena::Chunk& ch = arena.chunk(c);
+    if (ch.used) e = hipMemcpyAsync(b->d_in + ch.dev_base, ch.p, ch.used, hipMemcpyHostToDevice, ctx->stream);
+  }
   if (e == hipSuccess && b->any_crop) {
-    e = hipMalloc(&b->d_desc2, sizeof(FrameDesc) * (size_t)n);
-    if (e == hipSuccess)
-      e = hipMemcpyAsync(b->d_desc2, b->desc2.data(), sizeof(FrameDesc) * (size_t)n, hipMemcpyHostToDevice,
-                         ctx->stream);
+    b->d_desc2 = static_cast<FrameDesc*>(cache.get(sizeof(FrameDesc) * (size_t)n));
+    e = b->d_desc2 ? hipMemcpyAsync(b->d_desc2, b->desc2.data(), sizeof(FrameDesc) * (size_t)n, hipMemcpyHostToDevice,
+                                    ctx->stream)
+                   : hipErrorOutOfMemory;
   }
   if (e == hipSuccess)
     e = hipMemcpyAsync(b->d_desc, b->desc.data(), sizeof(FrameDesc) * (size_t)n, hipMemcpyHostToDevice,
@@ -775,10 +709,13 @@ wg_batch* batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t* si
   if (e == hipSuccess && !b->adesc.empty())
     e = hipMemcpyAsync(b->d_adesc, b->adesc.data(), sizeof(AlphaDesc) * b->adesc.size(), hipMemcpyHostToDevice,
                        ctx->stream);
+  // the staging memory is reused by the next batch: the copies complete here
   if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
-  hipHostFree(h_in);
-  if (e != hipSuccess) return fail(WG_STATUS_OUT_OF_MEMORY);
-  return b;
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(WG_STATUS_OUT_OF_MEMORY);
+  }
+  return bp.release();
 }
 }  // namespace
 
@@ -844,6 +781,7 @@ int wg_batch_run(wg_batch* b, void* stream) {
     if (e != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
   }
   hipEventRecord(t.ev[4], s);
+  batch_mark_done(b, s);
   return WG_STATUS_OK;
 }
 
@@ -911,6 +849,7 @@ int wg_batch_run_emit(wg_batch* b, void* stream) {
   hipError_t e = wg::launch_yuv_to_rgba(b->d_desc, nullptr, b->n, b->max_out_w, b->max_out_h,
                                         (b->flags & WG_FLAG_NO_FANCY_UPSAMPLING) ? 0 : 1, s);
   for (int k = 2; k < 5; ++k) hipEventRecord(t.ev[k], s);
+  batch_mark_done(b, s);
   return e == hipSuccess ? WG_STATUS_OK : WG_STATUS_UNSUPPORTED_FEATURE;
 }
 
@@ -935,8 +874,7 @@ namespace {
 // Wait for the batch's work and check the kernels' error word.
 int batch_sync(wg_batch* b) {
   hipSetDevice(b->ctx->device);
-  hipError_t e = hipStreamSynchronize(b->ctx->stream);
-  if (e == hipSuccess) e = hipDeviceSynchronize();
+  hipError_t e = batch_wait(b);
   int err = 0;
   if (e == hipSuccess) e = hipMemcpy(&err, b->d_err, sizeof(int), hipMemcpyDeviceToHost);
   return (e != hipSuccess || err) ? WG_STATUS_USER_ABORT : WG_STATUS_OK;
@@ -945,6 +883,25 @@ const uint8_t* window_ptr(const wg_batch* b, int i) {
   const FrameParse& f = b->fp[i];
   const FrameDesc& d = b->desc[i];
   return d.rgba + (size_t)f.win_y * d.rgba_stride + 4 * (size_t)f.win_x;
+}
+// Every OK frame's RGBA window to out[i] (stride strides[i]): one wait for the batch, the
+// copies queued on the context stream, one wait for them.
+int download_rgba_all(wg_batch* b, uint8_t* const* out, const int32_t* strides, int32_t* status) {
+  int st = batch_sync(b);
+  if (st != WG_STATUS_OK) return st;
+  hipError_t e = hipSuccess;
+  for (int i = 0; i < b->n && e == hipSuccess; ++i) {
+    if (status[i] != WG_STATUS_OK) continue;
+    const FrameParse& f = b->fp[(size_t)i];
+    if (out[i] == nullptr || strides[i] < 4 * f.out_w) {
+      status[i] = WG_STATUS_INVALID_PARAM;
+      continue;
+    }
+    e = hipMemcpy2DAsync(out[i], strides[i], window_ptr(b, i), b->desc[(size_t)i].rgba_stride, 4 * (size_t)f.out_w,
+                         f.out_h, hipMemcpyDeviceToHost, b->ctx->stream);
+  }
+  const hipError_t se = hipStreamSynchronize(b->ctx->stream);
+  return (e != hipSuccess || se != hipSuccess) ? WG_STATUS_USER_ABORT : WG_STATUS_OK;
 }
 }  // namespace
 
@@ -975,17 +932,20 @@ int wg_batch_download(wg_batch* b, int i, uint8_t* out, int stride) {
   wg::EmitDesc* d_ed = nullptr;
   wg::EmitDesc ed{window_ptr(b, i), nullptr, b->desc[i].rgba_stride, (int32_t)row, f.out_w, f.out_h,
                   b->opt.colorspace, b->opt.flip ? 1 : 0, 1, 0};
-  hipError_t e = hipMalloc(&d_out, row * f.out_h);
-  if (e == hipSuccess) e = hipMalloc(&d_ed, sizeof(ed));
+  DeviceCache& cache = b->ctx->cache;
+  d_out = static_cast<uint8_t*>(cache.get(row * f.out_h));
+  d_ed = static_cast<wg::EmitDesc*>(cache.get(sizeof(ed)));
+  hipError_t e = d_out && d_ed ? hipSuccess : hipErrorOutOfMemory;
   if (e == hipSuccess) {
     ed.dst = d_out;
     e = hipMemcpyAsync(d_ed, &ed, sizeof(ed), hipMemcpyHostToDevice, b->ctx->stream);
   }
   if (e == hipSuccess) e = wg::launch_emit(d_ed, 1, f.out_w * f.out_h, b->ctx->stream);
   if (e == hipSuccess) e = hipMemcpy2DAsync(out, stride, d_out, row, row, f.out_h, hipMemcpyDeviceToHost, b->ctx->stream);
-  if (e == hipSuccess) e = hipStreamSynchronize(b->ctx->stream);
-  if (d_out) hipFree(d_out);
-  if (d_ed) hipFree(d_ed);
+  const hipError_t se = hipStreamSynchronize(b->ctx->stream);  // before the buffers go back
+  if (e == hipSuccess) e = se;
+  cache.put(d_out);
+  cache.put(d_ed);
   return e == hipSuccess ? WG_STATUS_OK : WG_STATUS_USER_ABORT;
 }
 
@@ -995,7 +955,7 @@ int wg_batch_download_yuv(wg_batch* b, int i, uint8_t* y, uint8_t* u, uint8_t* v
   if (b->fp[i].lossless) return WG_STATUS_UNSUPPORTED_FEATURE;  // VP8L has no YUV planes
   const FrameDesc& d = b->desc[i];
   hipSetDevice(b->ctx->device);
-  hipError_t e = hipDeviceSynchronize();
+  hipError_t e = batch_wait(b);
   const int uw = (d.width + 1) / 2, uh = (d.height + 1) / 2;
   if (e == hipSuccess && y) e = hipMemcpy2D(y, d.width, d.y, d.y_stride, d.width, d.height, hipMemcpyDeviceToHost);
   if (e == hipSuccess && u) e = hipMemcpy2D(u, uw, d.u, d.uv_stride, uw, uh, hipMemcpyDeviceToHost);
@@ -1009,19 +969,38 @@ int wg_decode_rgba_batch(wg_ctx* ctx, const uint8_t* const* data, const size_t* 
   wg_batch* b = wg_batch_create(ctx, data, sizes, n, flags, status);
   if (!b) return WG_STATUS_OUT_OF_MEMORY;
   int st = wg_batch_run(b, nullptr);
-  if (st == WG_STATUS_OK && hipStreamSynchronize(ctx->stream) != hipSuccess) st = WG_STATUS_USER_ABORT;
-  if (st == WG_STATUS_OK) {
-    for (int i = 0; i < n; ++i) {
-      if (status[i] != WG_STATUS_OK) continue;
-      if (rgba[i] == nullptr || strides[i] < 4 * b->desc[i].width) {
-        status[i] = WG_STATUS_INVALID_PARAM;
-        continue;
-      }
-      status[i] = wg_batch_download_rgba(b, i, rgba[i], strides[i]);
-    }
-  }
+  if (st == WG_STATUS_OK) st = download_rgba_all(b, rgba, strides, status);
   wg_batch_destroy(b);
   return st;
+}
+
+int wg_decode_rgba_batch_multi(wg_ctx* const* ctxs, int n_ctx, const uint8_t* const* data, const size_t* sizes,
+                               int n, uint8_t* const* rgba, const int32_t* strides, int32_t* status, int32_t flags) {
+  if (!ctxs || n_ctx <= 0 || !data || !sizes || !rgba || !strides || !status || n <= 0) return WG_STATUS_INVALID_PARAM;
+  for (int k = 0; k < n_ctx; ++k)
+    if (!ctxs[k]) return WG_STATUS_INVALID_PARAM;
+  const int shards = std::min(n_ctx, n);
+  std::vector<int> rc((size_t)shards, WG_STATUS_OK);
+  // contiguous shards, frames [k * n / shards, (k + 1) * n / shards) on context k
+  auto run = [&](int k) {
+    const int a = (int)((int64_t)k * n / shards), e = (int)((int64_t)(k + 1) * n / shards);
+    rc[(size_t)k] = guarded([&] {
+      return wg_decode_rgba_batch(ctxs[k], data + a, sizes + a, e - a, rgba + a, strides + a, status + a, flags);
+    });
+  };
+  std::vector<std::thread> th;
+  for (int k = 1; k < shards; ++k) {
+    try {
+      th.emplace_back(run, k);
+    } catch (const std::system_error&) {
+      run(k);  // no thread: this shard on the calling thread
+    }
+  }
+  run(0);
+  for (auto& t : th) t.join();
+  for (int r : rc)
+    if (r != WG_STATUS_OK) return r;
+  return WG_STATUS_OK;
 }
 
 int wg_decode_batch(wg_ctx* ctx, const uint8_t* const* data, const size_t* sizes, int n, const wg_decoder_options* opt,
@@ -1046,8 +1025,9 @@ int wg_decode_batch(wg_ctx* ctx, const uint8_t* const* data, const size_t* sizes
     }
     uint8_t* d_out = nullptr;
     wg::EmitDesc* d_ed = nullptr;
-    hipError_t e = hipMalloc(&d_out, std::max<size_t>(total, kAlign));
-    if (e == hipSuccess) e = hipMalloc(&d_ed, sizeof(wg::EmitDesc) * (size_t)n);
+    d_out = static_cast<uint8_t*>(ctx->cache.get(std::max<size_t>(total, kAlign)));
+    d_ed = static_cast<wg::EmitDesc*>(ctx->cache.get(sizeof(wg::EmitDesc) * (size_t)n));
+    hipError_t e = d_out && d_ed ? hipSuccess : hipErrorOutOfMemory;
     for (int i = 0; e == hipSuccess && i < n; ++i) {
       const FrameParse& f = b->fp[i];
       if (f.status != WG_STATUS_OK) continue;
@@ -1071,18 +1051,11 @@ int wg_decode_batch(wg_ctx* ctx, const uint8_t* const* data, const size_t* sizes
           hipSuccess)
         status[i] = WG_STATUS_USER_ABORT;
     }
-    if (d_out) hipFree(d_out);
-    if (d_ed) hipFree(d_ed);
+    hipStreamSynchronize(ctx->stream);  // (an error path may have left K6 queued)
+    ctx->cache.put(d_out);
+    ctx->cache.put(d_ed);
   } else if (st == WG_STATUS_OK) {
-    if (hipStreamSynchronize(ctx->stream) != hipSuccess) st = WG_STATUS_USER_ABORT;
-    for (int i = 0; st == WG_STATUS_OK && i < n; ++i) {
-      if (status[i] != WG_STATUS_OK) continue;
-      if (out[i] == nullptr || strides[i] < 4 * b->fp[i].out_w) {
-        status[i] = WG_STATUS_INVALID_PARAM;
-        continue;
-      }
-      status[i] = wg_batch_download_rgba(b, i, out[i], strides[i]);
-    }
+    st = download_rgba_all(b, out, strides, status);
   }
   wg_batch_destroy(b);
   return st;
@@ -1232,8 +1205,11 @@ int wg_anim_decode(wg_ctx* ctx, const uint8_t* data, size_t size, uint8_t* canva
     std::lock_guard<std::mutex> lock(ctx->mu);
     hipSetDevice(ctx->device);
     hipError_t e = st == WG_STATUS_OK ? hipSuccess : hipErrorUnknown;
-    if (e == hipSuccess) e = hipMalloc(&d_fd, sizeof(AnimFrameDesc) * (size_t)n);
-    if (e == hipSuccess) e = hipMalloc(&d_canvases, canvas_bytes * (size_t)n);
+    if (e == hipSuccess) {
+      d_fd = static_cast<AnimFrameDesc*>(ctx->cache.get(sizeof(AnimFrameDesc) * (size_t)n));
+      d_canvases = static_cast<uint8_t*>(ctx->cache.get(canvas_bytes * (size_t)n));
+      if (!d_fd || !d_canvases) e = hipErrorOutOfMemory;
+    }
     if (e == hipSuccess)
       e = hipMemcpyAsync(d_fd, fd.data(), sizeof(AnimFrameDesc) * (size_t)n, hipMemcpyHostToDevice, ctx->stream);
     if (e == hipSuccess)
@@ -1244,8 +1220,9 @@ int wg_anim_decode(wg_ctx* ctx, const uint8_t* data, size_t size, uint8_t* canva
     int err = 0;
     if (e == hipSuccess) e = hipMemcpy(&err, b->d_err, sizeof(int), hipMemcpyDeviceToHost);
     if (st == WG_STATUS_OK && (e != hipSuccess || err)) st = WG_STATUS_USER_ABORT;
-    if (d_fd) hipFree(d_fd);
-    if (d_canvases) hipFree(d_canvases);
+    hipStreamSynchronize(ctx->stream);
+    ctx->cache.put(d_fd);
+    ctx->cache.put(d_canvases);
   }
   wg_batch_destroy(b);
   return st;

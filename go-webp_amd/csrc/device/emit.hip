@@ -93,23 +93,6 @@ __global__ void __launch_bounds__(kThreads) emit_kernel(const EmitDesc* __restri
 
 }  // namespace
 
-int output_bpp(int mode) {
-  switch (mode) {
-    case 0:
-    case 2: return 3;
-    case 5:
-    case 6:
-    case 10: return 2;
-    case 1:
-    case 3:
-    case 4:
-    case 7:
-    case 8:
-    case 9: return 4;
-    default: return 0;
-  }
-}
-
 hipError_t launch_emit(const EmitDesc* d_frames, int n_frames, int max_pixels, hipStream_t stream) {
   if (n_frames <= 0) return hipSuccess;
   const int blocks = std::min(1024, std::max(1, (max_pixels + kThreads - 1) / kThreads));

@@ -33,7 +33,6 @@ hipError_t launch_vp8l_transforms(const LLDesc* d_frames, const int* group_count
 hipError_t launch_alpha(const AlphaDesc* d_frames, int n_frames, hipStream_t stream);
 
 // K6: output colorspace / cropping window / flip, RGBA -> WEBP_CSP_MODE (0..10) bytes.
-int output_bpp(int mode);  // 3, 4 or 2 bytes per pixel; 0 for a mode K6 does not produce
 hipError_t launch_emit(const EmitDesc* d_frames, int n_frames, int max_pixels, hipStream_t stream);
 
 // K5: animation canvases (frames in display order, already decoded) -> n_frames canvases of

@@ -198,9 +198,11 @@ __device__ __forceinline__ void quad_transpose(int t[4]) {
 }
 
 // TransformOne (dec.c.go:49-88) of a 4x4 block spread over a lane quad.  In: column q of
-// the coefficients (c0..c3 = in[q], in[4+q], in[8+q], in[12+q]).  Out: residuals
-// (v >> 3) of pixel row q, x = 0..3.
-__device__ __forceinline__ void idct_quad(int q, uint2 cv, int r[4]) {
+// the coefficients (c0..c3 = in[q], in[4+q], in[8+q], in[12+q]) and `dadd`, the block's DC
+// from the Y2 transform (0 unless i16 luma): in[0] enters the vertical pass of column 0 only
+// as a common term of its four outputs, i.e. every row's tmp[0 + row], so it is added where
+// the horizontal pass reads that term.  Out: residuals (v >> 3) of pixel row q, x = 0..3.
+__device__ __forceinline__ void idct_quad(int q, uint2 cv, int dadd, int r[4]) {
   const int c0 = (int16_t)(cv.x & 0xffff), c1 = (int16_t)(cv.x >> 16);
   const int c2 = (int16_t)(cv.y & 0xffff), c3 = (int16_t)(cv.y >> 16);
   int t[4];
@@ -214,8 +216,8 @@ __device__ __forceinline__ void idct_quad(int q, uint2 cv, int r[4]) {
     t[2] = b - c;
     t[3] = a - d;
   }
-  quad_transpose(t);  // lane q ends with t[c] = tmp[4c + q]
-  const int dc = t[0] + 4;
+  quad_transpose(t);  // lane q ends with t[c] = tmp[4q + c]
+  const int dc = t[0] + 4 + dadd;
   const int a = dc + t[2];
   const int b = dc - t[2];
   const int c = mul2(t[1]) - mul1(t[3]);
@@ -229,15 +231,45 @@ __device__ __forceinline__ void idct_quad(int q, uint2 cv, int r[4]) {
 // Residuals of one IDCT pass (6 per MB step: luma blocks b0, b0+8 and chroma, for both
 // roles).  When every block in the pass (all four MBs) is zero or DC-only, TransformOne
 // reduces to (in[0] + 4) >> 3 on every pixel (TransformDC, dec.c.go:112-118): broadcast
-// the DC from the quad's column-0 lane instead of running both butterfly passes.
-__device__ __forceinline__ void idct_pass(int q, uint2 cv, int r[4]) {
+// the DC from the quad's column-0 lane instead of running both butterfly passes.  An i16
+// block's stored in[0] is 0 (its DC is dadd, from Y2), any other block's dadd is 0.
+__device__ __forceinline__ void idct_pass(int q, uint2 cv, int dadd, int r[4]) {
   const uint32_t ac = (q == 0 ? (cv.x & 0xffff0000u) : cv.x) | cv.y;
   if (__all(ac == 0)) {
-    const int dc = __builtin_amdgcn_mov_dpp((int)(int16_t)(cv.x & 0xffff), 0x00, 0xF, 0xF, true);
+    const int dc = __builtin_amdgcn_mov_dpp((int)(int16_t)(cv.x & 0xffff), 0x00, 0xF, 0xF, true) + dadd;
     r[0] = r[1] = r[2] = r[3] = (dc + 4) >> 3;
   } else {
-    idct_quad(q, cv, r);
+    idct_quad(q, cv, dadd, r);
   }
+}
+
+// TransformWHT (dec.c.go:142-167; called from ParseResiduals, vp8_dec.go:615-634) of the
+// MB's Y2 block, computed by every lane quad of the MB's 16 lanes: lane q holds column q of
+// Y2 (the same layout as the IDCT).  Vertical pass, quad transpose, horizontal pass: lane q
+// then holds row q of the 4x4 matrix of Y DCs (row = block row by, element = block column
+// bx), stored as int16 like libwebp's.  Lane (p, q), p = m >> 2, keeps element p, and the
+// quad broadcasts give every lane DC[by][p] for by = 0..3: its roles' luma blocks p + 4s
+// (row s) and p + 4s + 8 (row s + 2) read dc[s] and dc[s + 2].
+__device__ __forceinline__ void wht_quad(int p, uint2 cv, int dc[4]) {
+  const int c0 = (int16_t)(cv.x & 0xffff), c1 = (int16_t)(cv.x >> 16);
+  const int c2 = (int16_t)(cv.y & 0xffff), c3 = (int16_t)(cv.y >> 16);
+  int t[4];
+  {
+    const int a0 = c0 + c3, a1 = c1 + c2, a2 = c1 - c2, a3 = c0 - c3;
+    t[0] = a0 + a1;  // tmp[0 + q]
+    t[1] = a3 + a2;  // tmp[4 + q]
+    t[2] = a0 - a1;  // tmp[8 + q]
+    t[3] = a3 - a2;  // tmp[12 + q]
+  }
+  quad_transpose(t);  // lane q: t[c] = tmp[4q + c]
+  const int d0 = t[0] + 3;
+  const int a0 = d0 + t[3], a1 = t[1] + t[2], a2 = t[1] - t[2], a3 = d0 - t[3];
+  const int e = p == 0 ? a0 + a1 : p == 1 ? a3 + a2 : p == 2 ? a0 - a1 : a3 - a2;
+  const int v = (int16_t)(e >> 3);
+  dc[0] = __builtin_amdgcn_mov_dpp(v, 0x00, 0xF, 0xF, true);  // quad_perm [0,0,0,0]
+  dc[1] = __builtin_amdgcn_mov_dpp(v, 0x55, 0xF, 0xF, true);  // [1,1,1,1]
+  dc[2] = __builtin_amdgcn_mov_dpp(v, 0xAA, 0xF, 0xF, true);  // [2,2,2,2]
+  dc[3] = __builtin_amdgcn_mov_dpp(v, 0xFF, 0xF, 0xF, true);  // [3,3,3,3]
 }
 
 // clamp(a..d, 0, 255) packed little-endian into one dword with gfx950's v_ashr_pk_u8_i32
@@ -435,12 +467,16 @@ __device__ __forceinline__ uint2 ld_blockcol(__amdgpu_buffer_rsrc_t blks, bool n
   return make_uint2(v.x, v.y);
 }
 
-__device__ __forceinline__ Coefs load_coefs(__amdgpu_buffer_rsrc_t blks, uint32_t nz, uint32_t blk, int b0, int cb,
+// The MB's blocks start at `blk`: its Y2 block first when kY2Bit is set, then the kept
+// Y / U / V blocks in order (device_format.h).
+__device__ __forceinline__ Coefs load_coefs(__amdgpu_buffer_rsrc_t blks, uint32_t flags, uint32_t blk, int b0, int cb,
                                             int q) {
+  const uint32_t nz = flags & kNzMask;
+  const uint32_t base = blk + ((flags & kY2Bit) ? 1u : 0u);
   Coefs c;
-  c.y0 = ld_blockcol(blks, (nz >> b0) & 1, blk + __builtin_popcount(nz & ((1u << b0) - 1)), q);
-  c.y1 = ld_blockcol(blks, (nz >> (b0 + 8)) & 1, blk + __builtin_popcount(nz & ((1u << (b0 + 8)) - 1)), q);
-  c.c = ld_blockcol(blks, (nz >> cb) & 1, blk + __builtin_popcount(nz & ((1u << cb) - 1)), q);
+  c.y0 = ld_blockcol(blks, (nz >> b0) & 1, base + __builtin_popcount(nz & ((1u << b0) - 1)), q);
+  c.y1 = ld_blockcol(blks, (nz >> (b0 + 8)) & 1, base + __builtin_popcount(nz & ((1u << (b0 + 8)) - 1)), q);
+  c.c = ld_blockcol(blks, (nz >> cb) & 1, base + __builtin_popcount(nz & ((1u << cb) - 1)), q);
   return c;
 }
 
@@ -570,8 +606,9 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int r = (lane & 15) + 16 * s;
-      cc[s] = load_coefs(blks, rc.flags & kNzMask, blk, r >> 2, 16 + (r >> 2), r & 3);
+      cc[s] = load_coefs(blks, rc.flags, blk, r >> 2, 16 + (r >> 2), r & 3);
     }
+    uint2 y2c = ld_blockcol(blks, (rc.flags & kY2Bit) != 0, blk, lane & 3);  // Y2 column (i16 MBs)
     // Retire the prologue loads here (visible to the waitcnt pass: 0x0F70 = vmcnt(0)), so the
     // loop header has no pending loads on cc/rc/rn and the in-loop uses of cc do not
     // conservatively drain the NEXT MB's prefetch with a vmcnt(0).
@@ -616,7 +653,7 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
       // ---- software pipeline: record x+2 in flight during MB x; the coefficients of x+1 are
       //      loaded into cc as soon as the IDCT has consumed x's (below)
       const MbRec rnn = load_rec(recs, mb_w, y, row_ok, x + 2);
-      const uint32_t blk_next = blk + __builtin_popcount(rc.flags & kNzMask);
+      const uint32_t blk_next = blk + __builtin_popcount(rc.flags & (kNzMask | kY2Bit));
 
       K1_SECT(0);
       // ---- wait for the previous quad's last row (t = x + 2y wavefront)
@@ -697,14 +734,16 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
       lds_sync();
 
       K1_SECT(3);
-      // ---- residuals of all blocks (prediction-independent)
+      // ---- residuals of all blocks (prediction-independent); i16 luma DCs from the Y2 WHT
+      int ydc[4] = {0, 0, 0, 0};
+      if (__any((fl & kY2Bit) != 0)) wht_quad(m >> 2, y2c, ydc);  // Y2 of i4 / no-Y2 MBs reads as 0: DCs 0
       int ry0[2][4], ry1[2][4], rcr[2][4];
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
 #ifndef WG_ABL_IDCT
-        idct_pass(q, cc[s].y0, ry0[s]);
-        idct_pass(q, cc[s].y1, ry1[s]);
-        idct_pass(q, cc[s].c, rcr[s]);
+        idct_pass(q, cc[s].y0, ydc[s], ry0[s]);
+        idct_pass(q, cc[s].y1, ydc[s + 2], ry1[s]);
+        idct_pass(q, cc[s].c, 0, rcr[s]);
 #else
         for (int t = 0; t < 4; ++t) ry0[s][t] = ry1[s][t] = rcr[s][t] = (int)(cc[s].y0.x + cc[s].y1.y + cc[s].c.x) >> 20;
 #endif
@@ -717,8 +756,9 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const int r = m + 16 * s;
-        cc[s] = load_coefs(blks, rn.flags & kNzMask, blk_next, r >> 2, 16 + (r >> 2), q);
+        cc[s] = load_coefs(blks, rn.flags, blk_next, r >> 2, 16 + (r >> 2), q);
       }
+      y2c = ld_blockcol(blks, (rn.flags & kY2Bit) != 0, blk_next, q);
       K1_SECT(4);
       // ---- luma prediction + residual (role r: block column (r>>2)&3, pixel rows
       //      4*((r>>2)>>2)+q and that + 8)

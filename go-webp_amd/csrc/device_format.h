@@ -6,9 +6,12 @@
 //                              VP8MBData + VP8FInfo (pkg/vp8/models.go:66-107)
 //   row_block0[mb_h]           index of the first coefficient block of each MB row
 //   blocks[n_nonzero][16]      int16 coefficients of every non-zero 4x4 block in MB
-//                              raster order, blocks 0..15 Y, 16..19 U, 20..23 V,
-//                              stored column-major (blocks[4*c + k] = coeff[4*k + c])
-//                              so lane c of the IDCT reads its column with one load
+//                              raster order: the i16 MB's Y2 block first (kY2Bit; its
+//                              Walsh-Hadamard transform runs on the device), then Y
+//                              0..15 (AC only for i16 MBs: their DC comes from Y2),
+//                              U 16..19, V 20..23; stored column-major
+//                              (blocks[4*c + k] = coeff[4*k + c]) so lane c of the
+//                              IDCT / WHT reads its column with one load
 //   Y/U/V planes               16*mb_w x 16*mb_h and 8*mb_w x 8*mb_h (MB padded)
 //   RGBA                       width x height x 4
 #pragma once
@@ -34,6 +37,7 @@ constexpr uint32_t kNzMask = 0x00ffffffu;  // bit b set: 4x4 block b has coeffic
 constexpr int kI4Shift = 24;                // is_i4x4
 constexpr int kYModeShift = 25;             // i16 mode (B_DC/TM/VE/HE = 0..3)
 constexpr int kUVModeShift = 27;            // chroma mode (0..3)
+constexpr uint32_t kY2Bit = 1u << 29;       // i16 MB with a non-zero Y2 block (stored first)
 
 struct MbRec {
   uint32_t flags;

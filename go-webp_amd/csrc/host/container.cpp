@@ -191,4 +191,21 @@ bool parse_alpha_header(const uint8_t* data, size_t size, int width, int height,
   return true;
 }
 
+int output_bpp(int mode) {
+  switch (mode) {
+    case 0:
+    case 2: return 3;
+    case 5:
+    case 6:
+    case 10: return 2;
+    case 1:
+    case 3:
+    case 4:
+    case 7:
+    case 8:
+    case 9: return 4;
+    default: return 0;
+  }
+}
+
 }  // namespace wg

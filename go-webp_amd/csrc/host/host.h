@@ -24,6 +24,10 @@ struct Container {
   int is_lossless = 0;
 };
 
+// Bytes per pixel of an RGB-family WEBP_CSP_MODE (0..10): 3, 4 or 2; 0 for any other mode
+// (K6, emit.hip, produces exactly these).
+int output_bpp(int mode);
+
 // have_all_data: 1 = DecodeInto's header pass, 0 = WebPGetFeatures' (see container.cpp).
 int parse_container(const uint8_t* data, size_t size, Container* c, wg_features* feat, bool have_all_data = true);
 
@@ -54,22 +58,46 @@ struct PodBuf {
   }
 };
 
-// Parsed lossy frame in the device layout.
-struct SparseFrame {
+// Where the entropy stage writes one lossy frame's device layout (device_format.h): the
+// batch hands out pinned staging memory, tools a SparseFrame's vectors.
+struct SparseSink {
+  MbRec* mbs = nullptr;            // mb_w * mb_h, raster order
+  uint32_t* row_block0 = nullptr;  // mb_h: first coefficient block of each MB row
+  int16_t* blocks = nullptr;       // room for sparse_max_blocks(mb_w, rows) blocks of 16 int16
+};
+// Upper bound on the coefficient blocks of `rows` MB rows: Y2 + 16 Y + 8 chroma per MB.
+inline size_t sparse_max_blocks(int mb_w, int rows) { return (size_t)mb_w * (size_t)rows * 25; }
+// Called once the headers are known: provide a sink for a frame of inf.mb_w x inf.mb_h MBs
+// of which `rows` MB rows are parsed; false = out of memory.
+using SparseAllocFn = bool (*)(void* ctx, const wg_vp8_info& inf, int rows, SparseSink* sink);
+struct SparseResult {
   wg_vp8_info info{};
-  std::vector<MbRec> mbs;              // mb_w * mb_h, raster order
-  std::vector<uint32_t> row_block0;    // first coefficient block of each MB row
-  PodBuf<int16_t> blocks;              // 16 int16 per non-zero 4x4 block, column-major
-  int br_mb_y = 0;                     // MB rows parsed (VP8EnterCritical's br_mb_y_)
-  int fail_row = -1;                   // MB row whose parse failed (-1: none, or the headers)
+  size_t n_blocks = 0;  // blocks written
+  int br_mb_y = 0;      // MB rows parsed (VP8EnterCritical's br_mb_y_)
+  int fail_row = -1;    // MB row whose parse failed (-1: none, or the headers)
 };
 
-// Entropy-decode one lossy frame.  `dense` (mb_w*mb_h) and/or `sparse` may be null.
-// crop_bottom >= 0 bounds the MB rows parsed as WebPDecode does for a crop window
-// (br_mb_y_ = (crop_bottom + 15 + kFilterExtraRows[filter_type]) >> 4, frame_dec.c.go);
-// rows below it are left zero and a corrupt token stream there is not seen.
-int vp8_parse(const uint8_t* data, size_t size, int flags, wg_vp8_info* info,
-              wg_vp8_mb* dense, SparseFrame* sparse, int crop_bottom = -1);
+// Entropy-decode one lossy frame into the device layout.  crop_bottom >= 0 bounds the MB
+// rows parsed as WebPDecode does for a crop window (br_mb_y_ = (crop_bottom + 15 +
+// kFilterExtraRows[filter_type]) >> 4, frame_dec.c.go); rows below it (and below a failing
+// row) read as empty MBs, and a corrupt token stream there is not seen.
+int vp8_parse_sparse(const uint8_t* data, size_t size, int flags, int crop_bottom, SparseAllocFn alloc, void* actx,
+                     SparseResult* res);
+
+// The same into vectors (tools, tests).
+struct SparseFrame {
+  wg_vp8_info info{};
+  std::vector<MbRec> mbs;
+  std::vector<uint32_t> row_block0;
+  PodBuf<int16_t> blocks;  // 16 int16 per kept block
+  int br_mb_y = 0, fail_row = -1;
+};
+int vp8_parse(const uint8_t* data, size_t size, int flags, SparseFrame* sf, int crop_bottom = -1);
+
+// Entropy-decode one lossy frame into libwebp's data model (the CPU checker's input);
+// `dense` (mb_w*mb_h) may be null to parse the headers only.
+int vp8_parse(const uint8_t* data, size_t size, int flags, wg_vp8_info* info, wg_vp8_mb* dense,
+              int crop_bottom = -1);
 
 // VP8L (lossless) after the host entropy stage: the entropy-coded ARGB image and the
 // transforms in bitstream (read) order; the device applies them in reverse.

@@ -418,11 +418,45 @@ int parse_residuals(Decoder* d, MBCtx* mb, MBCtx* left_mb, BoolReader* token_br,
   return !(non_zero_y | non_zero_uv);
 }
 
+// TransformWHT_C (dsp/dec.c.go:142-167) of a column-major Y2 block (the device layout):
+// the 16 Y DC values, raster block order.  The device runs the same transform (K1); the
+// host needs only which outputs are non-zero (NzCodeBits' dc_nz and through it f_inner).
+void transform_wht_colmajor(const int16_t* cm, int16_t* dcs) {
+  int tmp[16];
+  for (int i = 0; i < 4; ++i) {  // column i: in[4r + i] = cm[4i + r]
+    const int16_t* c = cm + 4 * i;
+    const int a0 = c[0] + c[3], a1 = c[1] + c[2], a2 = c[1] - c[2], a3 = c[0] - c[3];
+    tmp[0 + i] = a0 + a1;
+    tmp[8 + i] = a0 - a1;
+    tmp[4 + i] = a3 + a2;
+    tmp[12 + i] = a3 - a2;
+  }
+  for (int i = 0; i < 4; ++i) {
+    const int dc = tmp[0 + i * 4] + 3;
+    const int a0 = dc + tmp[3 + i * 4];
+    const int a1 = tmp[1 + i * 4] + tmp[2 + i * 4];
+    const int a2 = tmp[1 + i * 4] - tmp[2 + i * 4];
+    const int a3 = dc - tmp[3 + i * 4];
+    dcs[4 * i + 0] = (int16_t)((a0 + a1) >> 3);
+    dcs[4 * i + 1] = (int16_t)((a3 + a2) >> 3);
+    dcs[4 * i + 2] = (int16_t)((a0 - a1) >> 3);
+    dcs[4 * i + 3] = (int16_t)((a3 - a2) >> 3);
+  }
+}
+
+inline bool block_nonzero(const int16_t* ob) {
+  uint64_t w[4];
+  std::memcpy(w, ob, 32);
+  return (w[0] | w[1] | w[2] | w[3]) != 0;
+}
+
 // ParseResiduals for the sparse device layout: the same token walk and contexts as
 // parse_residuals, but each 4x4 block is decoded straight into the next free slot of
-// `out` (column-major, kZigzagColMajor) and kept only if some coefficient is non-zero
-// (no 384-coefficient MB buffer, no copy).  Returns the kept-block mask (bit b = block b,
-// blocks 0..15 Y raster, 16..19 U, 20..23 V) and sets *n_kept and block->non_zero_*.
+// `out` (column-major, kZigzagColMajor) and kept only if some coefficient is non-zero.
+// An i16 MB ships its Y2 block itself (first slot, kY2Bit) instead of 16 DC-filled Y
+// blocks: its Y blocks hold only their AC coefficients and the device adds the WHT's DC.
+// Returns the flags' block bits (bit b = block b kept, blocks 0..15 Y raster, 16..19 U,
+// 20..23 V, plus kY2Bit) and sets *n_kept and block->non_zero_*.
 uint32_t parse_residuals_sparse(Decoder* d, MBCtx* mb, MBCtx* left_mb, BoolReader* token_br, MBOut* block,
                                 const BandProbas* const (*bands)[17], int16_t* out, int* n_kept) {
   const int seg = block->segment;
@@ -431,26 +465,20 @@ uint32_t parse_residuals_sparse(Decoder* d, MBCtx* mb, MBCtx* left_mb, BoolReade
   int16_t dcs[16];
   const BandProbas* const* ac_proba;
   int first;
-  auto keep = [&](int16_t* ob, int b) {
-    uint64_t w[4];
-    std::memcpy(w, ob, 32);
-    if (w[0] | w[1] | w[2] | w[3]) {
-      mask |= 1u << b;
-      ++nb;
-    }
-  };
-  if (!block->is_i4x4) {  // parse DC
-    int16_t dc[16] = {0};
+  if (!block->is_i4x4) {  // parse DC (Y2)
+    int16_t* y2 = out;
+    std::memset(y2, 0, 32);
     const int ctx = mb->nz_dc + left_mb->nz_dc;
-    const int nz = get_coeffs_t<false>(token_br, bands[1], ctx, d->dq_y2[seg], 0, dc);
+    const int nz = get_coeffs_t<true>(token_br, bands[1], ctx, d->dq_y2[seg], 0, y2);
     mb->nz_dc = left_mb->nz_dc = (nz > 0);
-    if (nz > 1) {
-      int16_t tmp[256];
-      transform_wht(dc, tmp);
-      for (int i = 0; i < 16; ++i) dcs[i] = tmp[16 * i];
+    if (block_nonzero(y2)) {
+      // nz <= 1: libwebp's shortcut (dc[0] + 3) >> 3 for all 16, which is what the full
+      // transform gives for a DC-only input (vp8_dec.go:620-628)
+      transform_wht_colmajor(y2, dcs);
+      mask |= kY2Bit;
+      nb = 1;
     } else {
-      const int16_t dc0 = (int16_t)((dc[0] + 3) >> 3);
-      for (int i = 0; i < 16; ++i) dcs[i] = dc0;
+      std::memset(dcs, 0, sizeof(dcs));
     }
     first = 1;
     ac_proba = bands[0];
@@ -466,13 +494,15 @@ uint32_t parse_residuals_sparse(Decoder* d, MBCtx* mb, MBCtx* left_mb, BoolReade
     for (int x = 0; x < 4; ++x) {
       int16_t* ob = out + 16 * nb;
       std::memset(ob, 0, 32);
-      ob[0] = dcs[4 * y + x];
       const int ctx = l + (tnz & 1);
       const int nz = get_coeffs_t<true>(token_br, ac_proba, ctx, d->dq_y1[seg], first, ob);
       l = (nz > first);
       tnz = (uint8_t)((tnz >> 1) | (l << 7));
-      nz_coeffs = nz_code_bits(nz_coeffs, nz, ob[0] != 0);
-      keep(ob, 4 * y + x);
+      nz_coeffs = nz_code_bits(nz_coeffs, nz, (first ? dcs[4 * y + x] : ob[0]) != 0);
+      if (block_nonzero(ob)) {
+        mask |= 1u << (4 * y + x);
+        ++nb;
+      }
     }
     tnz >>= 4;
     lnz = (uint8_t)((lnz >> 1) | (l << 7));
@@ -493,7 +523,10 @@ uint32_t parse_residuals_sparse(Decoder* d, MBCtx* mb, MBCtx* left_mb, BoolReade
         l = (nz > 0);
         tnz = (uint8_t)((tnz >> 1) | (l << 3));
         nz_coeffs = nz_code_bits(nz_coeffs, nz, ob[0] != 0);
-        keep(ob, 16 + 2 * ch + 2 * y + x);
+        if (block_nonzero(ob)) {
+          mask |= 1u << (16 + 2 * ch + 2 * y + x);
+          ++nb;
+        }
       }
       tnz >>= 2;
       lnz = (uint8_t)((lnz >> 1) | (l << 5));
@@ -552,57 +585,57 @@ int get_headers(Decoder* d, const uint8_t* buf, size_t buf_size) {  // vp8_dec.g
 
 }  // namespace
 
-int vp8_parse(const uint8_t* data, size_t size, int flags, wg_vp8_info* info, wg_vp8_mb* dense,
-              SparseFrame* sparse, int crop_bottom) {
+namespace {
+
+// VP8GetHeaders + PrecomputeFilterStrengths of a frame: fills *inf and the decoder state.
+int begin_frame(const uint8_t* data, size_t size, int flags, Decoder* d, wg_vp8_info* inf) {
   Container c;
   int st = parse_container(data, size, &c, nullptr);
   if (st != WG_STATUS_OK) return st;
   if (c.is_lossless) return WG_STATUS_UNSUPPORTED_FEATURE;  // VP8L: not this entry point
-  std::unique_ptr<Decoder> dp(new Decoder());
-  Decoder* d = dp.get();
   st = get_headers(d, data + c.payload_off, c.payload_size);
   if (st != WG_STATUS_OK) return st;
   if (flags & WG_FLAG_BYPASS_FILTERING) d->filter_type = 0;  // VP8EnterCritical
   precompute_filter_strengths(d);
-  const int mb_w = d->mb_w, mb_h = d->mb_h;
+  *inf = wg_vp8_info{};
+  inf->width = d->width;
+  inf->height = d->height;
+  inf->mb_w = d->mb_w;
+  inf->mb_h = d->mb_h;
+  inf->filter_type = d->filter_type;
+  inf->num_parts = d->num_parts_minus_one + 1;
+  inf->use_segment = d->use_segment;
+  inf->frame_offset = (int32_t)c.payload_off;
+  return WG_STATUS_OK;
+}
+
+// The MB rows WebPDecode parses for a crop window (VP8EnterCritical's br_mb_y_).
+int parsed_rows(const Decoder* d, int crop_bottom) {
   static const int kFilterExtraRows[3] = {0, 2, 8};  // frame_dec.c.go (VP8EnterCritical)
-  const int br_mb_y =
-      crop_bottom < 0 ? mb_h : std::min(mb_h, (crop_bottom + 15 + kFilterExtraRows[d->filter_type]) >> 4);
-  wg_vp8_info inf{};
-  inf.width = d->width;
-  inf.height = d->height;
-  inf.mb_w = mb_w;
-  inf.mb_h = mb_h;
-  inf.filter_type = d->filter_type;
-  inf.num_parts = d->num_parts_minus_one + 1;
-  inf.use_segment = d->use_segment;
-  inf.frame_offset = (int32_t)c.payload_off;
-  if (info) *info = inf;
-  if (!dense && !sparse) return WG_STATUS_OK;
+  return crop_bottom < 0 ? d->mb_h : std::min(d->mb_h, (crop_bottom + 15 + kFilterExtraRows[d->filter_type]) >> 4);
+}
+
+// ParseFrame (vp8_dec.go:750-774) over rows [0, rows): the libwebp MB model into `dense`,
+// or the device layout into `sink`.  Returns the status and the failing row.
+int parse_rows(Decoder* d, int rows, wg_vp8_mb* dense, const SparseSink* sink, size_t* n_blocks, int* fail_row) {
+  const int mb_w = d->mb_w;
   // bands_ptr (tree_dec.c.go:127-129)
   const BandProbas* bands_ptr[4][17];
   for (int t = 0; t < 4; ++t)
     for (int b = 0; b < 17; ++b) bands_ptr[t][b] = &d->bands[t][kBands[b]];
-
   std::vector<uint8_t> intra_t(4 * (size_t)mb_w, 0);  // B_DC_PRED
   uint8_t intra_l[4];
   std::vector<MBCtx> mb_info((size_t)mb_w + 1);  // [0] = left
   MBCtx* left = &mb_info[0];
-  if (sparse) {
-    sparse->info = inf;
-    sparse->mbs.assign((size_t)mb_w * mb_h, MbRec{0, 0, 0, 0});
-    sparse->row_block0.assign((size_t)mb_h, 0);
-    sparse->blocks.clear();
-  }
   MBOut blk;
   size_t nblocks = 0;
-  st = WG_STATUS_OK;
-  int fail_row = -1;
-  for (int mb_y = 0; mb_y < br_mb_y && st == WG_STATUS_OK; ++mb_y) {
+  int st = WG_STATUS_OK;
+  *fail_row = -1;
+  for (int mb_y = 0; mb_y < rows && st == WG_STATUS_OK; ++mb_y) {
     BoolReader* token_br = &d->parts[mb_y & d->num_parts_minus_one];
     std::memset(intra_l, 0, sizeof(intra_l));  // VP8InitScanline: B_DC_PRED
     left->nz = left->nz_dc = 0;
-    if (sparse) sparse->row_block0[mb_y] = (uint32_t)nblocks;
+    if (sink) sink->row_block0[mb_y] = (uint32_t)nblocks;
     for (int mb_x = 0; mb_x < mb_w; ++mb_x) {
       // Modes come from partition 0.  libwebp parses the whole row of modes first
       // (VP8ParseIntraModeRow); partition 0 is independent of the token partitions,
@@ -616,8 +649,7 @@ int vp8_parse(const uint8_t* data, size_t size, int flags, wg_vp8_info* info, wg
         if (dense) {
           skip = parse_residuals(d, mb, left, token_br, &blk, bands_ptr);
         } else {
-          int16_t* ob = sparse->blocks.reserve_more(24 * 16);
-          mask = parse_residuals_sparse(d, mb, left, token_br, &blk, bands_ptr, ob, &n_kept);
+          mask = parse_residuals_sparse(d, mb, left, token_br, &blk, bands_ptr, sink->blocks + 16 * nblocks, &n_kept);
           skip = !(blk.non_zero_y | blk.non_zero_uv);
         }
       } else {
@@ -634,7 +666,7 @@ int vp8_parse(const uint8_t* data, size_t size, int flags, wg_vp8_info* info, wg
       }
       if (token_br->eof) {
         st = WG_STATUS_NOT_ENOUGH_DATA;  // "Premature end-of-file encountered."
-        fail_row = mb_y;
+        *fail_row = mb_y;
         break;
       }
       const size_t idx = (size_t)mb_y * mb_w + mb_x;
@@ -650,24 +682,9 @@ int vp8_parse(const uint8_t* data, size_t size, int flags, wg_vp8_info* info, wg
         if (blk.is_i4x4) std::memcpy(o.imodes, blk.imodes, 16);
         else { std::memset(o.imodes, 0, 16); o.imodes[0] = blk.imodes[0]; }
         o.f_limit = fi[0]; o.f_ilevel = fi[1]; o.f_inner = fi[2]; o.hev_thresh = fi[3];
-      }
-      if (sparse) {
-        MbRec r{0, 0, 0, 0};
-        if (dense && (blk.non_zero_y | blk.non_zero_uv)) {  // dense + sparse: pack from the MB buffer
-          int16_t* ob = sparse->blocks.reserve_more(24 * 16);
-          for (int b = 0; b < 24; ++b) {
-            const int16_t* cb = blk.coeffs + 16 * b;
-            uint64_t any = 0;
-            for (int k = 0; k < 16; ++k) any |= (uint16_t)cb[k];
-            if (!any) continue;
-            mask |= 1u << b;
-            for (int cc = 0; cc < 4; ++cc)
-              for (int k = 0; k < 4; ++k) ob[16 * n_kept + 4 * cc + k] = cb[4 * k + cc];
-            ++n_kept;
-          }
-        }
-        sparse->blocks.n += 16 * (size_t)n_kept;
+      } else {
         nblocks += n_kept;
+        MbRec r{0, 0, 0, 0};
         r.flags = mask | ((uint32_t)blk.is_i4x4 << kI4Shift) |
                   ((uint32_t)(blk.is_i4x4 ? 0 : blk.imodes[0]) << kYModeShift) |
                   ((uint32_t)blk.uvmode << kUVModeShift);
@@ -676,18 +693,71 @@ int vp8_parse(const uint8_t* data, size_t size, int flags, wg_vp8_info* info, wg
           for (int n = 0; n < 8; ++n) r.imodes_hi |= (uint32_t)blk.imodes[8 + n] << (4 * n);
         }
         r.finfo = fi[0] | (fi[1] << 8) | (fi[2] << 16) | ((uint32_t)fi[3] << 24);
-        sparse->mbs[idx] = r;
+        sink->mbs[idx] = r;
       }
     }
     if (st == WG_STATUS_OK && d->br.eof) {  // partition 0 exhausted
       st = WG_STATUS_NOT_ENOUGH_DATA;
-      fail_row = mb_y;
+      *fail_row = mb_y;
     }
   }
-  if (sparse) {
-    sparse->br_mb_y = br_mb_y;
-    sparse->fail_row = fail_row;
-  }
+  *n_blocks = nblocks;
+  return st;
+}
+
+}  // namespace
+
+int vp8_parse(const uint8_t* data, size_t size, int flags, wg_vp8_info* info, wg_vp8_mb* dense, int crop_bottom) {
+  std::unique_ptr<Decoder> dp(new Decoder());
+  wg_vp8_info inf;
+  int st = begin_frame(data, size, flags, dp.get(), &inf);
+  if (st != WG_STATUS_OK) return st;
+  if (info) *info = inf;
+  if (!dense) return WG_STATUS_OK;
+  size_t nb = 0;
+  int fail_row = -1;
+  return parse_rows(dp.get(), parsed_rows(dp.get(), crop_bottom), dense, nullptr, &nb, &fail_row);
+}
+
+int vp8_parse_sparse(const uint8_t* data, size_t size, int flags, int crop_bottom, SparseAllocFn alloc, void* actx,
+                     SparseResult* res) {
+  std::unique_ptr<Decoder> dp(new Decoder());
+  Decoder* d = dp.get();
+  res->n_blocks = 0;
+  res->fail_row = -1;
+  res->br_mb_y = 0;
+  int st = begin_frame(data, size, flags, d, &res->info);
+  if (st != WG_STATUS_OK) return st;
+  const int rows = parsed_rows(d, crop_bottom);
+  res->br_mb_y = rows;
+  SparseSink sink{};
+  if (!alloc(actx, res->info, rows, &sink)) return WG_STATUS_OUT_OF_MEMORY;
+  st = parse_rows(d, rows, nullptr, &sink, &res->n_blocks, &res->fail_row);
+  // rows not parsed (below a crop window's br_mb_y, or after a failure) read as empty
+  const int done = st == WG_STATUS_OK ? rows : std::max(res->fail_row, 0);
+  const size_t mb_w = (size_t)d->mb_w;
+  std::memset(sink.mbs + (size_t)done * mb_w, 0, ((size_t)d->mb_h - done) * mb_w * sizeof(MbRec));
+  for (int y = done; y < d->mb_h; ++y) sink.row_block0[y] = (uint32_t)res->n_blocks;
+  return st;
+}
+
+int vp8_parse(const uint8_t* data, size_t size, int flags, SparseFrame* sf, int crop_bottom) {
+  auto alloc = [](void* p, const wg_vp8_info& inf, int rows, SparseSink* sink) {
+    SparseFrame* f = static_cast<SparseFrame*>(p);
+    f->mbs.resize((size_t)inf.mb_w * inf.mb_h);
+    f->row_block0.resize((size_t)inf.mb_h);
+    f->blocks.clear();
+    sink->mbs = f->mbs.data();
+    sink->row_block0 = f->row_block0.data();
+    sink->blocks = f->blocks.reserve_more(16 * sparse_max_blocks(inf.mb_w, rows));
+    return true;
+  };
+  SparseResult r;
+  const int st = vp8_parse_sparse(data, size, flags, crop_bottom, alloc, sf, &r);
+  sf->info = r.info;
+  sf->blocks.n = 16 * r.n_blocks;
+  sf->br_mb_y = r.br_mb_y;
+  sf->fail_row = r.fail_row;
   return st;
 }
 

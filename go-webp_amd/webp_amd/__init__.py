@@ -19,7 +19,7 @@ import numpy as np
 __all__ = [
     "Status", "WebPError", "FLAG_BYPASS_FILTERING", "FLAG_NO_FANCY_UPSAMPLING", "Features",
     "lib", "features", "decode_config", "decode", "Context", "Batch", "vp8_parse", "vp8l_parse", "MB_DTYPE",
-    "VP8Info", "VP8LInfo", "device_count", "yuv420_to_rgba_device",
+    "VP8Info", "VP8LInfo", "device_count", "yuv420_to_rgba_device", "MultiContext", "set_default_device",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -156,6 +156,8 @@ _SIGS = {
     "wg_batch_frame_status": (C.c_int, [_P, C.c_int]),
     "wg_anim_decode": (C.c_int, [_P, _P, C.c_size_t, _P, _P, C.c_int32]),
     "wg_decode_status": (C.c_int, [_P, C.c_size_t, _P]),
+    "wg_set_default_device": (C.c_int, [C.c_int]),
+    "wg_decode_rgba_batch_multi": (C.c_int, [_P, C.c_int, _P, _P, C.c_int, _P, _P, _P, C.c_int32]),
 }
 EXPORTED = tuple(_SIGS)
 
@@ -184,6 +186,8 @@ def lib():
             raise ImportError(f"{LIB_PATH} not built: run `make -C go-webp_amd/csrc` or __graft_entry__.build()")
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in _SIGS.items():
+            if os.environ.get("WG_LIB_VARIANT") and not hasattr(L, name):
+                continue  # measurement variants built from older sources (A/B runs)
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
@@ -199,6 +203,13 @@ def _buf(data):
 
 def device_count():
     return lib().wg_device_count()
+
+
+def set_default_device(device):
+    """Device of the context behind decode() / decode_into() (wg_set_default_device)."""
+    st = lib().wg_set_default_device(device)
+    if st != Status.OK:
+        raise WebPError(st, f"wg_set_default_device({device})")
 
 
 def features(data):
@@ -477,21 +488,7 @@ class Context:
         `out`: optional preallocated (H, W, 4) uint8 arrays, one per input."""
         bufs, ptrs, sizes = _ptr_arrays(datas)
         n = len(bufs)
-        outs, optr, strides = [], (C.c_void_p * n)(), (C.c_int32 * n)()
-        for i, b in enumerate(bufs):
-            if out is not None:
-                a = out[i]
-                if a.dtype != np.uint8 or a.ndim != 3 or a.shape[2] != 4 or not a.flags.c_contiguous:
-                    raise ValueError("out arrays must be C-contiguous (H, W, 4) uint8")
-            else:
-                try:
-                    f = features(b)
-                    a = np.empty((f.height, f.width, 4), np.uint8)
-                except WebPError:
-                    a = np.empty((1, 1, 4), np.uint8)
-            outs.append(a)
-            optr[i] = a.ctypes.data
-            strides[i] = a.shape[1] * 4
+        outs, optr, strides = _rgba_outs(bufs, out)
         status = np.zeros(n, np.int32)
         st = lib().wg_decode_rgba_batch(self._h, ptrs, sizes, n, optr, strides, status.ctypes.data, flags)
         if st != Status.OK:
@@ -510,6 +507,52 @@ class Context:
             self.close()
         except Exception:
             pass
+
+
+def _rgba_outs(bufs, out):
+    n = len(bufs)
+    outs, optr, strides = [], (C.c_void_p * n)(), (C.c_int32 * n)()
+    for i, b in enumerate(bufs):
+        if out is not None:
+            a = out[i]
+            if a.dtype != np.uint8 or a.ndim != 3 or a.shape[2] != 4 or not a.flags.c_contiguous:
+                raise ValueError("out arrays must be C-contiguous (H, W, 4) uint8")
+        else:
+            try:
+                f = features(b)
+                a = np.empty((f.height, f.width, 4), np.uint8)
+            except WebPError:
+                a = np.empty((1, 1, 4), np.uint8)
+        outs.append(a)
+        optr[i] = a.ctypes.data
+        strides[i] = a.shape[1] * 4
+    return outs, optr, strides
+
+
+class MultiContext:
+    """Frames sharded over several decode contexts: one Context per entry of
+    `devices` (a device may repeat: independent contexts on one GPU), decode_batch() splits the
+    list into contiguous shards decoded concurrently (wg_decode_rgba_batch_multi)."""
+
+    def __init__(self, devices, host_threads=0):
+        self.contexts = [Context(d, host_threads) for d in devices]
+
+    def decode_batch(self, datas, flags=0, out=None):
+        """Same contract as Context.decode_batch: (list of RGBA arrays or None, status)."""
+        bufs, ptrs, sizes = _ptr_arrays(datas)
+        n = len(bufs)
+        outs, optr, strides = _rgba_outs(bufs, out)
+        status = np.zeros(n, np.int32)
+        hs = (C.c_void_p * len(self.contexts))(*[c._h for c in self.contexts])
+        st = lib().wg_decode_rgba_batch_multi(hs, len(self.contexts), ptrs, sizes, n, optr, strides,
+                                              status.ctypes.data, flags)
+        if st != Status.OK:
+            raise WebPError(st, "wg_decode_rgba_batch_multi")
+        return [o if s == Status.OK else None for o, s in zip(outs, status)], status
+
+    def close(self):
+        for c in self.contexts:
+            c.close()
 
 
 def yuv420_to_rgba_device(y_ptr, u_ptr, v_ptr, y_stride, uv_stride, rgba_ptr, rgba_stride, width, height,

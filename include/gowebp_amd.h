@@ -72,6 +72,12 @@ int wg_get_features(const uint8_t* data, size_t size, wg_features* out);
 int wg_decode_rgba_into(const uint8_t* data, size_t size, uint8_t* rgba, size_t cap,
                         int stride, int flags);
 
+/* The HIP device of the context behind the single-frame entry points (wg_decode_rgba_into,
+ * wg_decode_into): 0 by default.  Replaces that context if it exists on another device (no
+ * call may be in flight).  INVALID_PARAM for a device that does not exist.  No libwebp
+ * counterpart (libwebp has no devices). */
+int wg_set_default_device(int device);
+
 /* ---- output options (WebPDecoderConfig subset, pkg/libwebp/webp/decode.go:59-83) --------- */
 /* colorspace = WEBP_CSP_MODE of the RGB family: 0 RGB, 1 RGBA, 2 BGR, 3 BGRA, 4 ARGB,
  * 5 RGBA_4444, 6 RGB_565, 7 rgbA, 8 bgrA, 9 Argb, 10 rgbA_4444 (lower case = premultiplied);
@@ -107,7 +113,10 @@ int wg_decode_into(const uint8_t* data, size_t size, const wg_decoder_options* o
 typedef struct wg_ctx wg_ctx;
 
 /* Create a decode context bound to HIP device `device` (host threads for the entropy
- * stage = `host_threads`, 0 = hardware concurrency).  NULL on failure. */
+ * stage = `host_threads`, 0 = hardware concurrency).  NULL on failure.  The context keeps a
+ * worker pool, pinned staging memory and device buffers of finished batches for reuse by
+ * later batches; all are released by wg_ctx_destroy.  Batches of one context are created one
+ * at a time (internal lock); contexts are independent (synchronisation is per stream). */
 wg_ctx* wg_ctx_create(int device, int host_threads);
 void wg_ctx_destroy(wg_ctx* ctx);
 
@@ -117,6 +126,15 @@ void wg_ctx_destroy(wg_ctx* ctx);
 int wg_decode_rgba_batch(wg_ctx* ctx, const uint8_t* const* data, const size_t* sizes, int n,
                          uint8_t* const* rgba, const int32_t* strides, int32_t* status,
                          int32_t flags);
+
+/* Multi-GPU batch: the n frames are split into n_ctx contiguous shards, shard k
+ * decoded by wg_decode_rgba_batch on ctxs[k] (normally one context per device), all shards
+ * concurrently from their own host threads.  Frames are independent: nothing is exchanged
+ * between devices, and every frame's output and status are those of a single-context decode.
+ * Returns OK if every shard ran (check status[]), else the first failing shard's code. */
+int wg_decode_rgba_batch_multi(wg_ctx* const* ctxs, int n_ctx, const uint8_t* const* data,
+                               const size_t* sizes, int n, uint8_t* const* rgba,
+                               const int32_t* strides, int32_t* status, int32_t flags);
 
 /* As wg_decode_rgba_batch with full output options (colorspace, cropping, flip). */
 int wg_decode_batch(wg_ctx* ctx, const uint8_t* const* data, const size_t* sizes, int n,

@@ -10,6 +10,7 @@
 #include <iterator>
 #include <random>
 #include <vector>
+#include "batch.h"
 #include "host.h"
 int main(int argc, char** argv) {
   std::mt19937 rng(1234);
@@ -35,21 +36,42 @@ int main(int argc, char** argv) {
           for (const auto& fr : af)
             if (fr.off > d.size() || fr.size > d.size() - fr.off) { printf("frame out of range\n"); return 1; }
       }
+      {
+        wg::StagingArena arena([](size_t b) { return std::malloc(b); }, [](void* q) { std::free(q); }, 1 << 20);
+        wg::StagingArena::Cursor cur;
+        wg::FrameParse fp;
+        wg_decoder_options opt{};
+        opt.colorspace = 1;
+        if (it % 5 == 2) {  // a crop window, sometimes invalid
+          opt.use_cropping = 1;
+          opt.crop_left = (int)(rng() % 40) - 4;
+          opt.crop_top = (int)(rng() % 40) - 4;
+          opt.crop_width = (int)(rng() % 80);
+          opt.crop_height = (int)(rng() % 80);
+        }
+        wg::parse_one(d.data(), d.size(), opt, &arena, &cur, &fp);
+        arena.release(&cur);
+      }
       if (wg::parse_container(d.data(), d.size(), &c, &ft) != 0) { ++runs; continue; }
       if (c.is_lossless) {
         wg::VP8LFrame lf;
         wg::vp8l_parse(d.data() + c.payload_off, c.payload_size, &lf);
       } else {
-        wg_vp8_info info; wg::SparseFrame sf;
+        wg::SparseFrame sf;
         // every third run bounded to a random crop bottom (the WebPDecode crop path)
         const int crop_bottom = it % 3 == 1 ? (int)(rng() % 64) : -1;
-        int st = wg::vp8_parse(d.data(), d.size(), 0, &info, nullptr, &sf, crop_bottom);
+        int st = wg::vp8_parse(d.data(), d.size(), 0, &sf, crop_bottom);
+        const wg_vp8_info& info = sf.info;
         if (st == 0) {
           // device-side invariants the kernels rely on
           size_t nmb = (size_t)info.mb_w * info.mb_h;
           if (sf.mbs.size() != nmb || sf.row_block0.size() != (size_t)info.mb_h) { printf("bad sizes\n"); return 1; }
           size_t tot = 0;
-          for (size_t m = 0; m < nmb; ++m) tot += __builtin_popcount(sf.mbs[m].flags & wg::kNzMask);
+          for (int y = 0; y < info.mb_h; ++y) {
+            if (sf.row_block0[(size_t)y] != tot) { printf("row index mismatch\n"); return 1; }
+            for (int x = 0; x < info.mb_w; ++x)
+              tot += __builtin_popcount(sf.mbs[(size_t)y * info.mb_w + x].flags & (wg::kNzMask | wg::kY2Bit));
+          }
           if (tot * 16 != sf.blocks.size()) { printf("block count mismatch\n"); return 1; }
         }
         if (c.alpha_size) {

@@ -64,3 +64,42 @@ def test_single_process_reduce_is_identity():
     sys.path.insert(0, ROOT)
     import bench
     assert bench.reduce_job(None, "cpu", 1.5, 123) == (1.5, 123)
+
+
+def _run_bench(args, env_extra=None, timeout=240):
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra or {})
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                       env=env, timeout=timeout)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout  # only rank 0 prints
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_bench_spawns_one_rank_per_gpu(n):
+    """`bench.py --gpus N` with no launcher starts N rank processes itself (the 1->8 GPU
+    curve, C4): one JSON line from rank 0 with n_gpus == N, every rank on its own
+    LOCAL_RANK (= device), whole-job pixels summed over the ranks.  --mock replaces the
+    device decode by a sleep, so this runs on CPU; the barrier and reduction are the real
+    gloo ones."""
+    out = _run_bench(["--gpus", str(n), "--mock", "--steps", "3", "--warmup", "1"])
+    assert out["n_gpus"] == n and out["mock"] is True
+    ranks = out["ranks"]
+    assert sorted(r["rank"] for r in ranks) == list(range(n))
+    assert sorted(r["local_rank"] for r in ranks) == list(range(n))
+    assert len({r["pid"] for r in ranks}) == n  # separate processes
+    assert out["value"] > 0 and out["scaling"] == "weak"
+    # every rank decoded 4 mock frames of 1000 px per step: value = n * 4000 * steps / max time
+    assert out["value"] == pytest.approx(n * 4000 * 3 / (out["ms_per_step"] * 3 * 1e-3) / 1e6, rel=0.01)
+
+
+def test_bench_under_external_launcher_env():
+    """Under torch.distributed.run the launcher's WORLD_SIZE / RANK / LOCAL_RANK are used and
+    nothing is spawned: a single process with WORLD_SIZE=1 reports n_gpus == 1."""
+    out = _run_bench(["--mock", "--steps", "2", "--warmup", "1"], {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert out["n_gpus"] == 1 and len(out["ranks"]) == 1
