@@ -40,7 +40,9 @@ WORKLOADS = {
     "c5": dict(prefix="c5_ll2048", name="c5_ll2048_x256",
                desc="2048x2048 VP8L lossless (predictor + cross-color + subtract-green + color cache), batch 256"),
 }
-KERNELS = ("vp8_recon_filter_kernel", "yuv_to_rgba_kernel", "vp8l_transforms_kernel", "alpha_kernel")
+# the order of Batch.kernel_ms() / kernel_bytes(): K1, K2, K3, K4, K7, K0
+KERNELS = ("vp8_recon_filter_kernel", "yuv_to_rgba_kernel", "vp8l_transforms_kernel", "alpha_kernel",
+           "vp8l_resolve_kernel", "vp8_y2_kernel")
 
 
 def _load_frames(prefix):
@@ -130,8 +132,8 @@ def _cpu_decode_one(d):
     import webp_amd
     from oracle_lib import oracle_decode, oracle_vp8l_decode
     if webp_amd.features(d).format == 2:
-        info, argb, tdata = webp_amd.vp8l_parse(d)
-        oracle_vp8l_decode(info, argb, tdata)
+        info, coded, tdata = webp_amd.vp8l_parse(d)
+        oracle_vp8l_decode(info, coded, tdata)
     else:
         info, mbs = webp_amd.vp8_parse(d)
         oracle_decode(info, mbs)
@@ -226,10 +228,10 @@ class _MockBatch:
         time.sleep(0.002)
 
     def kernel_ms(self):
-        return (0.0, 0.0, 0.0, 0.0)
+        return (0.0,) * len(KERNELS)
 
     def kernel_bytes(self):
-        return (0.0, 0.0, 0.0, 0.0)
+        return (0.0,) * len(KERNELS)
 
     def close(self):
         pass

@@ -140,9 +140,14 @@ namespace {
 constexpr size_t kAlign = 256;
 inline size_t align_up(size_t v) { return (v + kAlign - 1) & ~(kAlign - 1); }
 
+// Kernels in launch order (stage) and in the public order of wg_batch_kernel_ms (K1, K2, K3,
+// K4, K7, K0): stage s runs between events ev[s] and ev[s + 1].
+constexpr int kStages = 6;
+constexpr int kStageK0 = 0, kStageK1 = 1, kStageK2 = 2, kStageK7 = 3, kStageK3 = 4, kStageK4 = 5;
+constexpr int kPublicOfStage[kStages] = {5, 0, 1, 4, 2, 3};
 struct Timing {
-  hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
-  bool ran[4] = {false, false, false, false};  // K1, K2, K3, K4 launched in this run
+  hipEvent_t ev[kStages + 1] = {};
+  bool ran[kStages] = {};
 };
 
 }  // namespace
@@ -154,6 +159,8 @@ struct wg_batch {
   std::vector<FrameParse> fp;
   std::vector<FrameDesc> desc;
   std::vector<LLDesc> lldesc;     // lossless frames and lossless alpha streams (K3)
+  std::vector<wg::LLTokDesc> tokdesc;  // the same streams' tokens (K7)
+  wg::LLTokDesc* d_tokdesc = nullptr;
   std::vector<AlphaDesc> adesc;   // alpha planes (K4)
   FrameDesc* d_desc = nullptr;
   LLDesc* d_lldesc = nullptr;
@@ -175,7 +182,8 @@ struct wg_batch {
   int n_wide = 0;                          // lossy frames wider than that (global column store)
   int n_valid = 0;
   int64_t pixels = 0;
-  double kbytes[4] = {0, 0, 0, 0};
+  double kbytes[kStages] = {};  // public order: K1, K2, K3, K4, K7, K0
+  int max_mb_h = 1;
   double k1_fused_bytes = 0;  // K1 with its RGBA tail: inputs + RGBA (planes are an intermediate)
   std::vector<Timing> timings;  // one per run since the last query
   size_t n_runs_pending = 0;
@@ -195,7 +203,8 @@ wg_ctx* default_ctx() {
   return g_default_ctx;
 }
 
-void fill_vp8l_info(const wg::VP8LFrame& f, wg_vp8l_info* info, uint32_t* argb, uint32_t* const* transform_data);
+void fill_vp8l_info(const wg::VP8LFrame& f, wg_vp8l_info* info, uint32_t* tokens, uint32_t* literals,
+                    uint32_t* const* transform_data);
 
 // Errors never cross the C ABI as exceptions.
 template <class F>
@@ -246,7 +255,7 @@ int wg_decode_status(const uint8_t* data, size_t size, const wg_decoder_options*
   });
 }
 
-int wg_vp8l_parse(const uint8_t* data, size_t size, wg_vp8l_info* info, uint32_t* argb,
+int wg_vp8l_parse(const uint8_t* data, size_t size, wg_vp8l_info* info, uint32_t* tokens, uint32_t* literals,
                   uint32_t* const* transform_data) {
   if (data == nullptr || info == nullptr) return WG_STATUS_INVALID_PARAM;
   wg::Container c;
@@ -258,13 +267,13 @@ int wg_vp8l_parse(const uint8_t* data, size_t size, wg_vp8l_info* info, uint32_t
     wg::VP8LFrame f;
     const int st2 = wg::vp8l_parse(data + c.payload_off, c.payload_size, &f);
     if (st2 != WG_STATUS_OK) return st2;
-    fill_vp8l_info(f, info, argb, transform_data);
+    fill_vp8l_info(f, info, tokens, literals, transform_data);
     return (int)WG_STATUS_OK;
   });
 }
 
 int wg_alpha_parse(const uint8_t* data, size_t size, wg_alpha_info* info, uint8_t* filtered,
-                   wg_vp8l_info* ll_info, uint32_t* argb, uint32_t* const* transform_data) {
+                   wg_vp8l_info* ll_info, uint32_t* tokens, uint32_t* literals, uint32_t* const* transform_data) {
   if (data == nullptr) return WG_STATUS_INVALID_PARAM;
   wg::Container c;
   wg_features feat{};
@@ -292,7 +301,7 @@ int wg_alpha_parse(const uint8_t* data, size_t size, wg_alpha_info* info, uint8_
     wg::VP8LFrame f;
     const int st2 = wg::vp8l_parse_alpha(ad + 1, c.alpha_size - 1, c.width, c.height, &f);
     if (st2 != WG_STATUS_OK) return st2;
-    if (ll_info) fill_vp8l_info(f, ll_info, argb, transform_data);
+    if (ll_info) fill_vp8l_info(f, ll_info, tokens, literals, transform_data);
     return (int)WG_STATUS_OK;
   });
 }
@@ -300,13 +309,16 @@ int wg_alpha_parse(const uint8_t* data, size_t size, wg_alpha_info* info, uint8_
 }  // extern "C"
 
 namespace {
-void fill_vp8l_info(const wg::VP8LFrame& f, wg_vp8l_info* info, uint32_t* argb, uint32_t* const* transform_data) {
+void fill_vp8l_info(const wg::VP8LFrame& f, wg_vp8l_info* info, uint32_t* tokens, uint32_t* literals,
+                    uint32_t* const* transform_data) {
   std::memset(info, 0, sizeof(*info));
   info->width = f.width;
   info->height = f.height;
   info->has_alpha = f.has_alpha;
   info->coded_width = f.coded_width;
   info->num_transforms = (int32_t)f.transforms.size();
+  info->cache_bits = f.cache_bits;
+  info->num_literals = (int32_t)f.lits.size();
   for (size_t i = 0; i < f.transforms.size(); ++i) {
     info->transform_type[i] = f.transforms[i].type;
     info->transform_bits[i] = f.transforms[i].bits;
@@ -315,7 +327,8 @@ void fill_vp8l_info(const wg::VP8LFrame& f, wg_vp8l_info* info, uint32_t* argb, 
     if (transform_data && transform_data[i] && !f.transforms[i].data.empty())
       std::memcpy(transform_data[i], f.transforms[i].data.data(), f.transforms[i].data.size() * 4);
   }
-  if (argb) std::memcpy(argb, f.argb.data(), f.argb.size() * 4);
+  if (tokens) std::memcpy(tokens, f.tokens.data(), f.tokens.size() * 4);
+  if (literals && !f.lits.empty()) std::memcpy(literals, f.lits.data(), f.lits.size() * 4);
 }
 }  // namespace
 
@@ -400,6 +413,7 @@ void wg_batch_destroy(wg_batch* b) {
   DeviceCache& c = b->ctx->cache;
   c.put(b->d_desc);
   c.put(b->d_lldesc);
+  c.put(b->d_tokdesc);
   c.put(b->d_adesc);
   c.put(b->d_desc2);
   c.put(b->d_err);
@@ -442,12 +456,13 @@ struct BatchDeleter {
 };
 
 // The LLDesc of one lossless stream (transforms in application order = reverse of read
-// order); `d_in` + the arena's device offsets locate its staged coded image and data.
-LLDesc make_ll(const wg::LLMeta& m, const wg::StagingArena& arena, uint8_t* d_in, uint8_t* scratch, uint8_t* rgba,
-               int stride) {
+// order): its coded image is K7's output in the plane buffer; `d_in` + the arena's device
+// offsets locate its staged transform data.
+LLDesc make_ll(const wg::LLMeta& m, const wg::StagingArena& arena, uint8_t* d_in, uint8_t* d_planes, uint8_t* scratch,
+               uint8_t* rgba, int stride) {
   LLDesc l{};
-  l.coded = reinterpret_cast<const uint32_t*>(d_in + arena.dev_offset(m.coded));
-  l.coded_bytes = (int32_t)m.coded.bytes;
+  l.coded = reinterpret_cast<const uint32_t*>(d_planes + m.off_coded);
+  l.coded_bytes = (int32_t)(m.n_px() * 4);
   l.scratch = m.two_pass() ? reinterpret_cast<uint32_t*>(scratch) : nullptr;
   l.scratch_bytes = l.scratch ? m.width * m.height * 4 : 0;
   l.rgba = rgba;
@@ -476,10 +491,24 @@ LLDesc make_ll(const wg::LLMeta& m, const wg::StagingArena& arena, uint8_t* d_in
   return l;
 }
 
-// algorithmic bytes of one lossless stream on K3: reads + RGBA write
+wg::LLTokDesc make_tok(const wg::LLMeta& m, const wg::StagingArena& arena, uint8_t* d_in, uint8_t* d_planes) {
+  wg::LLTokDesc t{};
+  t.tokens = reinterpret_cast<const uint32_t*>(d_in + arena.dev_offset(m.tokens));
+  t.lits = reinterpret_cast<const uint32_t*>(d_in + arena.dev_offset(m.lits));
+  t.coded = reinterpret_cast<uint32_t*>(d_planes + m.off_coded);
+  t.n_px = (int32_t)m.n_px();
+  t.n_lits = (int32_t)(m.lits.bytes / 4);
+  t.cache_bits = m.cache_bits;
+  t.valid = 1;
+  return t;
+}
+
+// algorithmic bytes of one lossless stream: K7 reads tokens + literals and writes
+// the coded image; K3 reads it and the transform data and writes RGBA (two passes: + scratch)
+double k7_bytes(const wg::LLMeta& m) { return (double)m.tokens.bytes + (double)m.lits.bytes + 4.0 * m.n_px(); }
 double ll_bytes(const wg::LLMeta& m) {
   const double px = (double)m.width * m.height;
-  double bytes = (double)m.coded.bytes + 4.0 * px;
+  double bytes = 4.0 * m.n_px() + 4.0 * px;
   for (int t = 0; t < m.n_transforms; ++t) bytes += (double)m.tdata[t].bytes;
   if (m.two_pass()) bytes += 8.0 * px;
   return bytes;
@@ -506,7 +535,7 @@ wg_batch* batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t* si
   b->in_bytes = std::max<size_t>(arena.layout(), kAlign);
   // layout of the planes / RGBA, and the algorithmic bytes per kernel
   size_t pl_b = 0, rg_b = 0;
-  double k1 = 0, k2 = 0, k3 = 0, k4 = 0;
+  double k0 = 0, k1 = 0, k2 = 0, k3 = 0, k4 = 0, k7 = 0;
   for (int i = 0; i < n; ++i) {
     FrameParse& f = b->fp[(size_t)i];
     if (status) status[i] = f.status;
@@ -527,12 +556,18 @@ wg_batch* batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t* si
         f.off_scratch = pl_b;
         pl_b = align_up(pl_b + (size_t)f.width * f.height * 4);
       }
+      f.ll.off_coded = pl_b;
+      pl_b = align_up(pl_b + f.ll.n_px() * 4);
       k3 += ll_bytes(f.ll);
+      k7 += k7_bytes(f.ll);
       continue;
     }
     b->n_lossy++;
     const wg_vp8_info& inf = f.info;
     const size_t nmb = (size_t)inf.mb_w * inf.mb_h;
+    b->max_mb_h = std::max(b->max_mb_h, inf.mb_h);
+    f.off_dcs = pl_b;  // K0's output: 16 int16 per MB
+    pl_b = align_up(pl_b + nmb * 32);
     f.off_y = pl_b;
     pl_b = align_up(pl_b + nmb * 256);
     f.off_u = pl_b;
@@ -561,6 +596,7 @@ wg_batch* batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t* si
     // algorithmic bytes: K1 reads records + row index + coefficient blocks, writes
     // MB-padded planes (or, with its RGBA tail, the RGBA); K2 reads cropped planes, writes RGBA.
     const double k1_in = (double)nmb * sizeof(MbRec) + inf.mb_h * 4.0 + (double)f.n_blocks * 32.0;
+    k0 += (double)nmb * sizeof(MbRec) + inf.mb_h * 4.0 + 64.0 * (double)f.n_y2;  // records, Y2 in, DCs out
     k1 += k1_in + nmb * 384.0;
     b->k1_fused_bytes += k1_in + 4.0 * inf.width * (double)inf.height;
     const double opx = (double)f.out_w * f.out_h;
@@ -575,7 +611,10 @@ wg_batch* batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t* si
           f.off_ascratch = pl_b;
           pl_b = align_up(pl_b + (size_t)f.width * f.height * 4);
         }
+        f.al.off_coded = pl_b;
+        pl_b = align_up(pl_b + f.al.n_px() * 4);
         k3 += ll_bytes(f.al);
+        k7 += k7_bytes(f.al);
         f.off_argba = pl_b;
         pl_b = align_up(pl_b + (size_t)f.width * f.height * 4);
         k4 += 4.0 * px;
@@ -587,10 +626,12 @@ wg_batch* batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t* si
       k4 += 8.0 * px;
     }
   }
-  b->kbytes[3] = k4;
-  b->kbytes[2] = k3;
   b->kbytes[0] = k1;
   b->kbytes[1] = k2;
+  b->kbytes[2] = k3;
+  b->kbytes[3] = k4;
+  b->kbytes[4] = k7;
+  b->kbytes[5] = k0;
   b->plane_bytes = std::max<size_t>(pl_b, kAlign);
   b->rgba_bytes = std::max<size_t>(rg_b, kAlign);
   auto fail = [&](int st) {
@@ -605,9 +646,10 @@ wg_batch* batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t* si
   b->d_rgba = static_cast<uint8_t*>(cache.get(b->rgba_bytes));
   b->d_desc = static_cast<FrameDesc*>(cache.get(sizeof(FrameDesc) * (size_t)n));
   b->d_lldesc = static_cast<LLDesc*>(cache.get(sizeof(LLDesc) * (size_t)std::max(b->n_k3, 1)));
+  b->d_tokdesc = static_cast<wg::LLTokDesc*>(cache.get(sizeof(wg::LLTokDesc) * (size_t)std::max(b->n_k3, 1)));
   b->d_adesc = static_cast<AlphaDesc*>(cache.get(sizeof(AlphaDesc) * (size_t)std::max(b->n_alpha, 1)));
   b->d_err = static_cast<int*>(cache.get(sizeof(int)));
-  if (!b->d_in || !b->d_planes || !b->d_rgba || !b->d_desc || !b->d_lldesc || !b->d_adesc || !b->d_err ||
+  if (!b->d_in || !b->d_planes || !b->d_rgba || !b->d_desc || !b->d_lldesc || !b->d_tokdesc || !b->d_adesc || !b->d_err ||
       hipMemsetAsync(b->d_err, 0, sizeof(int), ctx->stream) != hipSuccess)
     return fail(WG_STATUS_OUT_OF_MEMORY);
   b->desc.assign((size_t)n, FrameDesc{});
@@ -620,7 +662,8 @@ wg_batch* batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t* si
     d.height = f.height;
     d.rgba_stride = 4 * f.rgba_w;
     if (f.lossless) {  // K1/K2 skip it (valid = 0); K3 gets an LLDesc
-      b->lldesc.push_back(make_ll(f.ll, arena, b->d_in, b->d_planes + f.off_scratch, d.rgba, d.rgba_stride));
+      b->lldesc.push_back(make_ll(f.ll, arena, b->d_in, b->d_planes, b->d_planes + f.off_scratch, d.rgba, d.rgba_stride));
+      b->tokdesc.push_back(make_tok(f.ll, arena, b->d_in, b->d_planes));
       continue;
     }
     const wg_vp8_info& inf = f.info;
@@ -629,6 +672,7 @@ wg_batch* batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t* si
     d.row_block0 = reinterpret_cast<const uint32_t*>(in + f.off_rows);
     d.blocks = reinterpret_cast<const int16_t*>(in + f.off_blocks);
     d.blocks_bytes = (int32_t)(f.n_blocks * 32);
+    d.dcs = reinterpret_cast<int16_t*>(b->d_planes + f.off_dcs);
     d.y = b->d_planes + f.off_y;
     d.cols = f.wide ? b->d_planes + f.off_cols : nullptr;
     d.u = b->d_planes + f.off_u;
@@ -643,8 +687,9 @@ wg_batch* batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t* si
     if (f.alpha) {
       AlphaDesc a{};
       if (f.ah.method == 1) {
-        b->lldesc.push_back(make_ll(f.al, arena, b->d_in, b->d_planes + f.off_ascratch, b->d_planes + f.off_argba,
-                                    4 * f.width));
+        b->lldesc.push_back(make_ll(f.al, arena, b->d_in, b->d_planes, b->d_planes + f.off_ascratch,
+                                    b->d_planes + f.off_argba, 4 * f.width));
+        b->tokdesc.push_back(make_tok(f.al, arena, b->d_in, b->d_planes));
         a.green = b->d_planes + f.off_argba;
       } else {
         a.raw = b->d_in + arena.dev_offset(f.araw);
@@ -706,6 +751,9 @@ wg_batch* batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t* si
   if (e == hipSuccess && !b->lldesc.empty())
     e = hipMemcpyAsync(b->d_lldesc, b->lldesc.data(), sizeof(LLDesc) * b->lldesc.size(), hipMemcpyHostToDevice,
                        ctx->stream);
+  if (e == hipSuccess && !b->tokdesc.empty())
+    e = hipMemcpyAsync(b->d_tokdesc, b->tokdesc.data(), sizeof(wg::LLTokDesc) * b->tokdesc.size(),
+                       hipMemcpyHostToDevice, ctx->stream);
   if (e == hipSuccess && !b->adesc.empty())
     e = hipMemcpyAsync(b->d_adesc, b->adesc.data(), sizeof(AlphaDesc) * b->adesc.size(), hipMemcpyHostToDevice,
                        ctx->stream);
@@ -733,18 +781,23 @@ int wg_batch_run(wg_batch* b, void* stream) {
     b->timings.push_back(t);
   }
   Timing& t = b->timings[b->n_runs_pending++];
-  t.ran[0] = b->n_lossy > 0;
-  t.ran[1] = b->n_lossy > 0 && !b->fused;
-  t.ran[2] = b->n_k3 > 0;
-  t.ran[3] = b->n_alpha > 0;
+  t.ran[kStageK0] = t.ran[kStageK1] = b->n_lossy > 0;
+  t.ran[kStageK2] = b->n_lossy > 0 && !b->fused;
+  t.ran[kStageK7] = t.ran[kStageK3] = b->n_k3 > 0;
+  t.ran[kStageK4] = b->n_alpha > 0;
   hipEventRecord(t.ev[0], s);
+  if (b->n_lossy > 0) {  // K0: the i16 MBs' Y2 Walsh-Hadamard transforms
+    hipError_t e = wg::launch_vp8_y2(b->d_desc, b->n, b->max_mb_h, s);
+    if (e != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
+  }
+  hipEventRecord(t.ev[kStageK1], s);
   if (b->n_lossy > 0) {
     hipError_t e = wg::launch_vp8_recon_filter(b->d_desc, b->n, b->max_mb_w, b->n_lossy > b->n_wide,
                                                b->n_wide > 0, b->d_err, s);
     if (e != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
   }
-  hipEventRecord(t.ev[1], s);
-  if (t.ran[1]) {
+  hipEventRecord(t.ev[kStageK2], s);
+  if (t.ran[kStageK2]) {
     if (b->any_crop) {
       // the crop windows of the reconstructed planes (even left/top, so chroma is aligned):
       // upsampled as standalone images, as EmitFancyRGB / EmitSampledRGB see them
@@ -770,17 +823,22 @@ int wg_batch_run(wg_batch* b, void* stream) {
                                           b->max_out_h, (b->flags & WG_FLAG_NO_FANCY_UPSAMPLING) ? 0 : 1, s);
     if (e != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
   }
-  hipEventRecord(t.ev[2], s);
+  hipEventRecord(t.ev[kStageK7], s);
+  if (b->n_k3 > 0) {  // K7: the lossless streams' color cache and back-references
+    hipError_t e = wg::launch_vp8l_resolve(b->d_tokdesc, (int)b->tokdesc.size(), b->d_err, s);
+    if (e != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
+  }
+  hipEventRecord(t.ev[kStageK3], s);
   if (b->n_k3 > 0) {
     hipError_t e = wg::launch_vp8l_transforms(b->d_lldesc, b->ll_groups, b->d_err, s);
     if (e != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
   }
-  hipEventRecord(t.ev[3], s);
+  hipEventRecord(t.ev[kStageK4], s);
   if (b->n_alpha > 0) {  // after K2 (A = 255) and K3 (alpha streams)
     hipError_t e = wg::launch_alpha(b->d_adesc, b->n_alpha, s);
     if (e != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
   }
-  hipEventRecord(t.ev[4], s);
+  hipEventRecord(t.ev[kStages], s);
   batch_mark_done(b, s);
   return WG_STATUS_OK;
 }
@@ -790,12 +848,12 @@ int wg_batch_kernel_ms(const wg_batch* bc, float* ms, int n_ms) {
   if (!b || !ms || n_ms < 1) return WG_STATUS_INVALID_PARAM;
   for (int k = 0; k < n_ms; ++k) ms[k] = 0.f;
   if (b->n_runs_pending == 0) return WG_STATUS_OK;
-  double acc[4] = {0, 0, 0, 0};
-  int cnt[4] = {0, 0, 0, 0};
+  double acc[kStages] = {};
+  int cnt[kStages] = {};
   for (size_t i = 0; i < b->n_runs_pending; ++i) {
     Timing& t = b->timings[i];
-    if (hipEventSynchronize(t.ev[4]) != hipSuccess) return WG_STATUS_USER_ABORT;
-    for (int k = 0; k < 4; ++k) {
+    if (hipEventSynchronize(t.ev[kStages]) != hipSuccess) return WG_STATUS_USER_ABORT;
+    for (int k = 0; k < kStages; ++k) {
       if (!t.ran[k]) continue;
       float a = 0;
       hipEventElapsedTime(&a, t.ev[k], t.ev[k + 1]);
@@ -805,14 +863,17 @@ int wg_batch_kernel_ms(const wg_batch* bc, float* ms, int n_ms) {
   }
   int err = 0;
   if (hipMemcpy(&err, b->d_err, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess || err) return WG_STATUS_USER_ABORT;
-  for (int k = 0; k < std::min(n_ms, 4); ++k) ms[k] = cnt[k] ? (float)(acc[k] / cnt[k]) : 0.f;
+  for (int k = 0; k < kStages; ++k) {
+    const int pub = kPublicOfStage[k];
+    if (pub < n_ms) ms[pub] = cnt[k] ? (float)(acc[k] / cnt[k]) : 0.f;
+  }
   b->n_runs_pending = 0;
   return WG_STATUS_OK;
 }
 
 int wg_batch_kernel_bytes(const wg_batch* b, double* bytes, int n_bytes) {
   if (!b || !bytes || n_bytes < 1) return WG_STATUS_INVALID_PARAM;
-  for (int k = 0; k < n_bytes; ++k) bytes[k] = k < 4 ? b->kbytes[k] : 0.0;
+  for (int k = 0; k < n_bytes; ++k) bytes[k] = k < kStages ? b->kbytes[k] : 0.0;
   if (b->fused) bytes[0] = b->k1_fused_bytes;
   return WG_STATUS_OK;
 }
@@ -843,12 +904,12 @@ int wg_batch_run_emit(wg_batch* b, void* stream) {
     b->timings.push_back(t);
   }
   Timing& t = b->timings[b->n_runs_pending++];
-  t.ran[0] = t.ran[2] = t.ran[3] = false;
-  t.ran[1] = true;
-  for (int k = 0; k < 2; ++k) hipEventRecord(t.ev[k], s);
+  for (bool& r : t.ran) r = false;
+  t.ran[kStageK2] = true;
+  for (int k = 0; k <= kStageK2; ++k) hipEventRecord(t.ev[k], s);
   hipError_t e = wg::launch_yuv_to_rgba(b->d_desc, nullptr, b->n, b->max_out_w, b->max_out_h,
                                         (b->flags & WG_FLAG_NO_FANCY_UPSAMPLING) ? 0 : 1, s);
-  for (int k = 2; k < 5; ++k) hipEventRecord(t.ev[k], s);
+  for (int k = kStageK2 + 1; k <= kStages; ++k) hipEventRecord(t.ev[k], s);
   batch_mark_done(b, s);
   return e == hipSuccess ? WG_STATUS_OK : WG_STATUS_UNSUPPORTED_FEATURE;
 }

@@ -7,6 +7,9 @@
 
 namespace wg {
 
+// K0: the Y2 Walsh-Hadamard transform of every i16 MB into FrameDesc::dcs (before K1).
+hipError_t launch_vp8_y2(const FrameDesc* d_frames, int n_frames, int max_mb_h, hipStream_t stream);
+
 // K1: fused reconstruction + loop filter, one 1024-thread workgroup per frame.
 size_t vp8_recon_lds_bytes(int mb_w);
 int vp8_recon_max_mb_w();
@@ -27,6 +30,10 @@ size_t vp8l_lds_bytes();
 constexpr int kVP8LVariants = 5;
 int vp8l_variant(const int* types, const int* bits, const int* tiles, int n_stages);  // stages in application order
 hipError_t launch_vp8l_transforms(const LLDesc* d_frames, const int* group_count, int* d_err, hipStream_t stream);
+
+// K7: VP8L color cache + back-references (tokens -> coded ARGB), one 1024-thread workgroup per
+// lossless stream; runs before K3.  d_err: OR-ed with 4 on an invalid token.
+hipError_t launch_vp8l_resolve(const LLTokDesc* d_descs, int n, int* d_err, hipStream_t stream);
 
 // K4: ALPH planes (unfilter) -> A bytes of the RGBA output, one 1024-thread workgroup per
 // plane; runs after K2 and K3.

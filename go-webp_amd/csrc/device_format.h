@@ -12,6 +12,8 @@
 //                              U 16..19, V 20..23; stored column-major
 //                              (blocks[4*c + k] = coeff[4*k + c]) so lane c of the
 //                              IDCT / WHT reads its column with one load
+//   dcs[mb_h][mb_w][16]        K0's Walsh-Hadamard output for i16 MBs with a Y2 block: the
+//                              16 Y DCs, stored dcs[4*bx + by] = DC of Y block (bx, by)
 //   Y/U/V planes               16*mb_w x 16*mb_h and 8*mb_w x 8*mb_h (MB padded)
 //   RGBA                       width x height x 4
 #pragma once
@@ -64,9 +66,28 @@ struct FrameDesc {
   int32_t width, height, mb_w, mb_h;
   int32_t y_stride, uv_stride, rgba_stride, filter_type;
   int32_t flags, valid, blocks_bytes, pad2;  // blocks_bytes: size of `blocks` (K1 bounds)
-  int32_t pad3[4];
+  int16_t* dcs;     // K0's output: per MB 16 int16 Y DCs of its Y2 block (mb_w * mb_h * 32 B)
+  int32_t pad3[2];
 };
 static_assert(sizeof(FrameDesc) == 128, "FrameDesc must be 128 bytes");
+
+// VP8L coded-image tokens (host entropy stage -> K7, vp8l_resolve.hip): bits 31..30 the kind,
+// bits 29..0 its payload.
+constexpr uint32_t kTokLiteral = 0u << 30;  // payload: index into the stream's literal array
+constexpr uint32_t kTokCache = 1u << 30;    // payload: color-cache key (< 1 << cache_bits)
+constexpr uint32_t kTokCopy = 2u << 30;     // payload: backward distance in pixels (>= 1)
+constexpr uint32_t kTokUnset = 3u << 30;    // after a failed symbol: value 0, no cache insert
+constexpr uint32_t kTokPayload = (1u << 30) - 1;
+
+// One lossless stream for K7: its tokens + literals in, the coded ARGB image out (K3's input).
+struct LLTokDesc {
+  const uint32_t* tokens;  // n_px tokens
+  const uint32_t* lits;    // n_lits literal ARGB values
+  uint32_t* coded;         // n_px resolved pixels
+  int32_t n_px, n_lits, cache_bits, valid;
+  int32_t pad[2];
+};
+static_assert(sizeof(LLTokDesc) == 48, "LLTokDesc must be 48 bytes");
 
 // One lossless (VP8L) frame for K3.  `coded` is the entropy-coded ARGB image from the host
 // stage; `stages` are its transforms in APPLICATION order (the reverse of bitstream order).

@@ -16,7 +16,10 @@ namespace wg {
 struct LLMeta {
   int width = 0, height = 0, coded_width = 0, n_transforms = 0;
   int type[4] = {0, 0, 0, 0}, bits[4] = {0, 0, 0, 0}, xsize[4] = {0, 0, 0, 0};
-  Region coded, tdata[4];
+  int cache_bits = 0;
+  Region tokens, lits, tdata[4];  // coded-image tokens (resolved by K7), literals, transform data
+  size_t off_coded = 0;           // capi.cpp: K7's output (the coded ARGB image) in the plane buffer
+  size_t n_px() const { return (size_t)coded_width * (size_t)height; }
   size_t fail_pixel = SIZE_MAX;  // see VP8LFrame::fail_pixel
   bool two_pass() const {        // predictor and color indexing both present
     int cores = 0;
@@ -33,7 +36,7 @@ struct FrameParse {
   // blocks[n_blocks][16]), offsets within it
   wg_vp8_info info{};
   Region input;
-  size_t off_rows = 0, off_blocks = 0, n_blocks = 0;
+  size_t off_rows = 0, off_blocks = 0, n_blocks = 0, n_y2 = 0;  // n_y2: i16 MBs with a Y2 block
   int br_mb_y = 0, fail_row = -1;
   // lossless
   LLMeta ll;
@@ -47,7 +50,7 @@ struct FrameParse {
   int out_w = 0, out_h = 0, win_x = 0, win_y = 0, rgba_w = 0, rgba_h = 0;
   bool cropped = false;
   // device layout (capi.cpp): offsets within the batch's plane and RGBA buffers
-  size_t off_y = 0, off_u = 0, off_v = 0, off_cols = 0, off_scratch = 0, off_rgba = 0;
+  size_t off_dcs = 0, off_y = 0, off_u = 0, off_v = 0, off_cols = 0, off_scratch = 0, off_rgba = 0;
   size_t off_ascratch = 0, off_argba = 0, off_aplane = 0;
   size_t off_yc = 0, off_uc = 0, off_vc = 0;
   int yc_stride = 0, uvc_stride = 0;

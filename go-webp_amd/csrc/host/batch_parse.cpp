@@ -76,7 +76,7 @@ bool lossy_alloc(void* p, const wg_vp8_info& inf, int rows, SparseSink* sink) {
   return true;
 }
 
-// A lossless stream into staging: its coded image and transform data.
+// A lossless stream into staging: its coded-image tokens, literals and transform data.
 bool stage_ll(const VP8LFrame& f, StagingArena* arena, StagingArena::Cursor* cur, LLMeta* m) {
   m->width = f.width;
   m->height = f.height;
@@ -90,7 +90,9 @@ bool stage_ll(const VP8LFrame& f, StagingArena* arena, StagingArena::Cursor* cur
     m->xsize[t] = tr.xsize;
     if (!arena->put(cur, tr.data.data(), tr.data.size() * 4, &m->tdata[t])) return false;
   }
-  return arena->put(cur, f.argb.data(), f.argb.size() * 4, &m->coded);
+  m->cache_bits = f.cache_bits;
+  return arena->put(cur, f.lits.data(), f.lits.size() * 4, &m->lits) &&
+         arena->put(cur, f.tokens.data(), f.tokens.size() * 4, &m->tokens);
 }
 
 // Per worker thread: the lossless entropy stage's output, reused frame after frame (its
@@ -140,13 +142,21 @@ int parse_one(const uint8_t* data, size_t size, const wg_decoder_options& opt, S
   if (c.is_lossless) {  // VP8L: host entropy stage, K3 on device
     fp->lossless = true;
     VP8LFrame& lf = tl_lf;
-    st = vp8l_parse(data + c.payload_off, c.payload_size, &lf);
-    if (st != WG_STATUS_OK && lf.fail_pixel == SIZE_MAX) return st;  // VP8LDecodeHeader
-    fp->width = lf.width;
-    fp->height = lf.height;
-    // (the options are checked once the header is known; libwebp does it before the pixels)
-    const int ost = apply_output_options(opt, fp);
-    if (ost != WG_STATUS_OK) return ost;
+    // the output options between the header/transforms/codes and the pixels, as DecodeInto
+    // orders VP8LDecodeHeader, WebPIoInitFromOptions and VP8LDecodeImage (webp.go:528-544)
+    struct Opt {
+      const wg_decoder_options* opt;
+      FrameParse* fp;
+      const VP8LFrame* lf;
+    } oc{&opt, fp, &lf};
+    auto check = [](void* p) {
+      Opt* o = static_cast<Opt*>(p);
+      o->fp->width = o->lf->width;
+      o->fp->height = o->lf->height;
+      return apply_output_options(*o->opt, o->fp);
+    };
+    st = vp8l_parse(data + c.payload_off, c.payload_size, &lf, check, &oc);
+    if (st != WG_STATUS_OK && lf.fail_pixel == SIZE_MAX) return st;  // VP8LDecodeHeader or the options
     if (st != WG_STATUS_OK) {  // DecodeImageData stops at the crop bottom (io->crop_bottom)
       // int64: crop_top + crop_height of a validated window fits, but keep it overflow-free
       const int64_t bottom = opt.use_cropping ? (int64_t)opt.crop_top + opt.crop_height : fp->height;
@@ -167,6 +177,7 @@ int parse_one(const uint8_t* data, size_t size, const wg_decoder_options& opt, S
   st = vp8_parse_sparse(data, size, flags, crop_bottom, lossy_alloc, &sink, &res);
   fp->info = res.info;
   fp->n_blocks = res.n_blocks;
+  fp->n_y2 = res.n_y2;
   fp->br_mb_y = res.br_mb_y;
   fp->fail_row = res.fail_row;
   if (sink.reserved) fp->input = arena->commit(cur, fp->off_blocks + res.n_blocks * 32);

@@ -73,6 +73,7 @@ using SparseAllocFn = bool (*)(void* ctx, const wg_vp8_info& inf, int rows, Spar
 struct SparseResult {
   wg_vp8_info info{};
   size_t n_blocks = 0;  // blocks written
+  size_t n_y2 = 0;      // of which Y2 blocks (one per i16 MB that has one)
   int br_mb_y = 0;      // MB rows parsed (VP8EnterCritical's br_mb_y_)
   int fail_row = -1;    // MB row whose parse failed (-1: none, or the headers)
 };
@@ -112,9 +113,14 @@ struct VP8LTransform {
 
 struct VP8LFrame {
   int width = 0, height = 0, has_alpha = 0;
-  int coded_width = 0;                    // width of `argb` (reduced by color-index packing)
+  int coded_width = 0;                    // width of the coded image (reduced by color-index packing)
   std::vector<VP8LTransform> transforms;  // read order
-  std::vector<uint32_t> argb;             // coded_width * height
+  // The coded image before its color cache and back-references are resolved: one token per
+  // pixel (coded_width * height, device_format.h kTok*), the literals they index, and the
+  // stream's color cache bits (0 = no cache).
+  std::vector<uint32_t> tokens;
+  std::vector<uint32_t> lits;
+  int cache_bits = 0;
   // After a failure in the pixel data: the first coded pixel whose symbol failed (SIZE_MAX:
   // the failure was in the header, transforms or codes).  A decode bounded to image rows
   // [0, r) -- a crop window, or the alpha rows requested so far -- fails iff
@@ -122,8 +128,11 @@ struct VP8LFrame {
   size_t fail_pixel = SIZE_MAX;
 };
 
-// Entropy-decode a VP8L bitstream (the VP8L chunk payload).
-int vp8l_parse(const uint8_t* data, size_t size, VP8LFrame* out);
+// Entropy-decode a VP8L bitstream (the VP8L chunk payload).  `pre_pixels` (optional) runs
+// after the header, transforms and prefix codes, before the pixels; its non-OK status is
+// returned as is (fail_pixel stays SIZE_MAX).
+int vp8l_parse(const uint8_t* data, size_t size, VP8LFrame* out, int (*pre_pixels)(void*) = nullptr,
+               void* ctx = nullptr);
 
 // Animation demux (demux/demux.go): canvas + frames in display order.  A still image is a
 // one-frame animation.  Status: OK, NOT_ENOUGH_DATA (truncated), BITSTREAM_ERROR (invalid).

@@ -724,6 +724,7 @@ int vp8_parse_sparse(const uint8_t* data, size_t size, int flags, int crop_botto
   std::unique_ptr<Decoder> dp(new Decoder());
   Decoder* d = dp.get();
   res->n_blocks = 0;
+  res->n_y2 = 0;
   res->fail_row = -1;
   res->br_mb_y = 0;
   int st = begin_frame(data, size, flags, d, &res->info);
@@ -738,6 +739,7 @@ int vp8_parse_sparse(const uint8_t* data, size_t size, int flags, int crop_botto
   const size_t mb_w = (size_t)d->mb_w;
   std::memset(sink.mbs + (size_t)done * mb_w, 0, ((size_t)d->mb_h - done) * mb_w * sizeof(MbRec));
   for (int y = done; y < d->mb_h; ++y) sink.row_block0[y] = (uint32_t)res->n_blocks;
+  for (size_t i = 0; i < (size_t)done * mb_w; ++i) res->n_y2 += (sink.mbs[i].flags & kY2Bit) != 0;
   return st;
 }
 

@@ -1,7 +1,9 @@
-// Host entropy stage of VP8L (lossless): header, transform side images, prefix codes,
-// LZ77 back-references and the color cache -- everything that is a serial walk over the
-// bit stream.  The inverse transforms (predictor, cross-color, add-green, color indexing)
-// are NOT applied here: they run on the device (K3, vp8l_transforms.hip).
+// Host entropy stage of VP8L (lossless): header, transform side images, prefix codes and
+// the symbol walk -- everything that is a serial walk over the bit stream.  The main image
+// leaves as one token per pixel (device_format.h kTok*: a literal's index, a color-cache key,
+// or a backward-reference distance): the color cache and the LZ77 copies are resolved on the
+// device (K7, vp8l_resolve.hip), and so are the inverse transforms (K3).  Side images
+// (transform data, the meta prefix-code image) are resolved here: the host needs them.
 //
 // Semantics follow the VP8L format as libwebp 1.6.0 decodes it (the reference's
 // pkg/vp8/vp8l_dec.c.go translates it; its DecodeImageStream is an unimplemented stub):
@@ -213,6 +215,12 @@ struct Decoder {
   bool in_main_pixels = false;  // the level-0 pixel loop has started (alpha error mapping)
   size_t fail_pos = SIZE_MAX;   // main image: first pixel of the symbol that failed
   std::vector<int> lengths;     // code lengths of the code being read (libwebp's code_lengths)
+  // Called once the main image's header, transforms and codes are read, before its pixels
+  // (libwebp's DecodeInto runs the output options between VP8LDecodeHeader and
+  // VP8LDecodeImage, webp.go:528-544): a non-OK status stops the decode there.
+  int (*pre_pixels)(void* ctx) = nullptr;
+  void* pre_pixels_ctx = nullptr;
+  int pre_pixels_status = WG_STATUS_OK;
   PrefixCode scratch;           // codes of meta groups the image never selects: read, validated, dropped
   explicit Decoder(const uint8_t* p, size_t n) : br(p, n), lengths(kMaxAlphabet, 0) {}
   bool fail(int st) {
@@ -292,7 +300,77 @@ struct Decoder {
     return dist >= 1 ? dist : 1;
   }
 
-  // One entropy-coded image (main image when `level0`, else a side image).
+  // The main image's symbol walk (DecodeImageData, vp8l_dec.c.go:1038-1189) without its
+  // pixel values: per pixel a token -- kTokLiteral | index into f->lits, kTokCache | key, or
+  // kTokCopy | distance (each pixel of a back-reference gets its own source distance).  The
+  // color cache lookups/inserts (vp8l_dec.c.go:1105-1109, 1141-1153) and the copies
+  // (CopyBlock32b, :915) are left to the device.  Pixels after a failing symbol are kTokUnset
+  // (value 0; they are never shown: see VP8LFrame::fail_pixel).
+  template <class GroupAt>
+  bool decode_tokens(size_t total, int xsize, uint32_t mask, int cache_size, bool rba_single, VP8LFrame* f,
+                     const GroupAt& group_at) {
+    f->tokens.resize(total);  // no fill: every token is written below
+    f->lits.clear();
+    uint32_t* data = f->tokens.data();
+    // The 8-bit alpha path (DecodeAlphaData) checks the end of stream only after storing a
+    // symbol's pixels: a stream that runs out on the symbol completing the image still
+    // decodes.  Everywhere else a symbol that reads past the end fails at its first pixel.
+    const bool late_eos = alpha_stream && f->transforms.size() == 1 &&
+                          f->transforms[0].type == kVP8LColorIndexing && cache_size == 0 && rba_single;
+    size_t pos = 0;
+    auto bad = [&](size_t at) {
+      fail_pos = at;
+      std::fill(data + at, data + total, kTokUnset);
+      return fail(WG_STATUS_BITSTREAM_ERROR);
+    };
+    int x = 0, y = 0;
+    const HTreeGroup* hg = &group_at(0, 0);
+    while (pos < total) {
+      const size_t start = pos;
+      if ((x & mask) == 0) hg = &group_at(x, y);
+      const int code = hg->code[0].read(br);
+      if (code < kNumLiteralCodes) {
+        const uint32_t r = (uint32_t)hg->code[1].read(br);
+        const uint32_t b = (uint32_t)hg->code[2].read(br);
+        const uint32_t a = (uint32_t)hg->code[3].read(br);
+        if (br.eos() && !(late_eos && pos + 1 == total)) return bad(start);
+        data[pos++] = kTokLiteral | (uint32_t)f->lits.size();
+        f->lits.push_back((a << 24) | (r << 16) | ((uint32_t)code << 8) | b);
+        if (++x >= xsize) {
+          x = 0;
+          ++y;
+        }
+      } else if (code < kNumLiteralCodes + kNumLengthCodes) {
+        const int length = copy_distance(code - kNumLiteralCodes, br);
+        const int dist_sym = hg->code[4].read(br);
+        const int dist = plane_code_to_distance(xsize, copy_distance(dist_sym, br));
+        if (br.eos() && !late_eos) return bad(start);
+        if ((size_t)dist > pos || total - pos < (size_t)length) return bad(start);
+        if (br.eos() && pos + (size_t)length < total) return bad(start);
+        const uint32_t t = kTokCopy | (uint32_t)dist;
+        for (int i = 0; i < length; ++i) data[pos++] = t;
+        x += length;
+        while (x >= xsize) {
+          x -= xsize;
+          ++y;
+        }
+        if (pos < total && (x & mask)) hg = &group_at(x, y);
+      } else {
+        if (br.eos()) return bad(start);
+        const int key = code - (kNumLiteralCodes + kNumLengthCodes);
+        if (key >= cache_size) return bad(start);
+        data[pos++] = kTokCache | (uint32_t)key;
+        if (++x >= xsize) {
+          x = 0;
+          ++y;
+        }
+      }
+    }
+    return true;
+  }
+
+  // One entropy-coded image: the main image when `level0` (as tokens into f->tokens /
+  // f->lits), else a side image (pixel values into *out).
   bool decode_stream(int xsize, int ysize, bool level0, VP8LFrame* f, std::vector<uint32_t>* out) {
     if (level0) {
       unsigned seen = 0;
@@ -382,41 +460,36 @@ struct Decoder {
       }
     }
     // pixels
-    if (level0) in_main_pixels = true;
     const size_t total = (size_t)xsize * ysize;
-    out->assign(total, 0u);
-    uint32_t* data = out->data();
-    std::vector<uint32_t> cache((size_t)std::max(cache_size, 1), 0u);
-    const int cache_shift = 32 - cache_bits;
     const uint32_t mask = huff_bits ? (1u << huff_bits) - 1 : ~0u;
     auto group_at = [&](int x, int y) -> const HTreeGroup& {
       if (!huff_bits) return groups[0];
       return groups[huff_image[(size_t)(y >> huff_bits) * huff_xsize + (x >> huff_bits)]];
     };
-    auto insert = [&](uint32_t argb) {
+    if (level0) {
+      if (pre_pixels && (pre_pixels_status = pre_pixels(pre_pixels_ctx)) != WG_STATUS_OK) return false;
+      in_main_pixels = true;
+      f->cache_bits = cache_bits;
+      return decode_tokens(total, xsize, mask, cache_size, rba_single, f, group_at);
+    }
+    out->assign(total, 0u);
+    uint32_t* data = out->data();
+    std::vector<uint32_t> cache((size_t)std::max(cache_size, 1), 0u);
+    const int cache_shift = 32 - cache_bits;
+    auto insert = [&](uint32_t argb) {  // VP8LColorCacheInsert (color_cache.go:50-55)
       if (cache_bits) cache[(argb * 0x1e35a7bdu) >> cache_shift] = argb;
-    };
-    // The 8-bit alpha path (DecodeAlphaData) checks the end of stream only after storing a
-    // symbol's pixels: a stream that runs out on the symbol completing the image still
-    // decodes.  Everywhere else a symbol that reads past the end fails at its first pixel.
-    const bool late_eos = alpha_stream && level0 && f->transforms.size() == 1 &&
-                          f->transforms[0].type == kVP8LColorIndexing && cache_bits == 0 && rba_single;
-    auto bad = [&](size_t at) {
-      if (level0) fail_pos = at;
-      return fail(WG_STATUS_BITSTREAM_ERROR);
     };
     size_t pos = 0;
     int x = 0, y = 0;
     const HTreeGroup* hg = &group_at(0, 0);
     while (pos < total) {
-      const size_t start = pos;
       if ((x & mask) == 0) hg = &group_at(x, y);
       const int code = hg->code[0].read(br);
       if (code < kNumLiteralCodes) {
         const uint32_t r = (uint32_t)hg->code[1].read(br);
         const uint32_t b = (uint32_t)hg->code[2].read(br);
         const uint32_t a = (uint32_t)hg->code[3].read(br);
-        if (br.eos() && !(late_eos && pos + 1 == total)) return bad(start);
+        if (br.eos()) return fail(WG_STATUS_BITSTREAM_ERROR);
         const uint32_t argb = (a << 24) | (r << 16) | ((uint32_t)code << 8) | b;
         data[pos++] = argb;
         insert(argb);
@@ -428,9 +501,7 @@ struct Decoder {
         const int length = copy_distance(code - kNumLiteralCodes, br);
         const int dist_sym = hg->code[4].read(br);
         const int dist = plane_code_to_distance(xsize, copy_distance(dist_sym, br));
-        if (br.eos() && !late_eos) return bad(start);
-        if ((size_t)dist > pos || total - pos < (size_t)length) return bad(start);
-        if (br.eos() && pos + (size_t)length < total) return bad(start);
+        if (br.eos() || (size_t)dist > pos || total - pos < (size_t)length) return fail(WG_STATUS_BITSTREAM_ERROR);
         for (int i = 0; i < length; ++i) {
           const uint32_t argb = data[pos - dist];
           data[pos++] = argb;
@@ -443,10 +514,10 @@ struct Decoder {
         }
         if (pos < total && (x & mask)) hg = &group_at(x, y);
       } else {
-        if (br.eos()) return bad(start);
+        if (br.eos()) return fail(WG_STATUS_BITSTREAM_ERROR);
         const int key = code - (kNumLiteralCodes + kNumLengthCodes);
-        if (key >= cache_size) return bad(start);
-        const uint32_t argb = cache[(size_t)key];
+        if (key >= cache_size) return fail(WG_STATUS_BITSTREAM_ERROR);
+        const uint32_t argb = cache[(size_t)key];  // VP8LColorCacheLookup (color_cache.go:57-63)
         data[pos++] = argb;
         insert(argb);
         if (++x >= xsize) {
@@ -461,7 +532,7 @@ struct Decoder {
 
 }  // namespace
 
-int vp8l_parse(const uint8_t* data, size_t size, VP8LFrame* out) {
+int vp8l_parse(const uint8_t* data, size_t size, VP8LFrame* out, int (*pre_pixels)(void*), void* ctx) {
   if (!data || size < 5 || !out) return WG_STATUS_NOT_ENOUGH_DATA;
   out->fail_pixel = SIZE_MAX;
   Decoder d(data, size);
@@ -472,7 +543,11 @@ int vp8l_parse(const uint8_t* data, size_t size, VP8LFrame* out) {
   if (d.br.read(3) != 0) return WG_STATUS_BITSTREAM_ERROR;
   out->transforms.clear();
   out->coded_width = out->width;
-  if (!d.decode_stream(out->width, out->height, true, out, &out->argb)) {
+  out->cache_bits = 0;
+  d.pre_pixels = pre_pixels;
+  d.pre_pixels_ctx = ctx;
+  if (!d.decode_stream(out->width, out->height, true, out, nullptr)) {
+    if (d.pre_pixels_status != WG_STATUS_OK) return d.pre_pixels_status;
     out->fail_pixel = d.fail_pos;
     return d.status;
   }
@@ -492,10 +567,11 @@ int vp8l_parse_alpha(const uint8_t* data, size_t size, int width, int height, VP
   out->has_alpha = 0;
   out->transforms.clear();
   out->coded_width = width;
+  out->cache_bits = 0;
   out->fail_pixel = SIZE_MAX;
   Decoder d(data, size);
   d.alpha_stream = true;
-  if (!d.decode_stream(width, height, true, out, &out->argb)) {
+  if (!d.decode_stream(width, height, true, out, nullptr)) {
     if (!d.in_main_pixels) return WG_STATUS_OUT_OF_MEMORY;
     out->fail_pixel = d.fail_pos;
     return WG_STATUS_BITSTREAM_ERROR;

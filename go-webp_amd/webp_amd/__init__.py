@@ -19,7 +19,7 @@ import numpy as np
 __all__ = [
     "Status", "WebPError", "FLAG_BYPASS_FILTERING", "FLAG_NO_FANCY_UPSAMPLING", "Features",
     "lib", "features", "decode_config", "decode", "Context", "Batch", "vp8_parse", "vp8l_parse", "MB_DTYPE",
-    "VP8Info", "VP8LInfo", "device_count", "yuv420_to_rgba_device", "MultiContext", "set_default_device",
+    "VP8Info", "VP8LInfo", "VP8LCoded", "device_count", "yuv420_to_rgba_device", "MultiContext", "set_default_device",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -109,7 +109,18 @@ class VP8LInfo(C.Structure):
     _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("has_alpha", C.c_int32),
                 ("coded_width", C.c_int32), ("num_transforms", C.c_int32),
                 ("transform_type", C.c_int32 * 4), ("transform_bits", C.c_int32 * 4),
-                ("transform_xsize", C.c_int32 * 4), ("transform_size", C.c_int32 * 4)]
+                ("transform_xsize", C.c_int32 * 4), ("transform_size", C.c_int32 * 4),
+                ("cache_bits", C.c_int32), ("num_literals", C.c_int32)]
+
+
+class VP8LCoded:
+    """A lossless image after the host prefix-code walk: one token per coded pixel
+    (tokens: (height, coded_width) uint32; bits 31..30 = 0 literal index, 1 color-cache key,
+    2 backward distance, 3 unset), the literal ARGB values and the color cache bits.  The
+    device (K7) resolves it into the coded ARGB image."""
+
+    def __init__(self, tokens, lits, cache_bits):
+        self.tokens, self.lits, self.cache_bits = tokens, lits, cache_bits
 
 
 # wg_vp8_mb: VP8MBData + VP8FInfo (pkg/vp8/models.go:66-107)
@@ -145,8 +156,8 @@ _SIGS = {
     "wg_yuv420_to_rgba_device": (C.c_int, [_P, _P, _P, C.c_int, C.c_int, _P, C.c_int, C.c_int, C.c_int,
                                            C.c_int, _P]),
     "wg_vp8_parse": (C.c_int, [_P, C.c_size_t, C.c_int, C.POINTER(VP8Info), _P]),
-    "wg_vp8l_parse": (C.c_int, [_P, C.c_size_t, C.POINTER(VP8LInfo), _P, _P]),
-    "wg_alpha_parse": (C.c_int, [_P, C.c_size_t, _P, _P, _P, _P, _P]),
+    "wg_vp8l_parse": (C.c_int, [_P, C.c_size_t, C.POINTER(VP8LInfo), _P, _P, _P]),
+    "wg_alpha_parse": (C.c_int, [_P, C.c_size_t, _P, _P, _P, _P, _P, _P]),
     "wg_anim_demux": (C.c_int, [_P, C.c_size_t, _P, _P, C.c_int]),
     "wg_output_bpp": (C.c_int, [C.c_int]),
     "wg_decode_into": (C.c_int, [_P, C.c_size_t, _P, _P, C.c_size_t, C.c_int]),
@@ -279,48 +290,52 @@ def vp8_parse(data, flags=0, with_mbs=True):
     return info, mbs
 
 
+def _vp8l_outputs(info):
+    tokens = np.zeros((info.height, info.coded_width), np.uint32)
+    lits = np.zeros(max(1, info.num_literals), np.uint32)
+    tdata = [np.zeros(max(1, info.transform_size[i]), np.uint32) for i in range(info.num_transforms)]
+    ptrs = (C.c_void_p * 4)(*([t.ctypes.data for t in tdata] + [None] * (4 - len(tdata))))
+    return tokens, lits, tdata, ptrs
+
+
 def vp8l_parse(data):
-    """Host entropy stage of a lossless file: (VP8LInfo, coded ARGB image as uint32
-    (height, coded_width), [transform data arrays in read order])."""
+    """Host entropy stage of a lossless file: (VP8LInfo, VP8LCoded, [transform data arrays
+    in read order])."""
     b = _buf(data)
     info = VP8LInfo()
     L = lib()
-    st = L.wg_vp8l_parse(b, len(b), C.byref(info), None, None)
+    st = L.wg_vp8l_parse(b, len(b), C.byref(info), None, None, None)
     if st != Status.OK:
         raise WebPError(st, "wg_vp8l_parse")
-    argb = np.zeros((info.height, info.coded_width), np.uint32)
-    tdata = [np.zeros(max(1, info.transform_size[i]), np.uint32) for i in range(info.num_transforms)]
-    ptrs = (C.c_void_p * 4)(*([t.ctypes.data for t in tdata] + [None] * (4 - len(tdata))))
-    st = L.wg_vp8l_parse(b, len(b), C.byref(info), argb.ctypes.data, ptrs)
+    tokens, lits, tdata, ptrs = _vp8l_outputs(info)
+    st = L.wg_vp8l_parse(b, len(b), C.byref(info), tokens.ctypes.data, lits.ctypes.data, ptrs)
     if st != Status.OK:
         raise WebPError(st, "wg_vp8l_parse")
-    return info, argb, tdata
+    return info, VP8LCoded(tokens, lits[:info.num_literals], info.cache_bits), tdata
 
 
 def alpha_parse(data):
     """Host stage of the ALPH chunk of a lossy file: (AlphaInfo, payload) with payload the
-    (height, width) filtered bytes for method 0, or (VP8LInfo, argb, tdata) of the alpha
+    (height, width) filtered bytes for method 0, or (VP8LInfo, VP8LCoded, tdata) of the alpha
     stream (as vp8l_parse returns them) for method 1."""
     b = _buf(data)
     info = AlphaInfo()
     ll = VP8LInfo()
     L = lib()
-    st = L.wg_alpha_parse(b, len(b), C.byref(info), None, C.byref(ll), None, None)
+    st = L.wg_alpha_parse(b, len(b), C.byref(info), None, C.byref(ll), None, None, None)
     if st != Status.OK:
         raise WebPError(st, "wg_alpha_parse")
     if info.method == 0:
         filt = np.zeros((info.height, info.width), np.uint8)
-        st = L.wg_alpha_parse(b, len(b), C.byref(info), filt.ctypes.data, None, None, None)
+        st = L.wg_alpha_parse(b, len(b), C.byref(info), filt.ctypes.data, None, None, None, None)
         if st != Status.OK:
             raise WebPError(st, "wg_alpha_parse")
         return info, filt
-    argb = np.zeros((ll.height, ll.coded_width), np.uint32)
-    tdata = [np.zeros(max(1, ll.transform_size[i]), np.uint32) for i in range(ll.num_transforms)]
-    ptrs = (C.c_void_p * 4)(*([t.ctypes.data for t in tdata] + [None] * (4 - len(tdata))))
-    st = L.wg_alpha_parse(b, len(b), C.byref(info), None, C.byref(ll), argb.ctypes.data, ptrs)
+    tokens, lits, tdata, ptrs = _vp8l_outputs(ll)
+    st = L.wg_alpha_parse(b, len(b), C.byref(info), None, C.byref(ll), tokens.ctypes.data, lits.ctypes.data, ptrs)
     if st != Status.OK:
         raise WebPError(st, "wg_alpha_parse")
-    return info, (ll, argb, tdata)
+    return info, (ll, VP8LCoded(tokens, lits[:ll.num_literals], ll.cache_bits), tdata)
 
 
 def anim_demux(data):
@@ -382,17 +397,17 @@ class Batch:
             raise WebPError(st, "wg_batch_run_emit")
 
     def kernel_ms(self):
-        """(K1, K2, K3, K4) per-launch ms averaged over the runs since the last call."""
-        ms = (C.c_float * 4)()
-        st = lib().wg_batch_kernel_ms(self._h, ms, 4)
+        """(K1, K2, K3, K4, K7, K0) per-launch ms averaged over the runs since the last call."""
+        ms = (C.c_float * 6)()
+        st = lib().wg_batch_kernel_ms(self._h, ms, 6)
         if st != Status.OK:
             raise WebPError(st, "wg_batch_kernel_ms")
         return tuple(float(v) for v in ms)
 
     def kernel_bytes(self):
-        """Algorithmic HBM bytes per launch of (K1, K2, K3, K4)."""
-        b = (C.c_double * 4)()
-        lib().wg_batch_kernel_bytes(self._h, b, 4)
+        """Algorithmic HBM bytes per launch of (K1, K2, K3, K4, K7, K0)."""
+        b = (C.c_double * 6)()
+        lib().wg_batch_kernel_bytes(self._h, b, 6)
         return tuple(float(v) for v in b)
 
     @property

@@ -176,10 +176,12 @@ int wg_batch_run_emit(wg_batch* b, void* stream);
 /* Per-launch kernel durations averaged over the runs since the last query:
  * ms[0] = VP8 reconstruct+filter (K1, with its RGBA tail by default), ms[1] = YUV->RGBA (K2), ms[2] = VP8L inverse
  * transforms (K3, lossless frames and lossless ALPH streams), ms[3] = ALPH unfilter + A
- * channel (K4); a kernel with no frames in the batch reports 0.  n_ms >= 1. */
+ * channel (K4), ms[4] = VP8L color cache + back-references (K7, before K3), ms[5] = the Y2
+ * Walsh-Hadamard transforms of the i16 macroblocks (K0, before K1); a kernel with no frames in
+ * the batch reports 0.  n_ms >= 1 (entries beyond n_ms are not written). */
 int wg_batch_kernel_ms(const wg_batch* b, float* ms, int n_ms);
 
-/* Algorithmic HBM bytes per launch of K1, K2, K3, K4; K1 with
+/* Algorithmic HBM bytes per launch of K1, K2, K3, K4, K7, K0; K1 with
  * its RGBA tail: records + coefficients in, RGBA out (the planes are an intermediate). */
 int wg_batch_kernel_bytes(const wg_batch* b, double* bytes, int n_bytes);
 
@@ -236,10 +238,14 @@ typedef struct {
 int wg_vp8_parse(const uint8_t* data, size_t size, int flags, wg_vp8_info* info, wg_vp8_mb* mbs);
 
 /* ---- host entropy stage of VP8L (lossless) --------------------------------------------- */
-/* A lossless frame after prefix-code / LZ77 / color-cache decoding (libwebp DecodeImageStream,
- * reference pkg/vp8/vp8l_dec.c.go), before its inverse transforms.  Transforms are listed in
- * bitstream (read) order; they are undone in reverse.  Types: 0 predictor, 1 cross-color,
- * 2 subtract-green, 3 color indexing. */
+/* A lossless frame after the prefix-code walk (libwebp DecodeImageStream, reference
+ * pkg/vp8/vp8l_dec.c.go), before its color cache, back-references and inverse transforms: one
+ * token per coded pixel -- bits 31..30: 0 literal (bits 29..0 = index into the literal array),
+ * 1 color-cache reference (key), 2 backward reference (distance in pixels), 3 unset (pixels
+ * after a failing symbol, value 0) -- plus the literals.  The device resolves the tokens
+ * (color cache: VP8LColorCache, color_cache.go:16-80; copies: CopyBlock32b) and applies the
+ * transforms.  Transforms are listed in bitstream (read) order; they are undone in reverse.
+ * Types: 0 predictor, 1 cross-color, 2 subtract-green, 3 color indexing. */
 typedef struct {
   int32_t width, height, has_alpha;
   int32_t coded_width;          /* width of the entropy-coded image (< width with pixel packing) */
@@ -248,12 +254,14 @@ typedef struct {
   int32_t transform_bits[4];    /* tile bits, or packing bits for color indexing              */
   int32_t transform_xsize[4];   /* output width of the transform                              */
   int32_t transform_size[4];    /* uint32 words of its data (tile image / expanded palette)    */
+  int32_t cache_bits;           /* color cache size 1 << cache_bits (0 = no cache)             */
+  int32_t num_literals;         /* uint32 words of the literal array                           */
 } wg_vp8l_info;
 
-/* `argb` (coded_width*height words) and `transform_data[i]` (transform_size[i] words) may be
- * NULL to only fill `info`. */
-int wg_vp8l_parse(const uint8_t* data, size_t size, wg_vp8l_info* info, uint32_t* argb,
-                  uint32_t* const* transform_data);
+/* `tokens` (coded_width*height words), `literals` (num_literals words) and
+ * `transform_data[i]` (transform_size[i] words) may be NULL to only fill `info`. */
+int wg_vp8l_parse(const uint8_t* data, size_t size, wg_vp8l_info* info, uint32_t* tokens,
+                  uint32_t* literals, uint32_t* const* transform_data);
 
 /* ---- host stage of an ALPH plane (VP8 + alpha) ----------------------------------------- */
 /* The ALPH chunk of a lossy frame (reference ALPHInit / VP8LDecodeAlphaHeader,
@@ -267,13 +275,14 @@ typedef struct {
 } wg_alpha_info;
 
 /* Parse the ALPH chunk of `data` (a whole WebP file).  method 0: the width*height filtered
- * bytes go to `filtered`; method 1: the alpha stream's entropy stage goes to ll_info / argb /
- * transform_data exactly as wg_vp8l_parse fills them.  Any output pointer may be NULL.
+ * bytes go to `filtered`; method 1: the alpha stream's entropy stage goes to ll_info / tokens /
+ * literals / transform_data exactly as wg_vp8l_parse fills them.  Any output pointer may be NULL.
  * Status as WebPDecode would report the plane: an invalid header or stream header is
  * OUT_OF_MEMORY (libwebp's ALPHInit failure path), a bad pixel stream BITSTREAM_ERROR; a frame
  * without ALPH is UNSUPPORTED_FEATURE. */
 int wg_alpha_parse(const uint8_t* data, size_t size, wg_alpha_info* info, uint8_t* filtered,
-                   wg_vp8l_info* ll_info, uint32_t* argb, uint32_t* const* transform_data);
+                   wg_vp8l_info* ll_info, uint32_t* tokens, uint32_t* literals,
+                   uint32_t* const* transform_data);
 
 /* ---- animation (ANIM / ANMF) --------------------------------------------------------- */
 /* WebPAnimInfo (reference pkg/libwebp/webp/demux.go:124-131). */

@@ -710,6 +710,8 @@ BENCH_CASES = [
     ("c3_4k", 2160, 3840, list(range(8)), {"filter_type": 1, "filter_strength": 60}, "synth6"),
     ("c5_ll2048", 2048, 2048, [0], {"lossless": 1}, "corr"),
 ]
+# section bench_c5x: the other C5 seeds (K = 8 distinct lossless frames, like C2 / C3)
+BENCH_C5X = [("c5_ll2048", 2048, 2048, list(range(1, 8)), {"lossless": 1}, "corr")]
 
 
 def sha(a):
@@ -719,15 +721,17 @@ def sha(a):
 def main(argv):
     """argv: sections to (re)generate among lossy, lossy_extra, lossless, alpha, modes, anim, bench (default: all);
     the manifest entries of the other sections are kept."""
-    sections = set(argv) or {"lossy", "lossy_extra", "lossless", "alpha", "modes", "anim", "bench"}
+    sections = set(argv) or {"lossy", "lossy_extra", "lossless", "alpha", "modes", "anim", "bench", "bench_c5x",
+                             "fuzz"}
     os.makedirs(os.path.join(HERE, "lossy"), exist_ok=True)
     os.makedirs(os.path.join(HERE, "lossless"), exist_ok=True)
     os.makedirs(os.path.join(HERE, "bench"), exist_ok=True)
     mpath = os.path.join(HERE, "manifest.json")
     manifest = json.load(open(mpath)) if os.path.exists(mpath) else {}
     manifest["libwebp"] = "1.6.0 (Pillow 12.2.0 bundle, plain-C DSP)"
-    for sec in sections:
+    for sec in sections - {"bench_c5x"}:  # (bench_c5x adds to "bench")
         manifest[sec] = {}
+    manifest.setdefault("bench", {})
     if "alpha" in sections:
         manifest["alpha_errors"] = {}
     extra = LOSSY_EXTRA_CASES if "lossy_extra" in sections else []
@@ -819,7 +823,8 @@ def main(argv):
             manifest["anim"][name] = dict(bytes=len(data), info=info, frames=flags)
             print(name, len(data), info, [(f["x"], f["y"], f["w"], f["h"], f["dispose_bg"], f["no_blend"])
                                           for f in flags], flush=True)
-    for name, H, W, seeds, kw, gen in BENCH_CASES if "bench" in sections else []:
+    bench = (BENCH_CASES if "bench" in sections else []) + (BENCH_C5X if "bench_c5x" in sections else [])
+    for name, H, W, seeds, kw, gen in bench:
         for s in seeds:
             img = synth(H, W, s, 6) if gen == "synth6" else corr_luma(H, W, s)
             lossless = kw.get("lossless", 0)
@@ -834,6 +839,23 @@ def main(argv):
                 ent["header"] = vp8_header(data)
             manifest["bench"][fn] = ent
             print(fn, len(data), flush=True)
+    if "fuzz" in sections:
+        # libwebp's WebPDecode status and RGBA digest of every mutant of the fuzz corpora
+        # (oracle_lib.fuzz_mutants), so the GPU fuzz tests compare against libwebp too
+        sys.path.insert(0, os.path.dirname(HERE))
+        from oracle_lib import FUZZ_LOSSLESS, FUZZ_LOSSY, fuzz_mutants
+        for kind, args in (("lossy", FUZZ_LOSSY), ("lossless", FUZZ_LOSSLESS)):
+            ent = {}
+            for key, data in fuzz_mutants(kind, *args):
+                st, rgba = decode_mode(data, MODE_RGBA)
+                _plain_c(False)
+                st2, rgba2 = decode_mode(data, MODE_RGBA)
+                _plain_c(True)
+                assert st == st2 and (rgba is None or np.array_equal(rgba, rgba2)), key
+                ent[key] = dict(status=st, rgba=sha(rgba) if rgba is not None else None)
+            manifest["fuzz"][kind] = ent
+            print("fuzz", kind, len(ent), "mutants,", sum(1 for e in ent.values() if e["status"] == 0), "decode",
+                  flush=True)
     with open(os.path.join(HERE, "manifest.json"), "w") as f:
         json.dump(manifest, f, indent=1, sort_keys=True)
 

@@ -24,9 +24,11 @@ uint64_t digest(const wg::StagingArena& a, const wg::FrameParse& f) {
     if (r.chunk >= 0 && r.bytes) h = fnv(a.host_ptr(r), r.bytes, h);
   };
   reg(f.input);
-  reg(f.ll.coded);
+  reg(f.ll.tokens);
+  reg(f.ll.lits);
   for (int t = 0; t < 4; ++t) reg(f.ll.tdata[t]);
-  reg(f.al.coded);
+  reg(f.al.tokens);
+  reg(f.al.lits);
   for (int t = 0; t < 4; ++t) reg(f.al.tdata[t]);
   reg(f.araw);
   return h;

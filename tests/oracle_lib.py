@@ -32,6 +32,7 @@ def oracle():
         L.oracle_transform_block.argtypes = [P, P, C.c_int]
         L.oracle_transform_block.restype = None
         L.oracle_vp8l_decode.argtypes = [P, P, P, P]
+        L.oracle_vp8l_resolve.argtypes = [P, P, C.c_int, C.c_int, C.c_int, P]
         L.oracle_alpha_unfilter.argtypes = [C.c_int, C.c_int, C.c_int, P, P]
         L.oracle_anim_compose.argtypes = [P, C.c_int, C.c_int, C.c_int, P, P]
         L.oracle_emit.argtypes = [P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, P, C.c_int]
@@ -53,8 +54,22 @@ def oracle_decode(info, mbs, fancy=True):
     return dict(y=y, u=u, v=v, rgba=rgba)
 
 
-def oracle_vp8l_decode(info, argb, tdata):
-    """CPU inverse transforms + BGRA->RGBA of a lossless frame from webp_amd.vp8l_parse."""
+def oracle_vp8l_resolve(info, coded):
+    """CPU color cache + back-references (the reference's pixel loop) of the tokens from
+    webp_amd.vp8l_parse: -> the coded ARGB image, (height, coded_width) uint32."""
+    toks = np.ascontiguousarray(coded.tokens, np.uint32)
+    lits = np.ascontiguousarray(coded.lits, np.uint32)
+    argb = np.empty((info.height, info.coded_width), np.uint32)
+    assert oracle().oracle_vp8l_resolve(toks.ctypes.data, lits.ctypes.data, len(lits), argb.size, coded.cache_bits,
+                                        argb.ctypes.data) == 0
+    return argb
+
+
+def oracle_vp8l_decode(info, coded, tdata):
+    """CPU decode of a lossless frame from webp_amd.vp8l_parse: the color cache and copies
+    (oracle_vp8l_resolve), then the inverse transforms + BGRA->RGBA.  `coded` may also be an
+    already resolved ARGB array."""
+    argb = coded if isinstance(coded, np.ndarray) else oracle_vp8l_resolve(info, coded)
     rgba = np.empty((info.height, info.width, 4), np.uint8)
     ptrs = (C.c_void_p * 4)(*([t.ctypes.data for t in tdata] + [None] * (4 - len(tdata))))
     assert oracle().oracle_vp8l_decode(C.addressof(info), argb.ctypes.data, ptrs, rgba.ctypes.data) == 0
@@ -95,6 +110,35 @@ def load_lossy(name):
     return data, dict(np.load(os.path.join(GOLDEN, "lossy", name + ".npz")))
 
 
+def fuzz_mutants(kind, seed, per_source, n_sources, lo, flips):
+    """The mutation fuzz corpus (tests/test_gpu_fuzz.py; libwebp's results for it are committed
+    by tests/golden/make_golden.py `fuzz`): for the n_sources smallest fixtures of `kind`
+    ('lossy' without the ALPH one, or 'lossless'), per_source copies with 1..flips-1 random bit
+    flips at byte positions >= lo.  -> [(key, bytes)] in generation order, key 'src:k'."""
+    rng = np.random.default_rng(seed)
+    if kind == "lossy":
+        names = [n for n in lossy_cases() if n != "alpha_64x48"]
+        load = load_lossy
+    else:
+        names = lossless_names()
+        load = load_lossless
+    out = []
+    for n in sorted(names, key=lambda n: len(load(n)[0]))[:n_sources]:
+        d = bytearray(load(n)[0])
+        for k in range(per_source):
+            m = bytearray(d)
+            for _ in range(int(rng.integers(1, flips))):
+                pos = int(rng.integers(lo, len(m)))
+                m[pos] ^= 1 << int(rng.integers(0, 8))
+            out.append((f"{n}:{k}", bytes(m)))
+    return out
+
+
+# (seed, per_source, n_sources, first byte, flips) of the two fuzz corpora
+FUZZ_LOSSY = (7, 24, 8, 40, 4)
+FUZZ_LOSSLESS = (11, 24, 10, 25, 3)
+
+
 def bench_files(prefix):
     return sorted(glob.glob(os.path.join(GOLDEN, "bench", prefix + "_s*.webp")))
 
@@ -109,8 +153,8 @@ def oracle_alpha_plane(data):
     if info.method == 0:
         filtered = payload
     else:
-        ll, argb, tdata = payload
-        filtered = np.ascontiguousarray(oracle_vp8l_decode(ll, argb, tdata)[..., 1])
+        ll, coded, tdata = payload
+        filtered = np.ascontiguousarray(oracle_vp8l_decode(ll, coded, tdata)[..., 1])
     out = np.empty((info.height, info.width), np.uint8)
     assert oracle().oracle_alpha_unfilter(info.filter, info.width, info.height, filtered.ctypes.data,
                                           out.ctypes.data) == 0
@@ -134,8 +178,8 @@ def oracle_still_rgba(data):
     import webp_amd
 
     if webp_amd.features(data).format == 2:
-        info, argb, tdata = webp_amd.vp8l_parse(data)
-        return oracle_vp8l_decode(info, argb, tdata)
+        info, coded, tdata = webp_amd.vp8l_parse(data)
+        return oracle_vp8l_decode(info, coded, tdata)
     info, mbs = webp_amd.vp8_parse(data)
     rgba = oracle_decode(info, mbs)["rgba"]
     try:
@@ -203,8 +247,8 @@ def oracle_output(data, mode=1, crop=None, flip=0, no_fancy=0, bypass=0):
         if not (ok(crop[0] & ~1, crop[1] & ~1) and ok(x, y)):
             return None
     if f.format == 2:
-        info, argb, tdata = webp_amd.vp8l_parse(data)
-        rgba = oracle_vp8l_decode(info, argb, tdata)[y:y + ch, x:x + cw]
+        info, coded, tdata = webp_amd.vp8l_parse(data)
+        rgba = oracle_vp8l_decode(info, coded, tdata)[y:y + ch, x:x + cw]
     else:
         info, mbs = webp_amd.vp8_parse(data, flags=1 if bypass else 0)
         planes = oracle_decode(info, mbs)

@@ -105,3 +105,18 @@ def test_yuv_stage_entry_rejects_bad_geometry_before_any_device_call():
         with pytest.raises(webp_amd.WebPError) as e:
             webp_amd.yuv420_to_rgba_device(p, p, p, a["ys"], a["uvs"], p, a["rs"], a["w"], a["h"], True, None)
         assert e.value.status == webp_amd.Status.INVALID_PARAM, a
+
+
+def test_go_shim_calls_only_exported_entry_points():
+    """go/webp/decode_amd.go (the cgo binding a maintainer of the reference would add; no Go
+    toolchain here to compile it) calls only entry points the header declares and the
+    library exports, and guards empty inputs before indexing them."""
+    src = open(os.path.join(ROOT, "go", "webp", "decode_amd.go")).read()
+    called = set(re.findall(r"\bC\.(wg_[a-z0-9_]+)\s*\(", src))
+    assert called >= {"wg_get_features", "wg_decode_rgba_into", "wg_decode_rgba_batch", "wg_decode_rgba_batch_multi",
+                      "wg_ctx_create", "wg_ctx_destroy", "wg_set_default_device", "wg_anim_decode"}
+    assert called <= set(webp_amd.EXPORTED), called - set(webp_amd.EXPORTED)
+    L = C.CDLL(webp_amd.LIB_PATH)
+    assert all(hasattr(L, s) for s in called)
+    # every `&x[0]` of a caller slice sits behind a length check
+    assert "if len(f) > 0" in src and "if len(data) == 0" in src

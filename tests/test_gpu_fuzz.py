@@ -1,99 +1,82 @@
-"""Mutation fuzz of the GPU lossy path against the CPU oracle.
+"""Mutation fuzz of the GPU paths against libwebp 1.6.0 and the CPU oracle.
 
-Bit-flipped copies of lossy fixtures that still parse decode to arbitrary (often extreme)
-coefficients, modes and filter parameters -- the int16 / 32-bit wrapping corners of
-TransformOne, the clamps of every predictor and filter tap.  Each parseable mutant goes
-through one GPU batch (K1 with its RGBA tail, and K2 separately) and must match the
-oracle's Y/U/V and RGBA bit for bit.  The oracle itself is pinned to libwebp 1.6.0 by
-tests/test_oracle.py; for the mutants no libwebp decode is committed, so parity here is
-GPU == oracle (the reference's own tests have no corrupted-stream vectors for this path).
+Bit-flipped copies of the smallest lossy and lossless fixtures (oracle_lib.fuzz_mutants, a
+fixed seeded corpus) decode to arbitrary, often extreme, coefficients, modes and filter
+parameters -- the int16 / 32-bit wrapping corners of TransformOne, the clamps of every
+predictor and filter tap -- or, for VP8L, to other prefix codes, cache sizes, transform data
+and palettes.  The whole corpus goes through one GPU batch, and every mutant must match
+libwebp 1.6.0's WebPDecode (tests/golden/manifest.json "fuzz": status and RGBA SHA-256,
+committed by make_golden.py) -- failing ones with libwebp's status -- and, where it decodes,
+the oracle bit for bit (Y/U/V and RGBA for lossy: K1's tail and a separate K2; RGBA through
+K7 + K3 for lossless).
 """
+import hashlib
+
 import numpy as np
 import pytest
 
 import webp_amd
-from oracle_lib import load_lossy, lossy_cases, oracle_decode
+from oracle_lib import (FUZZ_LOSSLESS, FUZZ_LOSSY, fuzz_mutants, manifest, oracle_decode, oracle_vp8l_decode)
 
 pytestmark = pytest.mark.gpu
 
 
-def _mutants(seed=7, per_source=24):
-    rng = np.random.default_rng(seed)
-    out = []
-    srcs = [n for n in lossy_cases() if n != "alpha_64x48"]
-    srcs = sorted(srcs, key=lambda n: len(load_lossy(n)[0]))[:8]
-    for n in srcs:
-        d = bytearray(load_lossy(n)[0])
-        for _ in range(per_source):
-            m = bytearray(d)
-            for _ in range(int(rng.integers(1, 4))):
-                pos = int(rng.integers(40, len(m)))  # past the RIFF + VP8 frame headers
-                m[pos] ^= 1 << int(rng.integers(0, 8))
-            try:
-                info, mbs = webp_amd.vp8_parse(bytes(m))
-            except webp_amd.WebPError:
-                continue
-            out.append((bytes(m), info, mbs))
-    return out
+def _sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
 
 
 @pytest.mark.parametrize("emit", ["fused", "separate"])
-def test_mutated_streams_gpu_equals_oracle(emit):
+def test_mutated_lossy_streams_vs_libwebp_and_oracle(emit):
     if webp_amd.device_count() < 1:
         pytest.fail("no HIP device visible")
-    cases = _mutants()
-    assert len(cases) >= 40, len(cases)
+    cases = fuzz_mutants("lossy", *FUZZ_LOSSY)
+    want = manifest()["fuzz"]["lossy"]
     ctx = webp_amd.Context(0)
-    b = ctx.batch([c[0] for c in cases])
+    b = ctx.batch([d for _, d in cases])
     b.set_emit(emit == "separate")
     b.run()
-    checked = 0
-    for i, (_, info, mbs) in enumerate(cases):
-        if b.status[i] != 0:
+    decoded = 0
+    for i, (key, data) in enumerate(cases):
+        w = want[key]
+        assert int(b.status[i]) == w["status"], (key, int(b.status[i]), w["status"])
+        if w["status"] != 0:
             continue
+        rgba = b.rgba(i)
+        assert _sha(rgba) == w["rgba"], f"mutant {key}: GPU != libwebp"
+        info, mbs = webp_amd.vp8_parse(data)
         o = oracle_decode(info, mbs)
         y, u, v = b.yuv(i)
-        np.testing.assert_array_equal(y, o["y"], err_msg=f"mutant {i} Y")
-        np.testing.assert_array_equal(u, o["u"], err_msg=f"mutant {i} U")
-        np.testing.assert_array_equal(v, o["v"], err_msg=f"mutant {i} V")
-        np.testing.assert_array_equal(b.rgba(i), o["rgba"], err_msg=f"mutant {i} RGBA")
-        checked += 1
-    assert checked >= 40, checked
+        np.testing.assert_array_equal(y, o["y"], err_msg=f"mutant {key} Y")
+        np.testing.assert_array_equal(u, o["u"], err_msg=f"mutant {key} U")
+        np.testing.assert_array_equal(v, o["v"], err_msg=f"mutant {key} V")
+        np.testing.assert_array_equal(rgba, o["rgba"], err_msg=f"mutant {key} RGBA")
+        decoded += 1
+    assert decoded >= 100, decoded
     b.close()
     ctx.close()
 
 
-def test_mutated_lossless_streams_gpu_equals_oracle():
-    """The same for VP8L: bit-flipped lossless fixtures that still parse (other prefix codes,
-    transform data, palettes, cache bits) -> K3 (every kernel variant the mutants select)
-    == the oracle's inverse transforms, bit for bit."""
-    from oracle_lib import load_lossless, lossless_names, oracle_vp8l_decode
+def test_mutated_lossless_streams_vs_libwebp_and_oracle():
+    """The same for VP8L: other prefix codes, cache sizes, transform data and palettes ->
+    K7 (color cache + back-references) and K3 (every kernel variant the mutants select)."""
     if webp_amd.device_count() < 1:
         pytest.fail("no HIP device visible")
-    rng = np.random.default_rng(11)
-    cases = []
-    for n in sorted(lossless_names(), key=lambda n: len(load_lossless(n)[0]))[:10]:
-        d = bytearray(load_lossless(n)[0])
-        for _ in range(24):
-            m = bytearray(d)
-            for _ in range(int(rng.integers(1, 3))):
-                pos = int(rng.integers(25, len(m)))  # past the RIFF header and VP8L size fields
-                m[pos] ^= 1 << int(rng.integers(0, 8))
-            try:
-                info, argb, tdata = webp_amd.vp8l_parse(bytes(m))
-            except webp_amd.WebPError:
-                continue
-            cases.append((bytes(m), info, argb, tdata))
-    assert len(cases) >= 30, len(cases)
+    cases = fuzz_mutants("lossless", *FUZZ_LOSSLESS)
+    want = manifest()["fuzz"]["lossless"]
     ctx = webp_amd.Context(0)
-    b = ctx.batch([c[0] for c in cases])
+    b = ctx.batch([d for _, d in cases])
     b.run()
-    checked = 0
-    for i, (_, info, argb, tdata) in enumerate(cases):
-        if b.status[i] != 0:
+    decoded = 0
+    for i, (key, data) in enumerate(cases):
+        w = want[key]
+        assert int(b.status[i]) == w["status"], (key, int(b.status[i]), w["status"])
+        if w["status"] != 0:
             continue
-        np.testing.assert_array_equal(b.rgba(i), oracle_vp8l_decode(info, argb, tdata), err_msg=f"mutant {i}")
-        checked += 1
-    assert checked >= 30, checked
+        rgba = b.rgba(i)
+        assert _sha(rgba) == w["rgba"], f"mutant {key}: GPU != libwebp"
+        info, coded, tdata = webp_amd.vp8l_parse(data)
+        np.testing.assert_array_equal(rgba, oracle_vp8l_decode(info, coded, tdata), err_msg=f"mutant {key}")
+        decoded += 1
+    assert decoded >= 150, decoded
     b.close()
     ctx.close()

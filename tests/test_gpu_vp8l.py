@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 
 import webp_amd
-from oracle_lib import (GOLDEN, load_lossless, load_lossy, lossless_names, manifest, oracle_decode,
+from oracle_lib import (GOLDEN, bench_files, load_lossless, load_lossy, lossless_names, manifest, oracle_decode,
                         oracle_vp8l_decode)
 
 pytestmark = pytest.mark.gpu
@@ -30,21 +30,28 @@ def test_lossless_fixtures_batch_vs_golden_and_oracle(ctx):
     for n, d, img in zip(names, datas, imgs):
         gold = load_lossless(n)[1]["rgba"]
         np.testing.assert_array_equal(img, gold, err_msg=n)
-        info, argb, tdata = webp_amd.vp8l_parse(d)
-        np.testing.assert_array_equal(img, oracle_vp8l_decode(info, argb, tdata), err_msg=n)
+        info, coded, tdata = webp_amd.vp8l_parse(d)
+        np.testing.assert_array_equal(img, oracle_vp8l_decode(info, coded, tdata), err_msg=n)
 
 
-def test_c5_bench_frame_sha256(ctx):
-    data = open(os.path.join(GOLDEN, "bench", "c5_ll2048_s0.webp"), "rb").read()
-    b = ctx.batch([data] * 3)  # several workgroups on the same frame
+def test_c5_bench_frames_sha256(ctx):
+    """All 8 distinct C5 bitstreams (corr_luma seeds 0..7, the bench cycles them) through
+    K7 + K3, twice in one batch (several workgroups per frame), against libwebp's SHA-256."""
+    paths = bench_files("c5_ll2048")
+    assert len(paths) == 8
+    datas = [open(p, "rb").read() for p in paths]
+    b = ctx.batch(datas + datas[:3])
+    assert (b.status == 0).all(), b.status
     b.run()
-    want = manifest()["bench"]["c5_ll2048_s0.webp"]["sha256"]["rgba"]
-    for i in range(3):
-        assert hashlib.sha256(b.rgba(i).tobytes()).hexdigest() == want
+    m = manifest()["bench"]
+    want = [m[os.path.basename(p)]["sha256"]["rgba"] for p in paths]
+    want = want + want[:3]
+    for i in range(b.n):
+        assert hashlib.sha256(b.rgba(i).tobytes()).hexdigest() == want[i], i
     b.run()
-    assert hashlib.sha256(b.rgba(2).tobytes()).hexdigest() == want  # idempotent re-run
+    assert hashlib.sha256(b.rgba(2).tobytes()).hexdigest() == want[2]  # idempotent re-run
     ms = b.kernel_ms()
-    assert ms[0] == 0 and ms[1] == 0 and ms[2] > 0 and ms[3] == 0
+    assert ms[0] == 0 and ms[1] == 0 and ms[2] > 0 and ms[3] == 0 and ms[4] > 0 and ms[5] == 0  # K3, K7 only
     b.close()
 
 

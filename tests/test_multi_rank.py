@@ -95,7 +95,8 @@ def test_bench_spawns_one_rank_per_gpu(n):
     assert len({r["pid"] for r in ranks}) == n  # separate processes
     assert out["value"] > 0 and out["scaling"] == "weak"
     # every rank decoded 4 mock frames of 1000 px per step: value = n * 4000 * steps / max time
-    assert out["value"] == pytest.approx(n * 4000 * 3 / (out["ms_per_step"] * 3 * 1e-3) / 1e6, rel=0.01)
+    # (value is rounded to 0.1 MPix/s, ms_per_step to 1 us)
+    assert out["value"] == pytest.approx(n * 4000 * 3 / (out["ms_per_step"] * 3 * 1e-3) / 1e6, abs=0.1)
 
 
 def test_bench_under_external_launcher_env():

@@ -14,9 +14,9 @@ from oracle_lib import GOLDEN, lossless_names, load_lossless, manifest, oracle_v
 @pytest.mark.parametrize("name", lossless_names())
 def test_vp8l_oracle_matches_libwebp(name):
     data, gold = load_lossless(name)
-    info, argb, tdata = webp_amd.vp8l_parse(data)
+    info, coded, tdata = webp_amd.vp8l_parse(data)
     assert (info.width, info.height) == gold["rgba"].shape[1::-1]
-    rgba = oracle_vp8l_decode(info, argb, tdata)
+    rgba = oracle_vp8l_decode(info, coded, tdata)
     np.testing.assert_array_equal(rgba, gold["rgba"], err_msg=name)
 
 
@@ -33,14 +33,19 @@ def test_vp8l_fixtures_cover_every_transform():
     assert len(packing) >= 3, packing  # palette sizes exercising several pixel-packing widths
 
 
-def test_vp8l_c5_bench_frame_sha256():
-    path = os.path.join(GOLDEN, "bench", "c5_ll2048_s0.webp")
-    data = open(path, "rb").read()
-    info, argb, tdata = webp_amd.vp8l_parse(data)
-    assert (info.width, info.height) == (2048, 2048)
-    rgba = oracle_vp8l_decode(info, argb, tdata)
-    want = manifest()["bench"]["c5_ll2048_s0.webp"]["sha256"]["rgba"]
-    assert hashlib.sha256(rgba.tobytes()).hexdigest() == want
+def test_vp8l_c5_bench_frames_sha256():
+    """The oracle (color cache + copies + transforms) on all 8 committed C5 bitstreams vs
+    libwebp's SHA-256; the tokens hold no resolved pixel (the host leaves the cache to the
+    device)."""
+    m = manifest()["bench"]
+    for s in range(8):
+        data = open(os.path.join(GOLDEN, "bench", f"c5_ll2048_s{s}.webp"), "rb").read()
+        info, coded, tdata = webp_amd.vp8l_parse(data)
+        assert (info.width, info.height) == (2048, 2048) and coded.cache_bits == info.cache_bits > 0
+        kinds = np.bincount((coded.tokens.ravel() >> 30).astype(np.int64), minlength=4)
+        assert kinds[0] == len(coded.lits) and kinds[1] > kinds[0] and kinds[3] == 0
+        rgba = oracle_vp8l_decode(info, coded, tdata)
+        assert hashlib.sha256(rgba.tobytes()).hexdigest() == m[f"c5_ll2048_s{s}.webp"]["sha256"]["rgba"], s
 
 
 def test_vp8l_truncated_and_corrupt():
