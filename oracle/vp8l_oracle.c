@@ -5,8 +5,10 @@
  * TEST INFRASTRUCTURE ONLY: the checker for the device transform kernel (K3) and the
  * CPU baseline of the C5 workload.  Nothing in the product library links or calls it.
  *
- * Input is the host entropy stage's output (wg_vp8l_parse: the entropy-coded ARGB image
- * and the transforms in read order).  Pinning: libwebp 1.6.0 RGBA of the lossless
+ * Input is the host entropy stage's output (wg_vp8l_parse: one token per coded pixel, the
+ * literals, and the transforms in read order); oracle_vp8l_resolve first restates the value
+ * half of the symbol loop -- the color cache and the back-references -- serially, exactly as
+ * the reference orders it.  Pinning: libwebp 1.6.0 RGBA of the lossless
  * fixtures and the C5 bench frame's SHA-256 (tests/test_vp8l.py); the reference's own
  * VP8L decoder is an unimplemented stub (pkg/vp8/vp8l_dec.c.go DecodeImageStream).
  * Semantics follow (file:line in /root/reference/pkg/libwebp/dsp):
@@ -21,12 +23,45 @@
  *   VP8LInverseTransform (reverse order)                            lossless.go:511-547
  *   VP8LConvertBGRAToRGBA                                           lossless.go:561-573
  *   VP8LAddPixels                                                   lossless_common.go:110-114
+ * and (/root/reference/pkg/vp8):
+ *   DecodeImageData pixel loop: literal / CopyBlock32b / cache       vp8l_dec.c.go:1038-1189
+ *     (every decoded pixel inserted in scan order :1105-1109,
+ *      lookup :1141-1153)
+ *   VP8LHashPix (0x1e35a7bd), Insert, Lookup                         color_cache.go:16, 46-63
  */
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
 
 #include "../include/gowebp_amd.h"
+
+/* The coded image from its tokens (device_format.h kTok*: 0 literal index, 1 cache key, 2 copy
+ * distance, 3 unset): one pixel at a time, every pixel inserted into the color cache in scan
+ * order (a never-written slot reads as 0, calloc'd like VP8LColorCacheInit's).  Returns 0, or
+ * -1 for a token the host stage cannot produce. */
+int oracle_vp8l_resolve(const uint32_t* tokens, const uint32_t* lits, int n_lits, int n_px, int cache_bits,
+                        uint32_t* argb) {
+  uint32_t cache[2048];
+  memset(cache, 0, sizeof(cache));
+  if (cache_bits < 0 || cache_bits > 11) return -1;
+  for (int i = 0; i < n_px; ++i) {
+    const uint32_t t = tokens[i], kind = t >> 30, pl = t & 0x3fffffffu;
+    uint32_t v = 0;
+    if (kind == 0) {
+      if (pl >= (uint32_t)n_lits) return -1;
+      v = lits[pl];
+    } else if (kind == 1) {
+      if (pl >= (1u << cache_bits) || cache_bits == 0) return -1;
+      v = cache[pl];                                  /* VP8LColorCacheLookup */
+    } else if (kind == 2) {
+      if (pl == 0 || pl > (uint32_t)i) return -1;
+      v = argb[i - (int)pl];                          /* CopyBlock32b, one pixel at a time */
+    }
+    argb[i] = v;
+    if (kind != 3 && cache_bits) cache[(v * 0x1e35a7bdu) >> (32 - cache_bits)] = v;  /* Insert */
+  }
+  return 0;
+}
 
 static uint32_t add_pixels(uint32_t a, uint32_t b) {
   const uint32_t ag = (a & 0xff00ff00u) + (b & 0xff00ff00u);
