@@ -141,10 +141,10 @@ constexpr size_t kAlign = 256;
 inline size_t align_up(size_t v) { return (v + kAlign - 1) & ~(kAlign - 1); }
 
 // Kernels in launch order (stage) and in the public order of wg_batch_kernel_ms (K1, K2, K3,
-// K4, K7, K0): stage s runs between events ev[s] and ev[s + 1].
-constexpr int kStages = 6;
-constexpr int kStageK0 = 0, kStageK1 = 1, kStageK2 = 2, kStageK7 = 3, kStageK3 = 4, kStageK4 = 5;
-constexpr int kPublicOfStage[kStages] = {5, 0, 1, 4, 2, 3};
+// K4, K7): stage s runs between events ev[s] and ev[s + 1].
+constexpr int kStages = 5;
+constexpr int kStageK1 = 0, kStageK2 = 1, kStageK7 = 2, kStageK3 = 3, kStageK4 = 4;
+constexpr int kPublicOfStage[kStages] = {0, 1, 4, 2, 3};
 struct Timing {
   hipEvent_t ev[kStages + 1] = {};
   bool ran[kStages] = {};
@@ -182,8 +182,7 @@ struct wg_batch {
   int n_wide = 0;                          // lossy frames wider than that (global column store)
   int n_valid = 0;
   int64_t pixels = 0;
-  double kbytes[kStages] = {};  // public order: K1, K2, K3, K4, K7, K0
-  int max_mb_h = 1;
+  double kbytes[kStages] = {};  // public order: K1, K2, K3, K4, K7
   double k1_fused_bytes = 0;  // K1 with its RGBA tail: inputs + RGBA (planes are an intermediate)
   std::vector<Timing> timings;  // one per run since the last query
   size_t n_runs_pending = 0;
@@ -535,7 +534,7 @@ wg_batch* batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t* si
   b->in_bytes = std::max<size_t>(arena.layout(), kAlign);
   // layout of the planes / RGBA, and the algorithmic bytes per kernel
   size_t pl_b = 0, rg_b = 0;
-  double k0 = 0, k1 = 0, k2 = 0, k3 = 0, k4 = 0, k7 = 0;
+  double k1 = 0, k2 = 0, k3 = 0, k4 = 0, k7 = 0;
   for (int i = 0; i < n; ++i) {
     FrameParse& f = b->fp[(size_t)i];
     if (status) status[i] = f.status;
@@ -565,9 +564,6 @@ wg_batch* batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t* si
     b->n_lossy++;
     const wg_vp8_info& inf = f.info;
     const size_t nmb = (size_t)inf.mb_w * inf.mb_h;
-    b->max_mb_h = std::max(b->max_mb_h, inf.mb_h);
-    f.off_dcs = pl_b;  // K0's output: 16 int16 per MB
-    pl_b = align_up(pl_b + nmb * 32);
     f.off_y = pl_b;
     pl_b = align_up(pl_b + nmb * 256);
     f.off_u = pl_b;
@@ -596,7 +592,6 @@ wg_batch* batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t* si
     // algorithmic bytes: K1 reads records + row index + coefficient blocks, writes
     // MB-padded planes (or, with its RGBA tail, the RGBA); K2 reads cropped planes, writes RGBA.
     const double k1_in = (double)nmb * sizeof(MbRec) + inf.mb_h * 4.0 + (double)f.n_blocks * 32.0;
-    k0 += (double)nmb * sizeof(MbRec) + inf.mb_h * 4.0 + 64.0 * (double)f.n_y2;  // records, Y2 in, DCs out
     k1 += k1_in + nmb * 384.0;
     b->k1_fused_bytes += k1_in + 4.0 * inf.width * (double)inf.height;
     const double opx = (double)f.out_w * f.out_h;
@@ -631,7 +626,6 @@ wg_batch* batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t* si
   b->kbytes[2] = k3;
   b->kbytes[3] = k4;
   b->kbytes[4] = k7;
-  b->kbytes[5] = k0;
   b->plane_bytes = std::max<size_t>(pl_b, kAlign);
   b->rgba_bytes = std::max<size_t>(rg_b, kAlign);
   auto fail = [&](int st) {
@@ -672,7 +666,6 @@ wg_batch* batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t* si
     d.row_block0 = reinterpret_cast<const uint32_t*>(in + f.off_rows);
     d.blocks = reinterpret_cast<const int16_t*>(in + f.off_blocks);
     d.blocks_bytes = (int32_t)(f.n_blocks * 32);
-    d.dcs = reinterpret_cast<int16_t*>(b->d_planes + f.off_dcs);
     d.y = b->d_planes + f.off_y;
     d.cols = f.wide ? b->d_planes + f.off_cols : nullptr;
     d.u = b->d_planes + f.off_u;
@@ -781,15 +774,10 @@ int wg_batch_run(wg_batch* b, void* stream) {
     b->timings.push_back(t);
   }
   Timing& t = b->timings[b->n_runs_pending++];
-  t.ran[kStageK0] = t.ran[kStageK1] = b->n_lossy > 0;
+  t.ran[kStageK1] = b->n_lossy > 0;
   t.ran[kStageK2] = b->n_lossy > 0 && !b->fused;
   t.ran[kStageK7] = t.ran[kStageK3] = b->n_k3 > 0;
   t.ran[kStageK4] = b->n_alpha > 0;
-  hipEventRecord(t.ev[0], s);
-  if (b->n_lossy > 0) {  // K0: the i16 MBs' Y2 Walsh-Hadamard transforms
-    hipError_t e = wg::launch_vp8_y2(b->d_desc, b->n, b->max_mb_h, s);
-    if (e != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
-  }
   hipEventRecord(t.ev[kStageK1], s);
   if (b->n_lossy > 0) {
     hipError_t e = wg::launch_vp8_recon_filter(b->d_desc, b->n, b->max_mb_w, b->n_lossy > b->n_wide,

@@ -7,9 +7,6 @@
 
 namespace wg {
 
-// K0: the Y2 Walsh-Hadamard transform of every i16 MB into FrameDesc::dcs (before K1).
-hipError_t launch_vp8_y2(const FrameDesc* d_frames, int n_frames, int max_mb_h, hipStream_t stream);
-
 // K1: fused reconstruction + loop filter, one 1024-thread workgroup per frame.
 size_t vp8_recon_lds_bytes(int mb_w);
 int vp8_recon_max_mb_w();

@@ -243,33 +243,33 @@ __device__ __forceinline__ void idct_pass(int q, uint2 cv, int dadd, int r[4]) {
   }
 }
 
-// TransformWHT (dec.c.go:142-167; called from ParseResiduals, vp8_dec.go:615-634) of one
-// column-major Y2 block (cm[4c + r] = in[4r + c]) by one lane: the 16 Y DCs, int16 like
-// libwebp's, written as dcs[4*bx + by] (the layout K1's lanes read: block column bx holds the
-// DCs of its four rows).
-__device__ __forceinline__ void wht_lane(const int16_t* cm, int16_t* dcs) {
-  int tmp[16];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {  // column i of in[]
-    const int c0 = cm[4 * i + 0], c1 = cm[4 * i + 1], c2 = cm[4 * i + 2], c3 = cm[4 * i + 3];
+// TransformWHT (dec.c.go:142-167; called from ParseResiduals, vp8_dec.go:615-634) of the
+// MB's Y2 block, computed by every lane quad of the MB's 16 lanes: lane q holds column q of
+// Y2 (the same layout as the IDCT).  Vertical pass, quad transpose, horizontal pass: lane q
+// then holds row q of the 4x4 matrix of Y DCs (row = block row by, element = block column
+// bx), stored as int16 like libwebp's.  Lane (p, q), p = m >> 2, keeps element p, and the
+// quad broadcasts give every lane DC[by][p] for by = 0..3: its roles' luma blocks p + 4s
+// (row s) and p + 4s + 8 (row s + 2) read dc[s] and dc[s + 2].
+__device__ __forceinline__ void wht_quad(int p, uint2 cv, int dc[4]) {
+  const int c0 = (int16_t)(cv.x & 0xffff), c1 = (int16_t)(cv.x >> 16);
+  const int c2 = (int16_t)(cv.y & 0xffff), c3 = (int16_t)(cv.y >> 16);
+  int t[4];
+  {
     const int a0 = c0 + c3, a1 = c1 + c2, a2 = c1 - c2, a3 = c0 - c3;
-    tmp[0 + i] = a0 + a1;
-    tmp[8 + i] = a0 - a1;
-    tmp[4 + i] = a3 + a2;
-    tmp[12 + i] = a3 - a2;
+    t[0] = a0 + a1;  // tmp[0 + q]
+    t[1] = a3 + a2;  // tmp[4 + q]
+    t[2] = a0 - a1;  // tmp[8 + q]
+    t[3] = a3 - a2;  // tmp[12 + q]
   }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {  // row i: blocks (bx, by = i)
-    const int dc = tmp[0 + i * 4] + 3;
-    const int a0 = dc + tmp[3 + i * 4];
-    const int a1 = tmp[1 + i * 4] + tmp[2 + i * 4];
-    const int a2 = tmp[1 + i * 4] - tmp[2 + i * 4];
-    const int a3 = dc - tmp[3 + i * 4];
-    dcs[4 * 0 + i] = (int16_t)((a0 + a1) >> 3);
-    dcs[4 * 1 + i] = (int16_t)((a3 + a2) >> 3);
-    dcs[4 * 2 + i] = (int16_t)((a0 - a1) >> 3);
-    dcs[4 * 3 + i] = (int16_t)((a3 - a2) >> 3);
-  }
+  quad_transpose(t);  // lane q: t[c] = tmp[4q + c]
+  const int d0 = t[0] + 3;
+  const int a0 = d0 + t[3], a1 = t[1] + t[2], a2 = t[1] - t[2], a3 = d0 - t[3];
+  const int e = p == 0 ? a0 + a1 : p == 1 ? a3 + a2 : p == 2 ? a0 - a1 : a3 - a2;
+  const int v = (int16_t)(e >> 3);
+  dc[0] = __builtin_amdgcn_mov_dpp(v, 0x00, 0xF, 0xF, true);  // quad_perm [0,0,0,0]
+  dc[1] = __builtin_amdgcn_mov_dpp(v, 0x55, 0xF, 0xF, true);  // [1,1,1,1]
+  dc[2] = __builtin_amdgcn_mov_dpp(v, 0xAA, 0xF, 0xF, true);  // [2,2,2,2]
+  dc[3] = __builtin_amdgcn_mov_dpp(v, 0xFF, 0xF, 0xF, true);  // [3,3,3,3]
 }
 
 // clamp(a..d, 0, 255) packed little-endian into one dword with gfx950's v_ashr_pk_u8_i32
@@ -467,15 +467,6 @@ __device__ __forceinline__ uint2 ld_blockcol(__amdgpu_buffer_rsrc_t blks, bool n
   return make_uint2(v.x, v.y);
 }
 
-// The four Y DCs DC[0..3][bx] of MB `mb` (K0's output, FrameDesc::dcs); zeros when no Y2.
-__device__ __forceinline__ uint2 ld_dcs(__amdgpu_buffer_rsrc_t dcb, bool has, int mb, int bx) {
-#ifdef WG_ABL_NODC  // measurement only (output wrong): no DC load
-  return make_uint2(0, 0);
-#endif
-  const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(dcb, has ? mb * 32 + 8 * bx : (int)kDrop, 0, 0);
-  return make_uint2(v.x, v.y);
-}
-
 // The MB's blocks start at `blk`: its Y2 block first when kY2Bit is set, then the kept
 // Y / U / V blocks in order (device_format.h).
 __device__ __forceinline__ Coefs load_coefs(__amdgpu_buffer_rsrc_t blks, uint32_t flags, uint32_t blk, int b0, int cb,
@@ -540,44 +531,6 @@ __device__ __forceinline__ void emit_tail(const FrameDesc& F, uint32_t* progress
 
 }  // namespace
 
-// K0: the Y2 Walsh-Hadamard transform of every i16 MB (dec.c.go:142-167), ahead of K1: its
-// output is the 16 DCs K1 adds into the IDCT's second pass, so K1's reconstruction chain only
-// loads them.  Fully parallel: one wave per MB row, lane = MB; the MB's first block is the
-// row's first (row_block0) plus a wave prefix sum of the block counts to its left.
-__global__ void __launch_bounds__(256) vp8_y2_kernel(const FrameDesc* __restrict__ frames) {
-  const FrameDesc* F = frames + blockIdx.y;
-  if (!F->valid) return;
-  const int y = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int mb_w = F->mb_w;
-  if (y >= F->mb_h) return;
-  const MbRec* recs = F->mbs + (size_t)y * mb_w;
-  const int16_t* blocks = F->blocks;
-  int16_t* dcs = F->dcs + (size_t)y * mb_w * 16;
-  uint32_t blk = F->row_block0[y];
-  for (int x0 = 0; x0 < mb_w; x0 += 64) {
-    const int x = x0 + lane;
-    const uint32_t fl = x < mb_w ? recs[x].flags : 0u;
-    const uint32_t cnt = __builtin_popcount(fl & (kNzMask | kY2Bit));
-    uint32_t inc = cnt;  // inclusive prefix sum over the wave
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t t = __shfl_up(inc, d);
-      if (lane >= d) inc += t;
-    }
-    if (fl & kY2Bit) {
-      int16_t cm[16], out[16];
-      const uint4* src = reinterpret_cast<const uint4*>(blocks + 16 * (size_t)(blk + inc - cnt));
-      *reinterpret_cast<uint4*>(cm) = src[0];
-      *reinterpret_cast<uint4*>(cm + 8) = src[1];
-      wht_lane(cm, out);
-      uint4* dst = reinterpret_cast<uint4*>(dcs + 16 * (size_t)x);
-      dst[0] = *reinterpret_cast<const uint4*>(out);
-      dst[1] = *reinterpret_cast<const uint4*>(out + 8);
-    }
-    blk += __shfl(inc, 63);
-  }
-}
-
 // kGlobalCols: the per-MB-column store (kColBytes per column) lives in LDS when the frame's
 // columns fit next to the workspaces (mb_w <= vp8_recon_max_mb_w()), else in a per-frame
 // global buffer (FrameDesc::cols, wide frames up to VP8's 16383 px).  Each variant skips the
@@ -605,7 +558,6 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
       __builtin_amdgcn_make_buffer_rsrc(const_cast<MbRec*>(F->mbs), 0, mb_w * mb_h * 16, 0x00020000);
   const __amdgpu_buffer_rsrc_t blks =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<int16_t*>(F->blocks), 0, F->blocks_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t dcb = __builtin_amdgcn_make_buffer_rsrc(F->dcs, 0, mb_w * mb_h * 32, 0x00020000);
   // One buffer descriptor over the frame's planes: the batch allocates Y, U, V of a frame
   // back to back (capi.cpp), so U and V are 32-bit offsets from Y.
   const uint32_t uoff = (uint32_t)(F->u - F->y), voff = (uint32_t)(F->v - F->y);
@@ -656,9 +608,7 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
       const int r = (lane & 15) + 16 * s;
       cc[s] = load_coefs(blks, rc.flags, blk, r >> 2, 16 + (r >> 2), r & 3);
     }
-    // the DCs of the lane's luma blocks (K0's output, i16 MBs with Y2): 4 int16 = DC[by][bx]
-    // for bx = (lane & 15) >> 2, by = 0..3
-    uint2 y2c = ld_dcs(dcb, (rc.flags & kY2Bit) != 0, y * mb_w - 2 * g, (lane & 15) >> 2);
+    uint2 y2c = ld_blockcol(blks, (rc.flags & kY2Bit) != 0, blk, lane & 3);  // Y2 column (i16 MBs)
     // Retire the prologue loads here (visible to the waitcnt pass: 0x0F70 = vmcnt(0)), so the
     // loop header has no pending loads on cc/rc/rn and the in-loop uses of cc do not
     // conservatively drain the NEXT MB's prefetch with a vmcnt(0).
@@ -785,8 +735,8 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
 
       K1_SECT(3);
       // ---- residuals of all blocks (prediction-independent); i16 luma DCs from the Y2 WHT
-      // (MBs without Y2 read zeros: the load is dropped)
-      const int ydc[4] = {(int16_t)(y2c.x & 0xffff), (int)y2c.x >> 16, (int16_t)(y2c.y & 0xffff), (int)y2c.y >> 16};
+      int ydc[4] = {0, 0, 0, 0};
+      if (__any((fl & kY2Bit) != 0)) wht_quad(m >> 2, y2c, ydc);  // Y2 of i4 / no-Y2 MBs reads as 0: DCs 0
       int ry0[2][4], ry1[2][4], rcr[2][4];
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
@@ -808,7 +758,7 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
         const int r = m + 16 * s;
         cc[s] = load_coefs(blks, rn.flags, blk_next, r >> 2, 16 + (r >> 2), q);
       }
-      y2c = ld_dcs(dcb, (rn.flags & kY2Bit) != 0, y * mb_w + x + 1, m >> 2);
+      y2c = ld_blockcol(blks, (rn.flags & kY2Bit) != 0, blk_next, q);
       K1_SECT(4);
       // ---- luma prediction + residual (role r: block column (r>>2)&3, pixel rows
       //      4*((r>>2)>>2)+q and that + 8)
@@ -1140,11 +1090,6 @@ size_t vp8_recon_lds_bytes(int mb_w) {
 }
 
 int vp8_recon_max_mb_w() { return (int)((163840 - kHdrBytes - kMaxRecon * kRows * kSlotBytes) / kColBytes); }
-
-hipError_t launch_vp8_y2(const FrameDesc* d_frames, int n_frames, int max_mb_h, hipStream_t stream) {
-  hipLaunchKernelGGL(vp8_y2_kernel, dim3((max_mb_h + 3) / 4, n_frames), dim3(256), 0, stream, d_frames);
-  return hipGetLastError();
-}
 
 hipError_t launch_vp8_recon_filter(const FrameDesc* d_frames, int n_frames, int max_mb_w, bool lds_frames,
                                    bool wide_frames, int* d_err, hipStream_t stream) {

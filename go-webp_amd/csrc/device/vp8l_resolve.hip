@@ -29,13 +29,15 @@
 //      lands inside the block): (a) every pending lookup before the first pending copy (so
 //      every updater before it has a known hash) resolves: no in-block updater of its key
 //      before it -> the slot table as the previous block left it; else the last such updater
-//      (the last overall if it precedes the lookup, else a walk of the key's list for the
-//      largest index below it); (b) every pending copy whose source is known takes its value
+//      (the last overall if it precedes the lookup; else, when every in-block updater of the
+//      key has one value -- runs of one color copied over and over -- that value; else a walk
+//      of the key's list for the largest index below it); (b) every pending copy whose source is known takes its value
 //      and registers as an updater, the others jump their source pointer one link further
 //      back along a chain of pending copies (pointer jumping: log-depth chains).  The earliest
 //      pending pixel always resolves, so the rounds end; a cap sends the block to the serial
 //      path.  Values leave as 16-byte stores.
-//   3. the slot table takes each hash's last in-block updater.
+//   3. the slot table takes each hash's last in-block updater, which also resets the hash's
+//      value range for the next block.
 // A block with a lookup of a never-written slot k != 0, a list walk over 64 entries, or more
 // than kMaxRounds rounds is redone exactly in scan order by one lane (the reference loop over
 // the same LDS table, literal and far-copy values already in LDS): always correct, slow, and
@@ -83,6 +85,7 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
   __shared__ int32_t head[kSlots];             // position of the last in-block updater of a hash
   __shared__ uint32_t first_tag[kSlots];       // tag | (kBlock - 1 - local) of the first one (max)
   __shared__ uint32_t list_tag[kSlots];        // tag | local of the most recently linked one
+  __shared__ uint32_t umin[kSlots], umax[kSlots];  // value range of the block's updaters per hash
   __shared__ int16_t nxt[kBlock];              // per updater: the previously linked one, -1 none
   __shared__ int16_t ref[kBlock];              // pending copy: source pointer (pointer jumping)
   __shared__ uint8_t st[kBlock];               // kKnown / kPendCopy / kPendLookup
@@ -104,6 +107,8 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
     head[i] = -1;
     first_tag[i] = 0;
     list_tag[i] = 0;
+    umin[i] = 0xffffffffu;
+    umax[i] = 0;
   }
   if (tid < kSlots / 32) slot_set[tid] = 0;
   if (tid < 2) slow[tid] = 0;
@@ -129,6 +134,8 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
       const uint32_t h = hash_px(v, shift);
       atomicMax(&head[h], base + li);
       atomicMax(&first_tag[h], tag | (uint32_t)(kBlock - 1 - li));
+      atomicMin(&umin[h], v);
+      atomicMax(&umax[h], v);
       const uint32_t prev = atomicExch(&list_tag[h], tag | (uint32_t)li);
       nxt[li] = (prev & ~(uint32_t)(kBlock - 1)) == tag ? (int16_t)(prev & (kBlock - 1)) : (int16_t)-1;
     };
@@ -231,8 +238,11 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
           x = sv[j];
         } else {
           const int last = hd[j] - base;
+          const uint32_t lo = umin[k];
           if (last < li) {
             x = val[last];
+          } else if (lo == umax[k]) {
+            x = lo;
           } else {
             int best = -1, cur = (int)(list_tag[k] & (kBlock - 1)), steps = 0;
             while (cur >= 0 && steps < kMaxWalk) {
@@ -326,14 +336,23 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
           coded[pos] = x;
         }
       }
-    } else if (cache_bits) {
+      __syncthreads();
+    }
+    if (cache_bits) {
+      // each hash's last registered updater (every hash with one has one) resets its value
+      // range; on the fast path it also writes the slot
+      const bool fast = !*slow_b;
 #pragma unroll
       for (int j = 0; j < kPer; ++j) {
         if (!upd[j]) continue;
         const uint32_t h = hash_px(v[j], shift);
         if (head[h] == base + li0 + j) {
-          slot_val[h] = v[j];
-          atomicOr(&slot_set[h >> 5], 1u << (h & 31));
+          umin[h] = 0xffffffffu;
+          umax[h] = 0;
+          if (fast) {
+            slot_val[h] = v[j];
+            atomicOr(&slot_set[h >> 5], 1u << (h & 31));
+          }
         }
       }
     }

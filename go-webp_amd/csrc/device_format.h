@@ -12,8 +12,6 @@
 //                              U 16..19, V 20..23; stored column-major
 //                              (blocks[4*c + k] = coeff[4*k + c]) so lane c of the
 //                              IDCT / WHT reads its column with one load
-//   dcs[mb_h][mb_w][16]        K0's Walsh-Hadamard output for i16 MBs with a Y2 block: the
-//                              16 Y DCs, stored dcs[4*bx + by] = DC of Y block (bx, by)
 //   Y/U/V planes               16*mb_w x 16*mb_h and 8*mb_w x 8*mb_h (MB padded)
 //   RGBA                       width x height x 4
 #pragma once
@@ -66,8 +64,7 @@ struct FrameDesc {
   int32_t width, height, mb_w, mb_h;
   int32_t y_stride, uv_stride, rgba_stride, filter_type;
   int32_t flags, valid, blocks_bytes, pad2;  // blocks_bytes: size of `blocks` (K1 bounds)
-  int16_t* dcs;     // K0's output: per MB 16 int16 Y DCs of its Y2 block (mb_w * mb_h * 32 B)
-  int32_t pad3[2];
+  int32_t pad3[4];
 };
 static_assert(sizeof(FrameDesc) == 128, "FrameDesc must be 128 bytes");
 

@@ -397,17 +397,17 @@ class Batch:
             raise WebPError(st, "wg_batch_run_emit")
 
     def kernel_ms(self):
-        """(K1, K2, K3, K4, K7, K0) per-launch ms averaged over the runs since the last call."""
-        ms = (C.c_float * 6)()
-        st = lib().wg_batch_kernel_ms(self._h, ms, 6)
+        """(K1, K2, K3, K4, K7) per-launch ms averaged over the runs since the last call."""
+        ms = (C.c_float * 5)()
+        st = lib().wg_batch_kernel_ms(self._h, ms, 5)
         if st != Status.OK:
             raise WebPError(st, "wg_batch_kernel_ms")
         return tuple(float(v) for v in ms)
 
     def kernel_bytes(self):
-        """Algorithmic HBM bytes per launch of (K1, K2, K3, K4, K7, K0)."""
-        b = (C.c_double * 6)()
-        lib().wg_batch_kernel_bytes(self._h, b, 6)
+        """Algorithmic HBM bytes per launch of (K1, K2, K3, K4, K7)."""
+        b = (C.c_double * 5)()
+        lib().wg_batch_kernel_bytes(self._h, b, 5)
         return tuple(float(v) for v in b)
 
     @property

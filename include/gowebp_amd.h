@@ -176,12 +176,11 @@ int wg_batch_run_emit(wg_batch* b, void* stream);
 /* Per-launch kernel durations averaged over the runs since the last query:
  * ms[0] = VP8 reconstruct+filter (K1, with its RGBA tail by default), ms[1] = YUV->RGBA (K2), ms[2] = VP8L inverse
  * transforms (K3, lossless frames and lossless ALPH streams), ms[3] = ALPH unfilter + A
- * channel (K4), ms[4] = VP8L color cache + back-references (K7, before K3), ms[5] = the Y2
- * Walsh-Hadamard transforms of the i16 macroblocks (K0, before K1); a kernel with no frames in
- * the batch reports 0.  n_ms >= 1 (entries beyond n_ms are not written). */
+ * channel (K4), ms[4] = VP8L color cache + back-references (K7, before K3); a kernel with no
+ * frames in the batch reports 0.  n_ms >= 1 (entries beyond n_ms are not written). */
 int wg_batch_kernel_ms(const wg_batch* b, float* ms, int n_ms);
 
-/* Algorithmic HBM bytes per launch of K1, K2, K3, K4, K7, K0; K1 with
+/* Algorithmic HBM bytes per launch of K1, K2, K3, K4, K7; K1 with
  * its RGBA tail: records + coefficients in, RGBA out (the planes are an intermediate). */
 int wg_batch_kernel_bytes(const wg_batch* b, double* bytes, int n_bytes);
 
