@@ -813,7 +813,7 @@ int wg_batch_run(wg_batch* b, void* stream) {
   }
   hipEventRecord(t.ev[kStageK7], s);
   if (b->n_k3 > 0) {  // K7: the lossless streams' color cache and back-references
-    hipError_t e = wg::launch_vp8l_resolve(b->d_tokdesc, (int)b->tokdesc.size(), b->d_err, s);
+    hipError_t e = wg::launch_vp8l_resolve(b->d_tokdesc, nullptr, (int)b->tokdesc.size(), b->d_err, s);
     if (e != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
   }
   hipEventRecord(t.ev[kStageK3], s);
@@ -1301,4 +1301,22 @@ int wg_yuv420_to_rgba_device(const uint8_t* y, const uint8_t* u, const uint8_t* 
   return e == hipSuccess ? WG_STATUS_OK : WG_STATUS_INVALID_PARAM;
 }
 
+int wg_vp8l_resolve_device(const uint32_t* tokens, const uint32_t* lits, int n_lits, int n_px, int cache_bits,
+                           uint32_t* argb, void* stream) {
+  if (!tokens || !argb || n_px <= 0 || n_lits < 0 || (n_lits > 0 && !lits) || cache_bits < 0 || cache_bits > 11 ||
+      (reinterpret_cast<uintptr_t>(tokens) & 15) || (reinterpret_cast<uintptr_t>(argb) & 15))
+    return WG_STATUS_INVALID_PARAM;
+  wg::LLTokDesc t{};
+  t.tokens = tokens;
+  t.lits = lits;
+  t.coded = argb;
+  t.n_px = n_px;
+  t.n_lits = n_lits;
+  t.cache_bits = cache_bits;
+  t.valid = 1;
+  const hipError_t e = wg::launch_vp8l_resolve(nullptr, &t, 1, nullptr, reinterpret_cast<hipStream_t>(stream));
+  return e == hipSuccess ? WG_STATUS_OK : WG_STATUS_INVALID_PARAM;
+}
+
 }  // extern "C"
+

@@ -30,7 +30,9 @@ hipError_t launch_vp8l_transforms(const LLDesc* d_frames, const int* group_count
 
 // K7: VP8L color cache + back-references (tokens -> coded ARGB), one 1024-thread workgroup per
 // lossless stream; runs before K3.  d_err: OR-ed with 4 on an invalid token.
-hipError_t launch_vp8l_resolve(const LLTokDesc* d_descs, int n, int* d_err, hipStream_t stream);
+// d_descs null: the single stream `single` (stage entry)
+hipError_t launch_vp8l_resolve(const LLTokDesc* d_descs, const LLTokDesc* single, int n, int* d_err,
+                               hipStream_t stream);
 
 // K4: ALPH planes (unfilter) -> A bytes of the RGBA output, one 1024-thread workgroup per
 // plane; runs after K2 and K3.

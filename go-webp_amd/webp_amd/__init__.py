@@ -19,7 +19,7 @@ import numpy as np
 __all__ = [
     "Status", "WebPError", "FLAG_BYPASS_FILTERING", "FLAG_NO_FANCY_UPSAMPLING", "Features",
     "lib", "features", "decode_config", "decode", "Context", "Batch", "vp8_parse", "vp8l_parse", "MB_DTYPE",
-    "VP8Info", "VP8LInfo", "VP8LCoded", "device_count", "yuv420_to_rgba_device", "MultiContext", "set_default_device",
+    "VP8Info", "VP8LInfo", "VP8LCoded", "device_count", "yuv420_to_rgba_device", "vp8l_resolve_device", "MultiContext", "set_default_device",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -168,6 +168,7 @@ _SIGS = {
     "wg_anim_decode": (C.c_int, [_P, _P, C.c_size_t, _P, _P, C.c_int32]),
     "wg_decode_status": (C.c_int, [_P, C.c_size_t, _P]),
     "wg_set_default_device": (C.c_int, [C.c_int]),
+    "wg_vp8l_resolve_device": (C.c_int, [_P, _P, C.c_int, C.c_int, C.c_int, _P, _P]),
     "wg_decode_rgba_batch_multi": (C.c_int, [_P, C.c_int, _P, _P, C.c_int, _P, _P, _P, C.c_int32]),
 }
 EXPORTED = tuple(_SIGS)
@@ -577,3 +578,11 @@ def yuv420_to_rgba_device(y_ptr, u_ptr, v_ptr, y_stride, uv_stride, rgba_ptr, rg
                                         width, height, 1 if fancy else 0, stream)
     if st != Status.OK:
         raise WebPError(st, "wg_yuv420_to_rgba_device")
+
+
+def vp8l_resolve_device(tokens_ptr, lits_ptr, n_lits, n_px, cache_bits, argb_ptr, stream=None):
+    """Stage entry point on device pointers (ints): the color cache + back-references of one
+    VP8L token stream (the tokens of webp_amd.vp8l_parse's VP8LCoded) -> n_px coded ARGB words."""
+    st = lib().wg_vp8l_resolve_device(tokens_ptr, lits_ptr, n_lits, n_px, cache_bits, argb_ptr, stream)
+    if st != Status.OK:
+        raise WebPError(st, "wg_vp8l_resolve_device")

@@ -208,6 +208,18 @@ int wg_yuv420_to_rgba_device(const uint8_t* y, const uint8_t* u, const uint8_t* 
                              int y_stride, int uv_stride, uint8_t* rgba, int rgba_stride,
                              int width, int height, int fancy, void* stream);
 
+/* ---- stage entry point: VP8L color cache + back-references on device pointers -------- */
+/* The value half of DecodeImageData's pixel loop (pkg/vp8/vp8l_dec.c.go:1038-1189; cache
+ * pkg/vp8/color_cache.go:46-63) on one token stream, the form the host entropy stage hands K7
+ * (one uint32 per pixel: kind in bits 31:30 -- 0 literal index into `lits`, 1 color-cache key,
+ * 2 backward distance, 3 unset = 0 without a cache insert -- payload in bits 29:0).  Writes
+ * the n_px coded ARGB pixels to `argb`.  Device pointers; tokens and argb 16-byte aligned;
+ * cache_bits 0..11.  A token outside the stream's bounds (literal index >= n_lits, key >=
+ * 1 << cache_bits, distance 0 or before the start) resolves to 0.  Asynchronous on `stream`.
+ * Anything else -> WG_STATUS_INVALID_PARAM. */
+int wg_vp8l_resolve_device(const uint32_t* tokens, const uint32_t* lits, int n_lits, int n_px,
+                           int cache_bits, uint32_t* argb, void* stream);
+
 /* ---- host entropy stage in the libwebp data model (tests / CPU checker) --------------- */
 /* One macroblock as libwebp keeps it after parsing: VP8MBData (pkg/vp8/models.go:89-107)
  * plus the VP8FInfo filter strengths (models.go:66-71). */

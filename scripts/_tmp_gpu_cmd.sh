@@ -1,5 +1,17 @@
+#!/bin/bash
+# K7 rewrite check: stage-entry parity, the lossless batch tests, K7 statistics, c5 bench.
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 240 python -u scripts/k7_stats.py 32 > gpurun_out/k7_stats.log 2>&1; rc=$?
-cat gpurun_out/k7_stats.log; exit $rc
+step() {  # step <name> <timeout_s> <cmd...>
+  local name=$1 to=$2; shift 2
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc"
+  tail -n ${TAILN:-6} "gpurun_out/$name.log"
+  if [ $rc -ne 0 ]; then echo "STOP: $name rc=$rc"; exit $rc; fi
+}
+step k7_tests 300 python -u -m pytest tests/test_gpu_k7.py tests/test_gpu_vp8l.py tests/test_gpu_fuzz.py -x -v --timeout 200 --timeout-method thread -p no:cacheprovider
+step k7_stats 200 python -u scripts/k7_stats.py 32
+step bench_c5 300 python bench.py --workload c5 --steps 10 --warmup 3 --no-cpu-baseline --no-e2e

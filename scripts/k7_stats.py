@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """K7 (vp8l_resolve.hip) block statistics from the measurement build (make VARIANT=timing,
 WG_LIB_VARIANT=timing): blocks, blocks redone serially, rounds, and wave 0's cycles per phase
-(1 = tokens/literals/far copies, 2 = rounds, 3 = stores, 4 = slot table) for one c5 batch."""
+(tokens + ranks, windows, serial path, stores) for one c5 batch."""
 import ctypes as C
 import os
 import sys
@@ -27,13 +27,14 @@ def main():
     b.run()
     ms = b.kernel_ms()
     L.wg_debug_k7_stats(st, 1)
-    blocks, slow, rounds = st[0], st[1], st[2]
-    tot = sum(st[3:7])
-    print(f"frames {n}: K7 {ms[4]:.3f} ms; blocks {blocks}, serial {slow} ({slow / blocks:.4f}), "
-          f"rounds/block {rounds / blocks:.2f}")
-    for i, name in zip(range(3, 7), ("tokens+literals+far copies", "rounds", "stores", "slot table")):
-        print(f"  {name:28s} {st[i] / blocks:10.0f} cycles/block  {st[i] / tot:.3f}")
-    print(f"  serial causes (events): bad token {st[7]}, empty slot {st[8]}, long walk {st[9]}, round cap {st[10]}")
+    blocks, serial, rounds, windows = st[0], st[1], st[2], st[3]
+    tot = sum(st[4:8])
+    print(f"frames {n}: K7 {ms[4]:.3f} ms; blocks {blocks}, windows/block {windows / blocks:.3f}, "
+          f"rounds/window {rounds / max(windows, 1):.3f}, serial windows {serial}")
+    for i, name in zip(range(4, 8), ("tokens + ranks", "windows (register, rounds, table)", "serial path",
+                                     "store + pipeline")):
+        print(f"  {name:36s} {st[i] / blocks:10.0f} cycles/block  {st[i] / max(tot, 1):.3f}")
+    print(f"  serial causes (events): empty slot {st[9]}, round cap {st[10]}")
     b.close()
     ctx.close()
 

@@ -1,0 +1,117 @@
+"""Synthetic VP8L token streams for K7 (vp8l_resolve.hip) parity tests.
+
+A token stream is what the host entropy stage hands K7 (device_format.h kTok*): one uint32 per
+pixel, kind in bits 31:30 (0 literal index, 1 color-cache key, 2 backward distance, 3 unset)
+and the payload in bits 29:0, plus the literal ARGB values.  The streams are generated the way
+an encoder would emit them -- every lookup names a key whose slot holds a value, unless a case
+asks for lookups of never-written slots -- by running the reference's pixel loop
+(pkg/vp8/vp8l_dec.c.go:1038-1189, color_cache.go:46-63) alongside, so each case can aim at one
+of K7's paths: windows (more updaters per block than the rank masks hold), in-block copy chains
+(pointer jumping), copies reaching back more than one block, the serial fallback (empty slots,
+the round cap).  The expected output is always the oracle's (oracle_vp8l_resolve), not this
+generator's.
+"""
+import numpy as np
+
+HASH_MUL = 0x1E35A7BD
+LIT, CACHE, COPY, UNSET = 0, 1, 2, 3
+
+
+def hash_px(v, bits):
+    return ((v * HASH_MUL) & 0xFFFFFFFF) >> (32 - bits)
+
+
+def make_stream(n, bits, seed, p_lit=0.035, p_copy=0.0, dist=(1,), palette=256, width=2048, run=1,
+                p_empty=0.0, chain=False):
+    """-> (tokens uint32[n], lits uint32[]).  p_lit / p_copy: probabilities of a literal / a copy
+    run (length 1..run, distances drawn from `dist`: ints, or "w" (the row above), "near"
+    (1..64), "far" (4096..20000)); the rest are cache lookups of keys whose slot holds a value
+    (p_empty of them of a never-written slot instead).  chain: alternate one-pixel copies of
+    distance 1 and lookups (each copy's source is a lookup: one round per pair)."""
+    rng = np.random.default_rng(seed)
+    pal = rng.integers(0, 1 << 32, size=palette, dtype=np.uint64).astype(np.uint32)
+    pal[0] = 0
+    nk = 1 << bits if bits else 0
+    cache = [0] * max(nk, 1)
+    written = set()
+    vals = []
+    toks = np.empty(n, np.uint32)
+    lits = []
+    keys = []  # written keys, for lookups
+
+    def insert(v):
+        if nk:
+            h = hash_px(v, bits)
+            if h not in written:
+                written.add(h)
+                keys.append(h)
+            cache[h] = v
+
+    i = 0
+    while i < n:
+        r = rng.random()
+        if chain and i > 0 and keys:
+            if i % 2:
+                toks[i] = (COPY << 30) | 1
+                v = vals[i - 1]
+            else:
+                k = keys[int(rng.integers(len(keys)))]
+                toks[i] = (CACHE << 30) | k
+                v = cache[k]
+            vals.append(v)
+            insert(v)
+            i += 1
+            continue
+        if i == 0 or r < p_lit or (nk and not keys and r >= p_lit + p_copy):
+            v = int(pal[int(rng.integers(palette))])
+            toks[i] = (LIT << 30) | len(lits)
+            lits.append(v)
+            vals.append(v)
+            insert(v)
+            i += 1
+        elif r < p_lit + p_copy or not nk:
+            d = dist[int(rng.integers(len(dist)))]
+            if d == "w":
+                d = width
+            elif d == "near":
+                d = int(rng.integers(1, 65))
+            elif d == "far":
+                d = int(rng.integers(4096, 20001))
+            d = min(int(d), i)
+            ln = int(rng.integers(1, run + 1))
+            for _ in range(min(ln, n - i)):
+                toks[i] = (COPY << 30) | d
+                v = vals[i - d]
+                vals.append(v)
+                insert(v)
+                i += 1
+        else:
+            if p_empty and rng.random() < p_empty and nk > 1:
+                k = int(rng.integers(1, nk))
+                while k in written and len(written) < nk - 1:
+                    k = int(rng.integers(1, nk))
+            else:
+                k = keys[int(rng.integers(len(keys)))]
+            toks[i] = (CACHE << 30) | k
+            v = cache[k]
+            vals.append(v)
+            insert(v)
+            i += 1
+    return toks, np.asarray(lits if lits else [0], np.uint32)
+
+
+# (name, n_px, cache_bits, kwargs): each aims at one path of K7
+CASES = [
+    ("c5like", 3 * 4096 + 123, 10, dict(p_lit=0.035, palette=300)),
+    ("windows_b11", 2 * 4096 + 7, 11, dict(p_lit=0.45, p_copy=0.15, dist=(1, "near"), palette=4000)),
+    ("windows_b8", 2 * 4096, 8, dict(p_lit=0.7, palette=2000)),
+    ("copy_runs", 3 * 4096 + 1, 8, dict(p_lit=0.05, p_copy=0.3, dist=(1, "w", "near"), run=300, width=1000)),
+    ("copy_far", 6 * 4096 + 5, 10, dict(p_lit=0.05, p_copy=0.3, dist=("far", 4096, 4097, 8191, 8192), run=20)),
+    ("no_cache", 2 * 4096 + 9, 0, dict(p_lit=0.4, p_copy=0.6, dist=(1, 3, "near", "far"), run=50)),
+    ("empty_slots", 4096 + 100, 6, dict(p_lit=0.05, p_empty=0.01, palette=40)),
+    ("round_cap", 4096 + 64, 9, dict(chain=True, palette=64)),
+    ("one_px", 1, 10, dict()),
+    ("three_px", 3, 4, dict()),
+    ("block_edge", 4097, 10, dict(p_lit=0.2, p_copy=0.2, dist=(1, "near"), run=8)),
+    ("b1", 4096 + 33, 1, dict(p_lit=0.3, palette=8)),
+]

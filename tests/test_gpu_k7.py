@@ -1,0 +1,63 @@
+"""K7 (color cache + back-references, vp8l_resolve.hip) through its stage entry
+wg_vp8l_resolve_device, bit-exact against the oracle's restatement of the reference's pixel
+loop (oracle_vp8l_resolve: pkg/vp8/vp8l_dec.c.go:1038-1189, color_cache.go:46-63) on synthetic
+token streams aimed at each of K7's paths (tests/k7_streams.py) and on the C5 bench streams'
+real tokens.  (The batch path -- host entropy stage -> K7 -> K3 -- is covered against libwebp
+by test_gpu_vp8l.py and test_gpu_fuzz.py.)"""
+import os
+import zlib
+
+import numpy as np
+import pytest
+
+import k7_streams
+from oracle_lib import oracle
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def oracle_resolve(toks, lits, bits):
+    out = np.empty(toks.size, np.uint32)
+    assert oracle().oracle_vp8l_resolve(toks.ctypes.data, lits.ctypes.data, lits.size, toks.size, bits,
+                                        out.ctypes.data) == 0
+    return out
+
+
+def device_resolve(toks, lits, bits):
+    import torch
+    import webp_amd
+    dt = torch.from_numpy(toks.view(np.int32)).cuda()
+    dl = torch.from_numpy(lits.view(np.int32)).cuda()
+    out = torch.full((toks.size,), -1, dtype=torch.int32, device="cuda")
+    webp_amd.vp8l_resolve_device(dt.data_ptr(), dl.data_ptr(), lits.size, toks.size, bits, out.data_ptr(),
+                                 torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    return out.cpu().numpy().view(np.uint32)
+
+
+@pytest.mark.parametrize("name,n,bits,kw", k7_streams.CASES, ids=[c[0] for c in k7_streams.CASES])
+def test_k7_synthetic_streams(name, n, bits, kw):
+    toks, lits = k7_streams.make_stream(n, bits, seed=zlib.crc32(name.encode()), **kw)
+    want = oracle_resolve(toks, lits, bits)
+    got = device_resolve(toks, lits, bits)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, f"{name}: {bad.size} pixels differ, first at {bad[:5]}"
+
+
+def test_k7_c5_streams():
+    import webp_amd
+    for s in range(8):
+        path = os.path.join(ROOT, "tests", "golden", "bench", f"c5_ll2048_s{s}.webp")
+        info, coded, _ = webp_amd.vp8l_parse(open(path, "rb").read())
+        toks = np.ascontiguousarray(coded.tokens, np.uint32).ravel()
+        lits = np.ascontiguousarray(coded.lits, np.uint32)
+        want = oracle_resolve(toks, lits, coded.cache_bits)
+        got = device_resolve(toks, lits, coded.cache_bits)
+        assert np.array_equal(got, want), f"s{s}: {(got != want).sum()} pixels differ"
+
+
+def test_k7_rejects_bad_params():
+    import webp_amd
+    with pytest.raises(webp_amd.WebPError):
+        webp_amd.vp8l_resolve_device(0, 0, 0, 16, 4, 0)
