@@ -63,7 +63,7 @@ constexpr int kSlots = 2048;              // 1 << MAX_CACHE_BITS (format_constan
 constexpr int kMaskWords = 8192;          // 64 KB of 64-bit rank masks, split over the keys
 constexpr int kMaxW = 32;                 // mask words per key (the summary is 32 bits)
 constexpr int kMaxRounds = 32;
-constexpr uint8_t kKnown = 1, kPendCopy = 2, kPendLookup = 3, kPendFar = 4;
+constexpr uint8_t kKnown = 1, kPendCopy = 2, kPendLookup = 3;
 constexpr uint32_t kDropOff = 0xffffffc0u;  // buffer offset past any stream: loads return 0
 
 __device__ __forceinline__ uint32_t hash_px(uint32_t v, int shift) { return (v * 0x1e35a7bdu) >> shift; }
@@ -78,12 +78,14 @@ __device__ __forceinline__ int count_below(uint64_t m) {
 // Measurement build only (make VARIANT=timing): block / window / round counts and wave 0's
 // cycles per phase.
 #ifdef WG_K7_STATS
-// blocks, serial windows, rounds, windows, t_phase1, t_windows, t_serial, t_store,
-// serial because: bad token, empty slot, round cap; lookups
-__device__ unsigned long long g_k7_stats[12];
+// counts: 0 blocks, 1 serial windows, 2 rounds, 3 windows, 9 empty-slot lookups, 10 round caps;
+// wave 0's cycles: 14 tokens (waits for the prefetched loads), 4 ranks + barrier, 11 registration, 12 lookups, 5 copies (rounds b), 13 slot
+// table, 6 serial path, 7 stores + pipeline
+__device__ unsigned long long g_k7_stats[16];
+__device__ unsigned long long g_k7_wave[kWaves][16];  // per wave (lane 0): the same phase cycles
 #define K7_T(i)                                                      \
   do {                                                               \
-    if (tid == 0) {                                                  \
+    if ((tid & 63) == 0) {                                           \
       const uint64_t t_ = __builtin_amdgcn_s_memtime();              \
       k7_acc[i] += t_ - k7_t;                                        \
       k7_t = t_;                                                     \
@@ -107,8 +109,9 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
                                                             int* err) {
   __shared__ uint64_t mask[kMaskWords];          // per key k: words k*W .. k*W+W-1, bit = rank in window
   __shared__ uint32_t summ[kSlots];              // per key: mask words holding a bit
-  __shared__ uint32_t last_rank[kSlots];         // per key: 1 + the window's last updater rank (0 none)
-  __shared__ uint32_t slot_val[kSlots];          // the color cache (VP8LColorCache.colors_)
+  // per key: x = 1 + the window's last updater rank (0 none), y = the slot (VP8LColorCache.colors_):
+  // one 8-byte read gives a lookup both
+  __shared__ uint2 slotrec[kSlots];
   __shared__ uint32_t slot_set[kSlots / 32];     // slot written at least once
   __shared__ __attribute__((aligned(16))) uint32_t uval[kBlock];    // window updater values by rank
                                                                      // (serial path: the block's tokens)
@@ -138,9 +141,8 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
   const __amdgpu_buffer_rsrc_t out_rs = __builtin_amdgcn_make_buffer_rsrc(D.coded, 0, 4 * n, 0x00020000);
   for (int i = tid; i < kMaskWords; i += kThreads) mask[i] = 0;
   for (int i = tid; i < kSlots; i += kThreads) {
-    slot_val[i] = 0;
+    slotrec[i] = make_uint2(0u, 0u);
     summ[i] = 0;
-    last_rank[i] = 0;
   }
   if (tid < kSlots / 32) slot_set[tid] = 0;
   if (tid == 0) {
@@ -178,174 +180,254 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
       lv[j] = __builtin_amdgcn_raw_buffer_load_b32(lit_rs, is_lit ? 4u * (tk[j] & kTokPayload) : kDropOff, 0, 0);
     }
   };
-  // software pipeline: tokens two blocks ahead, literal values one block ahead
-  uint32_t tk[kPer], lv[kPer], tk1[kPer], lv1[kPer], tk2[kPer];
-  load_tokens(0, tk);
-  load_tokens(1, tk1);
-  load_lits(tk, lv);
+  // Software pipeline: tokens two blocks ahead, literal values one block ahead.  Two register
+  // sets (A for even blocks, B for odd), the block body inlined once per set: rotating one set
+  // through copies at the loop latch would make every copy wait for its load (a register with
+  // a load in flight cannot be read), collapsing the prefetch distance to nothing.
+  uint32_t tkA[kPer], lvA[kPer], tkB[kPer], lvB[kPer];
+  load_tokens(0, tkA);
+  load_tokens(1, tkB);
+  load_lits(tkA, lvA);
   __syncthreads();
 #ifdef WG_K7_STATS
-  uint64_t k7_acc[8] = {}, k7_t = __builtin_amdgcn_s_memtime();
-  unsigned long long k7_cnt[12] = {};
+  uint64_t k7_acc[16] = {}, k7_t = __builtin_amdgcn_s_memtime();
+  unsigned long long k7_cnt[16] = {};
 #endif
 
-  for (int b = 0; b < nblocks; ++b) {
+  // Per-pixel state of a thread's four pixels, packed in one register: bits 2j..2j+1 the
+  // pixel's pending kind, bit 8+j updater.
+  constexpr uint32_t kPK = 0, kPC = 1, kPL = 2, kPF = 3;  // known / copy / lookup / far copy
+  auto pk = [](uint32_t ps, int j) { return (ps >> (2 * j)) & 3u; };
+  auto is_upd = [](uint32_t ps, int j) { return (ps >> (8 + j)) & 1u; };
+  auto set_known = [](uint32_t& ps, int j) { ps &= ~(3u << (2 * j)); };
+  // a uval slot beyond any rank for stores that are not registrations (ranks < cap <= 2048):
+  // one per thread, so the dropped stores of one instruction do not collide on one address
+  const int uval_dummy = 2048 + tid;
+  // A block's values go to the coded image (K3's input) from LDS during the NEXT block, ahead of
+  // that block's prefetches: in the in-order vmcnt, a store issued at the end of its own block
+  // would sit between the next block's loads and their first use.  Copies reaching back past
+  // the previous block read this image; they come two blocks later, after a barrier that every
+  // wave reaches only once its prefetch loads -- issued after its stores -- have completed.
+  auto store_block = [&](int b, const uint32_t* vals) {
+    const int pos0 = b * kBlock + li0;
+    const uint4 o = *reinterpret_cast<const uint4*>(&vals[li0]);
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    if (pos0 + kPer <= n) {
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4{o.x, o.y, o.z, o.w}, out_rs, 4u * (uint32_t)pos0, 0, 0);
+    } else {  // the stream's last pixels (the buffer range drops what lies past it)
+      const uint32_t ov[kPer] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+      for (int j = 0; j < kPer; ++j)
+        __builtin_amdgcn_raw_buffer_store_b32(ov[j], out_rs, pos0 + j < n ? 4u * (uint32_t)(pos0 + j) : kDropOff, 0, 0);
+    }
+  };
+  // mask bit, summary, last rank of an updater whose value is in uval[r]
+  auto reg_hash = [&](int r, uint32_t x) {
+    const uint32_t h = hash_px(x, shift);
+    atomicOr(reinterpret_cast<unsigned long long*>(&mask[h * W + (r >> 6)]), 1ull << (r & 63));
+    atomicOr(&summ[h], 1u << (r >> 6));
+    atomicMax(&slotrec[h].x, (uint32_t)r + 1u);
+  };
+  // step 3 for one registered updater: if it is its key's last in the window, write the slot
+  // (unless the window goes serial) and clear the key's masks.  The other updaters of the key
+  // only read its last rank, which the last one may already have reset (then they read 0: not
+  // theirs either).
+  auto table_update = [&](int r, uint32_t x, bool go_serial) {
+    const uint32_t h = hash_px(x, shift);
+    if (slotrec[h].x == (uint32_t)r + 1u) {
+      for (uint32_t sm = summ[h]; sm; sm &= sm - 1) mask[h * W + __builtin_ctz(sm)] = 0;
+      summ[h] = 0;
+      if (!go_serial) {
+        slotrec[h] = make_uint2(0u, x);
+        atomicOr(&slot_set[h >> 5], 1u << (h & 31));
+      } else {
+        slotrec[h].x = 0u;
+      }
+    }
+  };
+  const int lane = tid & 63;
+  static_assert(kBlock >= 2048 + kThreads, "uval: ranks below 2048, one dummy slot per thread above");
+  auto wave_sync = [] {  // intra-wave LDS hand-off: a wave's DS ops execute in order
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+
+  // one block: tk_in / lv_in its tokens and literal values; tk_nxt the next block's tokens
+  // (arrived), whose literal loads go out into lv_nxt, and tk_in is reloaded with the tokens two
+  // blocks on, once step 1 has consumed it.
+  //
+  // Instruction economy: K7 is bound by VALU issue (a wave64 VALU op holds its SIMD for four
+  // cycles and the four waves of a SIMD take turns; per-wave phase timings show the youngest
+  // wave of each SIMD setting every barrier's pace).  So the per-pixel work is branch-free
+  // (selects; a wave walks every side of a lane branch), the rare cases sit behind wave-uniform
+  // branches, and the per-updater work (3.5 % of C5's pixels) runs one updater per lane over
+  // the wave's compacted updaters instead of once per pixel slot.
+  auto block = [&](const int b, uint32_t* tk_in, uint32_t* lv_in, uint32_t* tk_nxt,
+                   uint32_t* lv_nxt) __attribute__((always_inline)) {
     const int base = b * kBlock;
     const int cur = b & 1, prv = cur ^ 1;
     uint32_t* vcur = val[cur];
     const uint32_t* vprv = val[prv];
-    // next blocks' inputs in flight while this block resolves
-    load_tokens(b + 2, tk2);
-    load_lits(tk1, lv1);
 
     // ---- 1. tokens: literals, copies from before the block, unset pixels are known; in-block
-    //         copies and lookups are pending.  Literals and copies are updaters (ranked).
-    uint8_t pend[kPer];  // 0 known, else kPendCopy / kPendLookup / kPendFar
-    bool upd[kPer];
-    uint32_t v[kPer];
-    bool bad = false, far = false;
+    //         copies and lookups are pending.  Literals and copies are updaters (ranked).  A
+    //         lookup's key / a copy's distance stays in `aux`.  (Literal values come from buffer
+    //         loads that read 0 out of range.)
+    uint32_t ps = 0, nearm = 0;
+    uint32_t v[kPer], aux[kPer];
+    bool bad = false;
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
       const int li = li0 + j, pos = base + li;
-      const uint32_t t = pos < n ? tk[j] : kTokUnset, kind = t & ~kTokPayload, pl = t & kTokPayload;
-      v[j] = 0;
-      pend[j] = 0;
-      upd[j] = false;
-      if (kind == kTokLiteral) {
-        if (pl >= (uint32_t)D.n_lits) bad = true;
-        v[j] = pl < (uint32_t)D.n_lits ? lv[j] : 0u;
-        upd[j] = true;
-      } else if (kind == kTokCopy) {
-        const int s = pos - (int)pl;
-        upd[j] = true;
-        if (pl == 0 || s < 0) {
-          bad = true;
-        } else if (s >= base) {
-          pend[j] = kPendCopy;
-          ref[li] = (int16_t)(s - base);
-        } else if (s >= base - kBlock) {
-          v[j] = vprv[s - base + kBlock];
-        } else {
-          pend[j] = kPendFar;  // loaded below, off the common path
-          far = true;
-        }
-      } else if (kind == kTokCache) {
-        if (pl >= (uint32_t)nkeys) bad = true;
-        else pend[j] = kPendLookup;
+      const uint32_t t = pos < n ? tk_in[j] : kTokUnset, kind = t >> 30, pl = t & kTokPayload;
+      const bool is_lit = kind == 0, is_cache = kind == 1, is_copy = kind == 2;
+      const int s = pos - (int)pl;
+      const bool cok = is_copy & (pl != 0u) & (s >= 0);
+      const bool kok = is_cache & (pl < (uint32_t)nkeys);
+      bad |= (is_copy & !cok) | (is_cache & !kok) | (is_lit & (pl >= (uint32_t)D.n_lits));
+      const uint32_t code = (cok & (s >= base)) ? kPC : kok ? kPL : (cok & (s < base - kBlock)) ? kPF : kPK;
+      ps |= code << (2 * j) | (uint32_t)(is_lit | is_copy) << (8 + j);
+      nearm |= (uint32_t)(cok & (s < base) & (s >= base - kBlock)) << j;
+      v[j] = lv_in[j];
+      aux[j] = pl;
+    }
+    if (__any(nearm != 0)) {  // copies from the previous block, in LDS
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) {
+        const bool nc = (nearm >> j) & 1u;
+        const uint32_t x = vprv[nc ? (int)(li0 + j + kBlock) - (int)aux[j] : 0];
+        v[j] = nc ? x : v[j];
       }
-      st[li] = pend[j] == kPendCopy || pend[j] == kPendLookup ? pend[j] : kKnown;
     }
     *reinterpret_cast<uint4*>(&vcur[li0]) = make_uint4(v[0], v[1], v[2], v[3]);
+    if (b > 0) store_block(b - 1, vprv);
+    // the next blocks' inputs go out now (tk_in and lv_in are consumed)
+    load_tokens(b + 2, tk_in);
+    load_lits(tk_nxt, lv_nxt);
+    K7_T(14);
     if (bad) {
       if (err) atomicOr(err, 4);
       slow = 1;
     }
     // ranks: updaters before each pixel, a block-wide prefix count (per-thread count 0..4 in
-    // three ballots)
-    const int cnt = (int)upd[0] + (int)upd[1] + (int)upd[2] + (int)upd[3];
+    // three ballots).  wsum: the wave's updaters, bit 16 a copy reaching back past the last
+    // block, bit 17 an in-block copy (pending).
+    const uint32_t cm = ps & (ps >> 1) & 0x55u, pm = ps & ~(ps >> 1) & 0x55u;  // codes kPF / kPC
+    const bool my_pc = pm != 0u;
+    const bool wave_pc = __any(my_pc);
+    const int cnt = __builtin_popcount((ps >> 8) & 0xfu);
     const uint64_t b0 = __ballot(cnt & 1), b1 = __ballot(cnt & 2), b2 = __ballot(cnt & 4);
     const int excl = count_below(b0) + 2 * count_below(b1) + 4 * count_below(b2);
-    const bool wave_far = __any(far);
-    if ((tid & 63) == 0)  // the wave's updaters, bit 16: it has a copy reaching back past the last block
+    const bool wave_far = __any(cm != 0u);
+    if (lane == 0)
       wsum[wave] = (uint32_t)(__builtin_popcountll(b0) + 2 * __builtin_popcountll(b1) + 4 * __builtin_popcountll(b2)) |
-                   (wave_far ? 0x10000u : 0u);
+                   (wave_far ? 0x10000u : 0u) | (wave_pc ? 0x20000u : 0u);
     __syncthreads();
     K7_T(4);
-    int ws[kWaves];  // (static indices only: a dynamic index would put the array in scratch)
-    uint32_t any_far = 0;
-#pragma unroll
-    for (int w = 0; w < kWaves; w += 4) {
-      const uint4 q = *reinterpret_cast<const uint4*>(&wsum[w]);
-      any_far |= q.x | q.y | q.z | q.w;
-      ws[w] = (int)(q.x & 0xffff), ws[w + 1] = (int)(q.y & 0xffff), ws[w + 2] = (int)(q.z & 0xffff),
-      ws[w + 3] = (int)(q.w & 0xffff);
+    // the sixteen wave counts in lanes 0..15 (one DPP row): inclusive scan, then read lanes
+    const uint32_t wraw = wsum[lane & 15];
+    const int wc = (int)(wraw & 0xffffu);
+    int scan = wc;
+    scan += __builtin_amdgcn_update_dpp(0, scan, 0x111, 0xf, 0xf, false);  // row_shr:1
+    scan += __builtin_amdgcn_update_dpp(0, scan, 0x112, 0xf, 0xf, false);  // row_shr:2
+    scan += __builtin_amdgcn_update_dpp(0, scan, 0x114, 0xf, 0xf, false);  // row_shr:4
+    scan += __builtin_amdgcn_update_dpp(0, scan, 0x118, 0xf, 0xf, false);  // row_shr:8
+    const int total = __builtin_amdgcn_readlane(scan, 15);
+    const int my_wc = __builtin_amdgcn_readlane(wc, wave);
+    const int woff = __builtin_amdgcn_readlane(scan, wave) - my_wc;
+    const uint64_t fl = __ballot(lane < 16 && (wraw & 0x10000u)), plm = __ballot(lane < 16 && (wraw & 0x20000u));
+    const bool blk_pc = plm != 0;
+    // windows: the fewest (1, 2, 4, 8 or 16 runs of whole waves) with at most `cap` updaters
+    // each (a one-wave window has at most 256 <= cap); almost always one
+    auto prefix = [&](int w) { return w <= 0 ? 0 : __builtin_amdgcn_readlane(scan, w - 1); };  // waves < w
+    int wpw = kWaves;  // waves per window
+    if (nkeys && total > cap) {
+      int l = 4;
+      for (int lv = 3; lv >= 1; --lv) {
+        const int span = kWaves >> lv;
+        int mx = 0;
+        for (int w0 = 0; w0 < kWaves; w0 += span) mx = max(mx, prefix(w0 + span) - prefix(w0));
+        if (mx <= cap) l = lv;  // ends at the smallest level that fits
+      }
+      wpw = kWaves >> l;
     }
-    // copies reaching back more than one block read the final image (stored at the end of their
-    // block, before a barrier); rare, so the whole workgroup takes this branch or none does (a
-    // load under a lane branch would make every later use wait for all outstanding loads)
-    if (any_far >> 16) {
+    // copies reaching back more than one block read the final image (stored during the
+    // previous block, complete before the barrier above); rare, so the whole workgroup takes
+    // this branch or none does (a load under a lane branch would make every later use wait for
+    // all outstanding loads)
+    if (fl != 0) {
 #pragma unroll
       for (int j = 0; j < kPer; ++j) {
-        const uint32_t s_off =
-            pend[j] == kPendFar ? 4u * (uint32_t)(base + li0 + j - (int)(tk[j] & kTokPayload)) : kDropOff;
+        const bool f = pk(ps, j) == kPF;
+        const uint32_t s_off = f ? 4u * (uint32_t)(base + li0 + j - (int)aux[j]) : kDropOff;
         const uint32_t x = __builtin_amdgcn_raw_buffer_load_b32(out_rs, s_off, 0, 0);
-        if (pend[j] == kPendFar) {
+        if (f) {
+          set_known(ps, j);
           v[j] = x;
-          pend[j] = 0;
           vcur[li0 + j] = x;  // (read by in-block copies in the rounds, after a barrier)
         }
       }
     }
-    int woff = 0;
+    // in-block copies: sources and every pixel's state for the pointer jumping (rare in C5)
+    if (blk_pc) {
+      uint32_t stw = 0, rfw[2] = {0u, 0u};
 #pragma unroll
-    for (int w = 0; w < kWaves; ++w) woff += w < wave ? ws[w] : 0;
-    // windows: the fewest (1, 2, 4, 8 or 16 runs of whole waves) with at most `cap` updaters
-    // each (a one-wave window has at most 256 <= cap)
-    int wpw = kWaves;  // waves per window
-    if (nkeys) {
-      int mx[5] = {0, 0, 0, 0, 0};  // largest window for 16, 8, 4, 2, 1 waves per window
-#pragma unroll
-      for (int l = 0; l < 5; ++l) {
-        const int span = kWaves >> l;
-#pragma unroll
-        for (int w0 = 0; w0 < kWaves; w0 += span) {
-          int s = 0;
-#pragma unroll
-          for (int w = w0; w < w0 + span; ++w) s += ws[w];
-          mx[l] = max(mx[l], s);
-        }
+      for (int j = 0; j < kPer; ++j) {
+        const uint32_t c = pk(ps, j);
+        stw |= (uint32_t)(c == kPC ? kPendCopy : c == kPL ? kPendLookup : kKnown) << (8 * j);
+        rfw[j >> 1] |= (c == kPC ? (uint32_t)(li0 + j) - aux[j] : 0u) << (16 * (j & 1));
       }
-      int l = 0;
-#pragma unroll
-      for (int i = 4; i >= 0; --i)
-        if (mx[i] <= cap) l = i;  // ends at the smallest level that fits (level 4 always does)
-      wpw = __builtin_amdgcn_readfirstlane(kWaves >> l);
+      *reinterpret_cast<uint2*>(&ref[li0]) = make_uint2(rfw[0], rfw[1]);
+      *reinterpret_cast<uint32_t*>(&st[li0]) = stw;
     }
-    const int nwin = kWaves / wpw;
-    const int myq = wave / wpw;
     int R[kPer];  // updaters of the block before each pixel
     {
       int r = woff + excl;
 #pragma unroll
       for (int j = 0; j < kPer; ++j) {
         R[j] = r;
-        r += (int)upd[j];
+        r += (int)is_upd(ps, j);
       }
     }
+    const int nwin = kWaves / wpw;
+    const int myq = wave / wpw;
     int serial_from = kBlock;  // local pixel where the serial path takes over
-    int rb = 0;                // updaters before the window
     for (int q = 0; q < nwin; ++q) {
       const bool in_win = myq == q;
+      const int rb = prefix(q * wpw);  // updaters before the window
       K7_COUNT(3, 1);
-      // ---- register the known updaters of the window
-      bool pc = false;  // a pending copy of mine in the window
-      if (in_win) {
+      // ---- 2. register the known updaters of the window: values by rank (one store per pixel
+      //         slot, to a dummy slot when it is not one), then one updater per lane over the
+      //         wave's ranks [woff - rb, woff - rb + my_wc) -- or per pixel slot when the wave
+      //         has in-block copies, whose ranks lie in the same range unregistered
 #pragma unroll
-        for (int j = 0; j < kPer; ++j) {
-          if (!upd[j]) continue;
-          if (pend[j]) {
-            pc = true;
-            continue;
+      for (int j = 0; j < kPer; ++j)
+        uval[in_win && is_upd(ps, j) && pk(ps, j) == kPK ? R[j] - rb : uval_dummy] = v[j];
+      if (in_win && nkeys) {
+        if (!wave_pc) {
+          wave_sync();
+          for (int i = lane; i < my_wc; i += 64) {
+            const int r = woff - rb + i;
+            reg_hash(r, uval[r]);
           }
-          const int r = R[j] - rb;
-          uval[r] = v[j];
-          if (nkeys) {
-            const uint32_t h = hash_px(v[j], shift);
-            atomicOr(reinterpret_cast<unsigned long long*>(&mask[h * W + (r >> 6)]), 1ull << (r & 63));
-            atomicOr(&summ[h], 1u << (r >> 6));
-            atomicMax(&last_rank[h], (uint32_t)r + 1u);
-          }
-        }
-        if (pc) {
-          int fp = kBlock;
+        } else {
 #pragma unroll
-          for (int j = kPer - 1; j >= 0; --j)
-            if (pend[j] == kPendCopy) fp = li0 + j;
-          atomicMin(&first_pend[0], fp);
+          for (int j = 0; j < kPer; ++j)
+            if (is_upd(ps, j) && pk(ps, j) == kPK) reg_hash(R[j] - rb, v[j]);
         }
+      }
+      const bool pc = in_win && my_pc;
+      if (pc) {
+        int fp = kBlock;
+#pragma unroll
+        for (int j = kPer - 1; j >= 0; --j)
+          if (pk(ps, j) == kPC) fp = li0 + j;
+        atomicMin(&first_pend[0], fp);
       }
       // ---- rounds (one when the window has no pending copy: every lookup resolves in (a))
       int any_pc = sync_or(pc);
+      K7_T(11);
       for (int r = 0;; ++r) {
         K7_COUNT(2, 1);
         if (r == kMaxRounds) {
@@ -357,52 +439,75 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
         // first_pend[(r + 1) & 1] was last read in round r - 1; it is next written in (b), after
         // the barrier below
         if (tid == 0) first_pend[(r + 1) & 1] = kBlock;
-        // (a) lookups before the first pending copy: the key's mask below the pixel's rank
-        //     count, else the slot as the previous window left it
+        // (a) lookups before the first pending copy: the key's last updater in the window if it
+        //     precedes the pixel, none (the slot as the previous window left it), or -- it
+        //     straddles the pixel -- the highest mask bit below the pixel's rank count
         if (in_win) {
+          uint32_t act = 0, strad = 0;
+          uint2 rec[kPer];
 #pragma unroll
           for (int j = 0; j < kPer; ++j) {
-            if (pend[j] != kPendLookup || li0 + j >= fp) continue;
-            const uint32_t k = tk[j] & kTokPayload;
-            const int rr = R[j] - rb;  // window updaters before the pixel
-            uint32_t x;
-            bool found = false;
-            if (rr > 0) {
+            const bool a = pk(ps, j) == kPL && li0 + j < fp;
+            act |= (uint32_t)a << j;
+            rec[j] = slotrec[a ? aux[j] : 0u];
+          }
+          uint32_t idx[kPer];  // uval index of the last updater below the pixel, or ~0
+#pragma unroll
+          for (int j = 0; j < kPer; ++j) {
+            const uint32_t rr = (uint32_t)(R[j] - rb), d = rec[j].x - 1u;  // (lr = 0: d = ~0)
+            idx[j] = d < rr ? d : ~0u;
+            strad |= (uint32_t)(d != ~0u && d >= rr) << j;
+          }
+          strad &= act;
+          if (__any(strad != 0)) {  // (~10 % of C5's lookups)
+#pragma unroll
+            for (int j = 0; j < kPer; ++j) {
+              if (!((strad >> j) & 1u)) continue;
+              const uint32_t k = aux[j];
+              const int rr = R[j] - rb;  // window updaters before the pixel
               const int wt = (rr - 1) >> 6;
-              uint32_t sm = summ[k] & (wt >= 31 ? ~0u : (2u << wt) - 1u);
-              if (sm) {
-                int w = 31 - __builtin_clz(sm);
-                uint64_t m = mask[k * W + w];
-                if (w == wt) {
-                  const int lb = rr - 64 * wt;  // 1..64 bits below the pixel
-                  m &= lb >= 64 ? ~0ull : (1ull << lb) - 1ull;
-                  if (!m) {
-                    sm &= (1u << wt) - 1u;
-                    if (sm) {
-                      w = 31 - __builtin_clz(sm);
-                      m = mask[k * W + w];
-                    }
-                  }
-                }
-                if (m) {
-                  x = uval[64 * w + 63 - __builtin_clzll(m)];
-                  found = true;
-                }
-              }
+              const uint32_t sm = rr <= 0 ? 0u : summ[k] & (wt >= 31 ? ~0u : (2u << wt) - 1u);
+              const int w1 = sm ? 31 - __builtin_clz(sm) : 0;
+              const uint32_t sm2 = sm & ~(1u << w1);
+              const int w2 = sm2 ? 31 - __builtin_clz(sm2) : 0;
+              const uint64_t m1 = sm ? mask[k * W + w1] : 0ull;
+              const uint64_t m2 = sm2 ? mask[k * W + w2] : 0ull;
+              // the top word is the pixel's own word: keep only the ranks below it (lb = 1..64)
+              const int lb = rr - 64 * w1;
+              const uint64_t top = lb < 64 ? m1 & ((1ull << lb) - 1ull) : m1;
+              const uint64_t m = top ? top : m2;
+              const int w = top ? w1 : w2;
+              if (m) idx[j] = (uint32_t)(64 * w + 63 - __builtin_clzll(m));
             }
-            if (!found) {
-              x = slot_val[k];
-              if (k != 0 && !((slot_set[k >> 5] >> (k & 31)) & 1)) {
+          }
+          uint32_t empty = 0;  // lookups of a slot that may never have been written
+#pragma unroll
+          for (int j = 0; j < kPer; ++j) {
+            const uint32_t xin = uval[idx[j] & (kBlock - 1)];
+            const bool a = (act >> j) & 1u;
+            const uint32_t x = idx[j] != ~0u ? xin : rec[j].y;
+            empty |= (uint32_t)(a & (idx[j] == ~0u) & (aux[j] != 0u) & (x == 0u)) << j;
+            v[j] = a ? x : v[j];
+          }
+          ps &= ~((act & 1u) * 0x3u | (act & 2u) * 0x6u | (act & 4u) * 0xcu | (act & 8u) * 0x18u);  // codes -> known
+          if (__any(empty != 0)) {
+#pragma unroll
+            for (int j = 0; j < kPer; ++j) {
+              const uint32_t k = aux[j];
+              if ((empty >> j) & 1u && !((slot_set[k >> 5] >> (k & 31)) & 1u)) {
                 K7_COUNT(9, 1);
                 slow = 1;
               }
             }
-            v[j] = x;
-            pend[j] = 0;
-            vcur[li0 + j] = x;  // (read by copies in (b), after the barrier)
-            st[li0 + j] = kKnown;
+          }
+          if (act) *reinterpret_cast<uint4*>(&vcur[li0]) = make_uint4(v[0], v[1], v[2], v[3]);
+          if (any_pc && act) {  // copies in (b) read these states, after the barrier
+#pragma unroll
+            for (int j = 0; j < kPer; ++j)
+              if ((act >> j) & 1u) st[li0 + j] = kKnown;
           }
         }
+        K7_T(12);
         if (!any_pc) break;
         __syncthreads();
         // (b) pending copies: take a known source's value and register, else jump one link back
@@ -411,25 +516,19 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
 #pragma unroll
           for (int j = 0; j < kPer; ++j) {
             const int li = li0 + j;
-            if (pend[j] != kPendCopy) continue;
+            if (pk(ps, j) != kPC) continue;
             const int src = ref[li];
             const uint8_t ss = st[src];
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
             if (ss == kKnown) {
               const uint32_t x = vcur[src];
+              set_known(ps, j);
               v[j] = x;
-              pend[j] = 0;
               vcur[li] = x;
               __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
               st[li] = kKnown;
-              const int rk = R[j] - rb;
-              uval[rk] = x;
-              if (nkeys) {
-                const uint32_t h = hash_px(x, shift);
-                atomicOr(reinterpret_cast<unsigned long long*>(&mask[h * W + (rk >> 6)]), 1ull << (rk & 63));
-                atomicOr(&summ[h], 1u << (rk >> 6));
-                atomicMax(&last_rank[h], (uint32_t)rk + 1u);
-              }
+              uval[R[j] - rb] = x;
+              if (nkeys) reg_hash(R[j] - rb, x);
             } else {
               if (ss == kPendCopy) ref[li] = ref[src];  // (a stale or fresh link: both lie on the chain)
               atomicMin(&first_pend[(r + 1) & 1], li);
@@ -438,27 +537,21 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
           }
         }
         any_pc = sync_or(still);
+        K7_T(5);
       }
       __syncthreads();  // every lookup has read the slot table; the masks are complete
       const bool go_serial = slow != 0;
-      // ---- 3. each key's last updater writes its slot (unless the window goes serial) and
-      //         clears the key's masks; the other updaters of the key only read last_rank, which
-      //         the last one may already have reset (then they read 0: not theirs either)
+      // ---- 3. each key's last updater writes its slot and clears the key's masks
       if (in_win && nkeys) {
-#pragma unroll
-        for (int j = 0; j < kPer; ++j) {
-          if (!upd[j] || pend[j]) continue;
-          const uint32_t h = hash_px(v[j], shift);
-          const int rk = R[j] - rb;
-          if (last_rank[h] == (uint32_t)rk + 1u) {
-            if (!go_serial) {
-              slot_val[h] = v[j];
-              atomicOr(&slot_set[h >> 5], 1u << (h & 31));
-            }
-            for (uint32_t sm = summ[h]; sm; sm &= sm - 1) mask[h * W + __builtin_ctz(sm)] = 0;
-            summ[h] = 0;
-            last_rank[h] = 0;
+        if (!wave_pc) {
+          for (int i = lane; i < my_wc; i += 64) {
+            const int r = woff - rb + i;
+            table_update(r, uval[r], go_serial);
           }
+        } else {
+#pragma unroll
+          for (int j = 0; j < kPer; ++j)
+            if (is_upd(ps, j) && pk(ps, j) == kPK) table_update(R[j] - rb, v[j], go_serial);
         }
       }
       if (tid == 0) first_pend[0] = first_pend[1] = kBlock;
@@ -469,17 +562,21 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
         __syncthreads();
         break;
       }
-      for (int w = q * wpw; w < (q + 1) * wpw; ++w) rb += (int)(wsum[w] & 0xffffu);  // (LDS: a dynamic index)
       __syncthreads();
+      K7_T(13);
     }
     K7_T(5);
     // ---- the exact serial path: DecodeImageData's order, one pixel at a time, from the start
     //      of the window that could not be resolved, on the table as the windows before it left
     //      it.  Literal and older-copy values are in vcur from step 1; everything else is
-    //      recomputed here.
+    //      recomputed here.  The block's tokens are read again (rare path).
     if (serial_from < kBlock) {
       K7_COUNT(1, 1);
-      *reinterpret_cast<uint4*>(&uval[li0]) = make_uint4(tk[0], tk[1], tk[2], tk[3]);
+      {
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(tok_rs, 4u * (uint32_t)(base + li0), 0, 0);
+        *reinterpret_cast<uint4*>(&uval[li0]) = make_uint4(q.x, q.y, q.z, q.w);
+      }
       __syncthreads();
       if (tid == 0) {
         const int cnt_px = min(kBlock, n - base);
@@ -493,11 +590,11 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
             const int s = pos - (int)pl;
             x = (pl == 0 || s < 0) ? 0 : s < base ? vcur[li] : vcur[s - base];
           } else if (kind == kTokCache) {
-            x = pl < (uint32_t)nkeys ? slot_val[pl] : 0;
+            x = pl < (uint32_t)nkeys ? slotrec[pl].y : 0;
           }
           if (kind != kTokUnset && nkeys) {
             const uint32_t h = hash_px(x, shift);
-            slot_val[h] = x;
+            slotrec[h].y = x;
             slot_set[h >> 5] |= 1u << (h & 31);
           }
           vcur[li] = x;
@@ -506,49 +603,33 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
       }
       __syncthreads();
     }
-    K7_T(6);
-    // ---- the block's values to the coded image (K3's input; older copies read them back)
-    {
-      const int pos0 = base + li0;
-      const uint4 o = *reinterpret_cast<const uint4*>(&vcur[li0]);
-      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-      if (pos0 + kPer <= n) {
-        __builtin_amdgcn_raw_buffer_store_b128(u32x4{o.x, o.y, o.z, o.w}, out_rs, 4u * (uint32_t)pos0, 0, 0);
-      } else {  // the stream's last pixels (the buffer range drops what lies past it)
-        const uint32_t ov[kPer] = {o.x, o.y, o.z, o.w};
-#pragma unroll
-        for (int j = 0; j < kPer; ++j)
-          __builtin_amdgcn_raw_buffer_store_b32(ov[j], out_rs, pos0 + j < n ? 4u * (uint32_t)(pos0 + j) : kDropOff, 0, 0);
-      }
-    }
-    // rotate the pipeline
-#pragma unroll
-    for (int j = 0; j < kPer; ++j) {
-      tk[j] = tk1[j];
-      lv[j] = lv1[j];
-      tk1[j] = tk2[j];
-    }
-    // vcur becomes the next block's vprv, and the stores above must be visible to copies that
-    // reach back further than one block
-    __syncthreads();
     K7_T(7);
+  };
+
+  for (int b = 0; b < nblocks; b += 2) {
+    block(b, tkA, lvA, tkB, lvB);
+    if (b + 1 < nblocks) block(b + 1, tkB, lvB, tkA, lvA);
   }
+  if (nblocks > 0) store_block(nblocks - 1, val[(nblocks - 1) & 1]);
 #ifdef WG_K7_STATS
   if (tid == 0) {
     k7_cnt[0] = (unsigned long long)nblocks;
-    for (int i = 0; i < 4; ++i) atomicAdd(&g_k7_stats[i], k7_cnt[i]);
-    for (int i = 4; i < 8; ++i) atomicAdd(&g_k7_stats[i], k7_acc[i]);
-    for (int i = 8; i < 12; ++i) atomicAdd(&g_k7_stats[i], k7_cnt[i]);
+    for (int i : {0, 1, 2, 3, 9, 10}) atomicAdd(&g_k7_stats[i], k7_cnt[i]);
+    for (int i : {4, 5, 6, 7, 11, 12, 13, 14}) atomicAdd(&g_k7_stats[i], k7_acc[i]);
   }
+  if ((tid & 63) == 0)
+    for (int i : {4, 5, 6, 7, 11, 12, 13, 14}) atomicAdd(&g_k7_wave[wave][i], k7_acc[i]);
 #endif
 }
 
 #ifdef WG_K7_STATS
 extern "C" int wg_debug_k7_stats(unsigned long long* out, int reset) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_k7_stats), sizeof(g_k7_stats)) != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out + 16, HIP_SYMBOL(g_k7_wave), sizeof(g_k7_wave)) != hipSuccess) return -1;
   if (reset) {
-    unsigned long long z[12] = {};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(g_k7_stats), z, sizeof(z)) != hipSuccess) return -1;
+    unsigned long long z[16 * (1 + kWaves)] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_k7_stats), z, sizeof(g_k7_stats)) != hipSuccess) return -1;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_k7_wave), z, sizeof(g_k7_wave)) != hipSuccess) return -1;
   }
   return 0;
 }

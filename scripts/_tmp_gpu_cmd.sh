@@ -1,5 +1,5 @@
 #!/bin/bash
-# K7 rewrite check: stage-entry parity, the lossless batch tests, K7 statistics, c5 bench.
+# K7 check: stage-entry parity, the lossless batch tests, K7 statistics, c5 bench.
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -12,6 +12,6 @@ step() {  # step <name> <timeout_s> <cmd...>
   tail -n ${TAILN:-6} "gpurun_out/$name.log"
   if [ $rc -ne 0 ]; then echo "STOP: $name rc=$rc"; exit $rc; fi
 }
-step k7_tests 300 python -u -m pytest tests/test_gpu_k7.py tests/test_gpu_vp8l.py tests/test_gpu_fuzz.py -x -v --timeout 200 --timeout-method thread -p no:cacheprovider
-step k7_stats 200 python -u scripts/k7_stats.py 32
-step bench_c5 300 python bench.py --workload c5 --steps 10 --warmup 3 --no-cpu-baseline --no-e2e
+TAILN=4 step k7_tests 300 python -u -m pytest tests/test_gpu_k7.py tests/test_gpu_vp8l.py tests/test_gpu_fuzz.py -x -q --timeout 200 --timeout-method thread -p no:cacheprovider
+TAILN=30 step k7_stats 200 python -u scripts/k7_stats.py 256
+TAILN=2 step bench_c5 300 python bench.py --workload c5 --steps 10 --warmup 3 --no-cpu-baseline --no-e2e

@@ -20,7 +20,7 @@ def main():
     ctx = webp_amd.Context(0, host_threads=16)
     b = ctx.batch([datas[i % len(datas)] for i in range(n)])
     L = webp_amd.lib()
-    st = (C.c_ulonglong * 12)()
+    st = (C.c_ulonglong * (16 * 17))()
     b.run()
     print("kernel ms", b.kernel_ms())
     L.wg_debug_k7_stats(st, 1)
@@ -28,12 +28,17 @@ def main():
     ms = b.kernel_ms()
     L.wg_debug_k7_stats(st, 1)
     blocks, serial, rounds, windows = st[0], st[1], st[2], st[3]
-    tot = sum(st[4:8])
+    phases = ((14, "tokens (load waits)"), (4, "ranks + barrier"), (11, "registration"), (12, "lookups"), (5, "copies (rounds b)"),
+              (13, "slot table"), (6, "serial path"), (7, "store + pipeline"))
+    tot = sum(st[i] for i, _ in phases)
     print(f"frames {n}: K7 {ms[4]:.3f} ms; blocks {blocks}, windows/block {windows / blocks:.3f}, "
           f"rounds/window {rounds / max(windows, 1):.3f}, serial windows {serial}")
-    for i, name in zip(range(4, 8), ("tokens + ranks", "windows (register, rounds, table)", "serial path",
-                                     "store + pipeline")):
-        print(f"  {name:36s} {st[i] / blocks:10.0f} cycles/block  {st[i] / max(tot, 1):.3f}")
+    for i, name in phases:
+        print(f"  {name:20s} {st[i] / blocks:10.0f} cycles/block  {st[i] / max(tot, 1):.3f}")
+    wv = [[st[16 + 16 * w + i] / blocks for i in range(16)] for w in range(16)]
+    print("  per wave (cycles/block):  " + " ".join(f"{name[:10]:>10s}" for _, name in phases))
+    for w in range(16):
+        print(f"    wave {w:2d}               " + " ".join(f"{wv[w][i]:10.0f}" for i, _ in phases))
     print(f"  serial causes (events): empty slot {st[9]}, round cap {st[10]}")
     b.close()
     ctx.close()
