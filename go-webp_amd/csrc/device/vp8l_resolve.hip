@@ -48,6 +48,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "../device_format.h"
 #include "kernels.h"
 
@@ -122,6 +124,7 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
   __shared__ int first_pend[2];                  // per round parity: first pending copy (local)
   __shared__ int slow;                           // this window goes serial
   __shared__ int orflag[4];                      // sync_or: a ring of flag words
+  __shared__ uint2 sscr[kWaves * 64];            // a wave's straddling lookups, compacted (key, rank)
   const LLTokDesc D = kSingle ? single : descs[blockIdx.x];
   if (!D.valid) return;
   const int tid = threadIdx.x;
@@ -253,6 +256,25 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   };
 
+  // A lookup whose key has window updaters on both sides of it: the highest bit of the key's
+  // rank mask below rr (the window updaters before the pixel), from the summary's top one or
+  // two words; ~0 if none.
+  auto straddle_idx = [&](uint32_t k, int rr) -> uint32_t {
+    const int wt = (rr - 1) >> 6;
+    const uint32_t sm = rr <= 0 ? 0u : summ[k] & (wt >= 31 ? ~0u : (2u << wt) - 1u);
+    const int w1 = sm ? 31 - __builtin_clz(sm) : 0;
+    const uint32_t sm2 = sm & ~(1u << w1);
+    const int w2 = sm2 ? 31 - __builtin_clz(sm2) : 0;
+    const uint64_t m1 = sm ? mask[k * W + w1] : 0ull;
+    const uint64_t m2 = sm2 ? mask[k * W + w2] : 0ull;
+    // the top word is the pixel's own word: keep only the ranks below it (lb = 1..64)
+    const int lb = rr - 64 * w1;
+    const uint64_t top = lb < 64 ? m1 & ((1ull << lb) - 1ull) : m1;
+    const uint64_t m = top ? top : m2;
+    const int w = top ? w1 : w2;
+    return m ? (uint32_t)(64 * w + 63 - __builtin_clzll(m)) : ~0u;
+  };
+
   // one block: tk_in / lv_in its tokens and literal values; tk_nxt the next block's tokens
   // (arrived), whose literal loads go out into lv_nxt, and tk_in is reloaded with the tokens two
   // blocks on, once step 1 has consumed it.
@@ -277,20 +299,27 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
     uint32_t ps = 0, nearm = 0;
     uint32_t v[kPer], aux[kPer];
     bool bad = false;
+    if (base + kBlock > n) {  // the stream's last block: pixels past its end are unset
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) tk_in[j] = base + li0 + j < n ? tk_in[j] : kTokUnset;
+    }
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
-      const int li = li0 + j, pos = base + li;
-      const uint32_t t = pos < n ? tk_in[j] : kTokUnset, kind = t >> 30, pl = t & kTokPayload;
-      const bool is_lit = kind == 0, is_cache = kind == 1, is_copy = kind == 2;
-      const int s = pos - (int)pl;
-      const bool cok = is_copy & (pl != 0u) & (s >= 0);
-      const bool kok = is_cache & (pl < (uint32_t)nkeys);
-      bad |= (is_copy & !cok) | (is_cache & !kok) | (is_lit & (pl >= (uint32_t)D.n_lits));
-      const uint32_t code = (cok & (s >= base)) ? kPC : kok ? kPL : (cok & (s < base - kBlock)) ? kPF : kPK;
-      ps |= code << (2 * j) | (uint32_t)(is_lit | is_copy) << (8 + j);
-      nearm |= (uint32_t)(cok & (s < base) & (s >= base - kBlock)) << j;
+      const int li = li0 + j;
+      const uint32_t t = tk_in[j], kind = t >> 30, pl = t & kTokPayload;
+      const bool is_copy = kind == 2, is_cache = kind == 1;
+      // out of the stream's bounds: literal index >= n_lits, key >= 1 << cache_bits, distance 0
+      // or before the start ((pl - 1) >= pos, unsigned) -- one compare against a per-kind limit
+      const uint32_t lim = kind == 0 ? (uint32_t)D.n_lits : is_cache ? (uint32_t)nkeys : is_copy ? (uint32_t)(base + li) : ~0u;
+      bad |= (is_copy ? pl - 1u : pl) >= lim;
+      // copies: in-block source (pl <= li), previous block (li < pl <= li + 4096), older
+      const bool inb = is_copy & (pl - 1u < (uint32_t)li);  // (pl = 0 wraps: not in-block)
+      const bool farc = is_copy & (pl > (uint32_t)(li + kBlock));
+      const uint32_t code = inb ? kPC : farc ? kPF : is_cache ? kPL : kPK;
+      ps |= code << (2 * j) | (~kind & 1u) << (8 + j);  // updaters: kinds 0 (literal) and 2 (copy)
+      nearm |= (uint32_t)(is_copy & !inb & !farc) << j;
       v[j] = lv_in[j];
-      aux[j] = pl;
+      aux[j] = is_cache ? pl & (kSlots - 1) : pl;
     }
     if (__any(nearm != 0)) {  // copies from the previous block, in LDS
 #pragma unroll
@@ -381,15 +410,9 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
       *reinterpret_cast<uint2*>(&ref[li0]) = make_uint2(rfw[0], rfw[1]);
       *reinterpret_cast<uint32_t*>(&st[li0]) = stw;
     }
-    int R[kPer];  // updaters of the block before each pixel
-    {
-      int r = woff + excl;
-#pragma unroll
-      for (int j = 0; j < kPer; ++j) {
-        R[j] = r;
-        r += (int)is_upd(ps, j);
-      }
-    }
+    // updaters of the block before pixel j (recomputed at each use: four live ranks cost registers)
+    const int r0 = woff + excl;
+    auto R = [&](int j) { return r0 + __builtin_popcount((ps >> 8) & ((1u << j) - 1u)); };
     const int nwin = kWaves / wpw;
     const int myq = wave / wpw;
     int serial_from = kBlock;  // local pixel where the serial path takes over
@@ -403,7 +426,7 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
       //         has in-block copies, whose ranks lie in the same range unregistered
 #pragma unroll
       for (int j = 0; j < kPer; ++j)
-        uval[in_win && is_upd(ps, j) && pk(ps, j) == kPK ? R[j] - rb : uval_dummy] = v[j];
+        uval[in_win && is_upd(ps, j) && pk(ps, j) == kPK ? R(j) - rb : uval_dummy] = v[j];
       if (in_win && nkeys) {
         if (!wave_pc) {
           wave_sync();
@@ -414,7 +437,7 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
         } else {
 #pragma unroll
           for (int j = 0; j < kPer; ++j)
-            if (is_upd(ps, j) && pk(ps, j) == kPK) reg_hash(R[j] - rb, v[j]);
+            if (is_upd(ps, j) && pk(ps, j) == kPK) reg_hash(R(j) - rb, v[j]);
         }
       }
       const bool pc = in_win && my_pc;
@@ -425,59 +448,58 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
           if (pk(ps, j) == kPC) fp = li0 + j;
         atomicMin(&first_pend[0], fp);
       }
-      // ---- rounds (one when the window has no pending copy: every lookup resolves in (a))
-      int any_pc = sync_or(pc);
-      K7_T(11);
-      for (int r = 0;; ++r) {
-        K7_COUNT(2, 1);
-        if (r == kMaxRounds) {
-          K7_COUNT(10, 1);
-          slow = 1;
-          break;  // uniform: any_pc and r are the same in every thread
-        }
-        const int fp = any_pc ? first_pend[r & 1] : kBlock;
-        // first_pend[(r + 1) & 1] was last read in round r - 1; it is next written in (b), after
-        // the barrier below
-        if (tid == 0) first_pend[(r + 1) & 1] = kBlock;
+      // (a) of a round: lookups of the window before the first pending copy fp.  kRounds: the
+      // window has in-block copies (fp varies, and copies read the lookups' states); instantiated
+      // twice so that the common case (no in-block copy: one pass, every lookup resolves)
+      // carries none of it.
+      auto lookups = [&](const int fp, auto kRoundsC) __attribute__((always_inline)) {
+        constexpr bool kRounds = decltype(kRoundsC)::value;
         // (a) lookups before the first pending copy: the key's last updater in the window if it
         //     precedes the pixel, none (the slot as the previous window left it), or -- it
         //     straddles the pixel -- the highest mask bit below the pixel's rank count
-        if (in_win) {
           uint32_t act = 0, strad = 0;
           uint2 rec[kPer];
 #pragma unroll
           for (int j = 0; j < kPer; ++j) {
-            const bool a = pk(ps, j) == kPL && li0 + j < fp;
+            const bool a = pk(ps, j) == kPL && (!kRounds || li0 + j < fp);
             act |= (uint32_t)a << j;
             rec[j] = slotrec[a ? aux[j] : 0u];
           }
           uint32_t idx[kPer];  // uval index of the last updater below the pixel, or ~0
 #pragma unroll
           for (int j = 0; j < kPer; ++j) {
-            const uint32_t rr = (uint32_t)(R[j] - rb), d = rec[j].x - 1u;  // (lr = 0: d = ~0)
+            const uint32_t rr = (uint32_t)(R(j) - rb), d = rec[j].x - 1u;  // (lr = 0: d = ~0)
             idx[j] = d < rr ? d : ~0u;
             strad |= (uint32_t)(d != ~0u && d >= rr) << j;
           }
           strad &= act;
-          if (__any(strad != 0)) {  // (~10 % of C5's lookups)
+          if (__any(strad != 0)) {
+            // (10 % of C5's lookups, in 96 % of its waves): compacted, one straddling lookup per
+            // lane, instead of each pixel slot's branch walked by the whole wave
+            const int sc = __builtin_popcount(strad);
+            const uint64_t s0 = __ballot(sc & 1), s1 = __ballot(sc & 2), s2 = __ballot(sc & 4);
+            const int sx = count_below(s0) + 2 * count_below(s1) + 4 * count_below(s2);
+            const int stot = __builtin_popcountll(s0) + 2 * __builtin_popcountll(s1) + 4 * __builtin_popcountll(s2);
+            uint2* const scr = sscr + wave * 64;
+            if (stot <= 64) {
+              int slot = sx;
 #pragma unroll
-            for (int j = 0; j < kPer; ++j) {
-              if (!((strad >> j) & 1u)) continue;
-              const uint32_t k = aux[j];
-              const int rr = R[j] - rb;  // window updaters before the pixel
-              const int wt = (rr - 1) >> 6;
-              const uint32_t sm = rr <= 0 ? 0u : summ[k] & (wt >= 31 ? ~0u : (2u << wt) - 1u);
-              const int w1 = sm ? 31 - __builtin_clz(sm) : 0;
-              const uint32_t sm2 = sm & ~(1u << w1);
-              const int w2 = sm2 ? 31 - __builtin_clz(sm2) : 0;
-              const uint64_t m1 = sm ? mask[k * W + w1] : 0ull;
-              const uint64_t m2 = sm2 ? mask[k * W + w2] : 0ull;
-              // the top word is the pixel's own word: keep only the ranks below it (lb = 1..64)
-              const int lb = rr - 64 * w1;
-              const uint64_t top = lb < 64 ? m1 & ((1ull << lb) - 1ull) : m1;
-              const uint64_t m = top ? top : m2;
-              const int w = top ? w1 : w2;
-              if (m) idx[j] = (uint32_t)(64 * w + 63 - __builtin_clzll(m));
+              for (int j = 0; j < kPer; ++j)
+                if ((strad >> j) & 1u) scr[slot++] = make_uint2(aux[j], (uint32_t)(R(j) - rb));
+              wave_sync();
+              if (lane < stot) {
+                const uint2 e = scr[lane];
+                scr[lane].x = straddle_idx(e.x, (int)e.y);
+              }
+              wave_sync();
+              slot = sx;
+#pragma unroll
+              for (int j = 0; j < kPer; ++j)
+                if ((strad >> j) & 1u) idx[j] = scr[slot++].x;
+            } else {
+#pragma unroll
+              for (int j = 0; j < kPer; ++j)
+                if ((strad >> j) & 1u) idx[j] = straddle_idx(aux[j], R(j) - rb);
             }
           }
           uint32_t empty = 0;  // lookups of a slot that may never have been written
@@ -501,12 +523,32 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
             }
           }
           if (act) *reinterpret_cast<uint4*>(&vcur[li0]) = make_uint4(v[0], v[1], v[2], v[3]);
-          if (any_pc && act) {  // copies in (b) read these states, after the barrier
+          if (kRounds && act) {  // copies in (b) read these states, after the barrier
 #pragma unroll
             for (int j = 0; j < kPer; ++j)
               if ((act >> j) & 1u) st[li0 + j] = kKnown;
           }
+      };
+      // ---- rounds (one when the window has no pending copy: every lookup resolves in (a))
+      int any_pc = sync_or(pc);
+      K7_T(11);
+      if (!any_pc) {
+        K7_COUNT(2, 1);
+        if (in_win) lookups(kBlock, std::false_type{});
+        K7_T(12);
+      }
+      for (int r = 0; any_pc || r > 0; ++r) {  // (entered only with copies; ends after the (a) that follows the last)
+        K7_COUNT(2, 1);
+        if (r == kMaxRounds) {
+          K7_COUNT(10, 1);
+          slow = 1;
+          break;  // uniform: any_pc and r are the same in every thread
         }
+        const int fp = any_pc ? first_pend[r & 1] : kBlock;
+        // first_pend[(r + 1) & 1] was last read in round r - 1; it is next written in (b), after
+        // the barrier below
+        if (tid == 0) first_pend[(r + 1) & 1] = kBlock;
+        if (in_win) lookups(fp, std::true_type{});
         K7_T(12);
         if (!any_pc) break;
         __syncthreads();
@@ -527,8 +569,8 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
               vcur[li] = x;
               __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
               st[li] = kKnown;
-              uval[R[j] - rb] = x;
-              if (nkeys) reg_hash(R[j] - rb, x);
+              uval[R(j) - rb] = x;
+              if (nkeys) reg_hash(R(j) - rb, x);
             } else {
               if (ss == kPendCopy) ref[li] = ref[src];  // (a stale or fresh link: both lie on the chain)
               atomicMin(&first_pend[(r + 1) & 1], li);
@@ -551,7 +593,7 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
         } else {
 #pragma unroll
           for (int j = 0; j < kPer; ++j)
-            if (is_upd(ps, j) && pk(ps, j) == kPK) table_update(R[j] - rb, v[j], go_serial);
+            if (is_upd(ps, j) && pk(ps, j) == kPK) table_update(R(j) - rb, v[j], go_serial);
         }
       }
       if (tid == 0) first_pend[0] = first_pend[1] = kBlock;

@@ -499,7 +499,8 @@ uint32_t parse_residuals_sparse(Decoder* d, MBCtx* mb, MBCtx* left_mb, BoolReade
       l = (nz > first);
       tnz = (uint8_t)((tnz >> 1) | (l << 7));
       nz_coeffs = nz_code_bits(nz_coeffs, nz, (first ? dcs[4 * y + x] : ob[0]) != 0);
-      if (block_nonzero(ob)) {
+      // (nz == first: no coefficient was decoded; past it one may still wrap to 0 in int16)
+      if (nz > first && block_nonzero(ob)) {
         mask |= 1u << (4 * y + x);
         ++nb;
       }
@@ -523,7 +524,7 @@ uint32_t parse_residuals_sparse(Decoder* d, MBCtx* mb, MBCtx* left_mb, BoolReade
         l = (nz > 0);
         tnz = (uint8_t)((tnz >> 1) | (l << 3));
         nz_coeffs = nz_code_bits(nz_coeffs, nz, ob[0] != 0);
-        if (block_nonzero(ob)) {
+        if (nz > 0 && block_nonzero(ob)) {
           mask |= 1u << (16 + 2 * ch + 2 * y + x);
           ++nb;
         }
