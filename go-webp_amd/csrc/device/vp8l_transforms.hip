@@ -48,6 +48,9 @@ constexpr int kLdsBytes = kRingBytes + kModeTabMax + kCCTabMax * 4 + kWaves * kS
 static_assert(kLdsBytes + 4 * kWaves <= 160 * 1024, "K3 LDS (dynamic + the progress counters) exceeds gfx950's 160 KB");
 static_assert(kOutCols >= 14 + kChunk && kOutCols % 4 == 0, "row ring: 14 open columns + a chunk; 16-byte pieces never wrap");
 constexpr uint32_t kDrop = 0x80000000u;
+#ifndef WG_K3_STORE_AUX
+#define WG_K3_STORE_AUX 0  // cache policy of the output block stores (buffer aux bits; A/B builds)
+#endif
 constexpr int T_PRED = 0, T_CC = 1, T_AG = 2;  // 3 = color indexing
 
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
@@ -365,17 +368,22 @@ __device__ __forceinline__ bool pred_wavefront(const Pass& P, int W, int H, int 
     // (ignored) or, in row 0, wrap to an out-of-range offset (reads 0).
     const int rows_left = H - b * kBand;
     // Row ring of 24 columns (column x at position x mod 24), inputs staged and outputs
-    // emitted per chunk.  Loads: chunk c's 8 columns of a row (32 B) by two lanes, rows
-    // lane/2 and lane/2 + 32, issued two chunks ahead.  Stores: whenever a row completes an
+    // emitted per chunk.  Loads: per chunk one aligned 32-byte block (8 columns) of each
+    // row, the block holding the chunk's last column (c - r/4 for row r; the block before it
+    // came with the previous chunk), by two lanes, rows lane/2 and lane/2 + 32, issued two
+    // chunks ahead: every HBM sector of the input is requested once (an unaligned 32-byte
+    // row piece touches two, and the L2 does not keep the shared one for the next chunk).
+    // Staged blocks reach at most 6 columns past the chunk: with the <= 14 un-emitted output
+    // columns the ring still holds <= 24.  Stores: whenever a row completes an
     // aligned 16-column block (64 B, every other chunk per row; 32 rows per chunk, 4 lanes
     // each) it goes out whole, so no HBM sector is left half written between groups.
     // Occupancy: at most 14 un-emitted columns + the chunk's 8 <= 24.
     auto ring_pos = [](int v) { return v >= kOutCols ? v - kOutCols : v; };
     const int cpos0 = (kOutCols - (2 * lane) % kOutCols) % kOutCols;  // column -2*lane
     const int l_row0 = lane >> 1, l_piece = lane & 1;
-    const int spos0 = ((4 * l_piece - 2 * l_row0) % kOutCols + kOutCols) % kOutCols;  // h = 0, c = 0
-    const int spos1 = ((4 * l_piece - 2 * (l_row0 + 32)) % kOutCols + kOutCols) % kOutCols;
-    const uint32_t l_off0 = (uint32_t)((b * kBand + l_row0) * w_in * 4) + 16u * l_piece - 8u * l_row0;
+    const int spos0 = ((4 * l_piece - 8 * (l_row0 >> 2)) % kOutCols + kOutCols) % kOutCols;  // h = 0, c = 0
+    const int spos1 = ((4 * l_piece - 8 * ((l_row0 + 32) >> 2)) % kOutCols + kOutCols) % kOutCols;
+    const uint32_t l_off0 = (uint32_t)((b * kBand + l_row0) * w_in * 4) + 16u * l_piece - 32u * (uint32_t)(l_row0 >> 2);
     const uint32_t l_off1 = l_off0 + 32u * (uint32_t)w_in * 4u - 256u;  // +32 rows, -64 columns
     auto load_chunk = [&](int c, uint32x4_t* L) {
       L[0] = __builtin_amdgcn_raw_buffer_load_b128(in_rs, l_row0 < rows_left ? l_off0 + 32u * c : kDrop, 0, 0);
@@ -385,11 +393,9 @@ __device__ __forceinline__ bool pred_wavefront(const Pass& P, int W, int H, int 
       const int c8 = 8 * (c % 3);
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const int pa = ring_pos((h ? spos1 : spos0) + c8);
-        const int pb = pa + 2 == kOutCols ? 0 : pa + 2;
+        const int pa = ring_pos((h ? spos1 : spos0) + c8);  // a multiple of 4 below 24: no wrap
         uint8_t* const row = slot + (l_row0 + 32 * h) * kSlotStride;
-        *reinterpret_cast<uint32x2_t*>(row + 4 * pa) = uint32x2_t{L[h][0], L[h][1]};
-        *reinterpret_cast<uint32x2_t*>(row + 4 * pb) = uint32x2_t{L[h][2], L[h][3]};
+        *reinterpret_cast<uint32x4_t*>(row + 4 * pa) = L[h];
       }
     };
     // rows completing a block after chunk c (a multiple of 16 in (8c - 2r, 8c + 8 - 2r]):
@@ -418,7 +424,7 @@ __device__ __forceinline__ bool pred_wavefront(const Pass& P, int W, int H, int 
       }
 #pragma unroll
       for (int h = 0; h < 2; ++h)
-        __builtin_amdgcn_raw_buffer_store_b128(d[h], out_rs, rok[h] && x0[h] + 3 < W ? off[h] : kDrop, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(d[h], out_rs, rok[h] && x0[h] + 3 < W ? off[h] : kDrop, 0, WG_K3_STORE_AUX);
       if (!inner) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
