@@ -49,7 +49,10 @@ static_assert(kLdsBytes + 4 * kWaves <= 160 * 1024, "K3 LDS (dynamic + the progr
 static_assert(kOutCols >= 14 + kChunk && kOutCols % 4 == 0, "row ring: 14 open columns + a chunk; 16-byte pieces never wrap");
 constexpr uint32_t kDrop = 0x80000000u;
 #ifndef WG_K3_STORE_AUX
-#define WG_K3_STORE_AUX 0  // cache policy of the output block stores (buffer aux bits; A/B builds)
+// Cache policy of the output block stores (buffer aux bits): sc1 (16) writes the lines
+// through, so they do not hold L2 capacity the input rows' lines need until their next chunk:
+// c5 reads 7.9 -> 5.7 GB per launch, K3 3.09 -> 3.04-3.06 ms (nt, 2: 5.9 GB, 3.06 ms; same call)
+#define WG_K3_STORE_AUX 16
 #endif
 constexpr int T_PRED = 0, T_CC = 1, T_AG = 2;  // 3 = color indexing
 
