@@ -1303,9 +1303,11 @@ int wg_yuv420_to_rgba_device(const uint8_t* y, const uint8_t* u, const uint8_t* 
 
 int wg_vp8l_resolve_device(const uint32_t* tokens, const uint32_t* lits, int n_lits, int n_px, int cache_bits,
                            uint32_t* argb, void* stream) {
-  if (!tokens || !argb || n_px <= 0 || n_lits < 0 || (n_lits > 0 && !lits) || cache_bits < 0 || cache_bits > 11 ||
-      (reinterpret_cast<uintptr_t>(tokens) & 15) || (reinterpret_cast<uintptr_t>(argb) & 15))
+  if (!tokens || !argb || n_px < 0 || n_lits < 0 || (n_lits > 0 && !lits) || cache_bits < 0 || cache_bits > 11 ||
+      (reinterpret_cast<uintptr_t>(tokens) & 15) || (reinterpret_cast<uintptr_t>(argb) & 15) ||
+      n_px > (INT32_MAX >> 2) || n_lits > (INT32_MAX >> 2))  // (byte offsets are 32-bit)
     return WG_STATUS_INVALID_PARAM;
+  if (n_px == 0) return WG_STATUS_OK;  // an empty stream: nothing to resolve
   wg::LLTokDesc t{};
   t.tokens = tokens;
   t.lits = lits;

@@ -216,7 +216,9 @@ int wg_yuv420_to_rgba_device(const uint8_t* y, const uint8_t* u, const uint8_t* 
  * the n_px coded ARGB pixels to `argb`.  Device pointers; tokens and argb 16-byte aligned;
  * cache_bits 0..11.  A token outside the stream's bounds (literal index >= n_lits, key >=
  * 1 << cache_bits, distance 0 or before the start) resolves to 0.  Asynchronous on `stream`.
- * Anything else -> WG_STATUS_INVALID_PARAM. */
+ * n_px = 0 is a no-op (WG_STATUS_OK).  Null / misaligned pointers, negative counts, n_px or
+ * n_lits above 2^29 - 1 (32-bit byte offsets) or cache_bits outside 0..11 ->
+ * WG_STATUS_INVALID_PARAM, checked before any device call. */
 int wg_vp8l_resolve_device(const uint32_t* tokens, const uint32_t* lits, int n_lits, int n_px,
                            int cache_bits, uint32_t* argb, void* stream);
 

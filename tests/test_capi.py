@@ -107,6 +107,29 @@ def test_yuv_stage_entry_rejects_bad_geometry_before_any_device_call():
         assert e.value.status == webp_amd.Status.INVALID_PARAM, a
 
 
+def test_resolve_stage_entry_validates_before_any_device_call():
+    """wg_vp8l_resolve_device (K7's stage entry) rejects bad arguments on the host, and an empty
+    stream is a no-op: none of these touch the device, so they run without a GPU."""
+    p = 1 << 20  # aligned dummy addresses: never dereferenced on these paths
+    bad = [
+        dict(t=0, l=p, nl=1, n=16, cb=4, o=p),            # null tokens
+        dict(t=p, l=p, nl=1, n=16, cb=4, o=0),            # null output
+        dict(t=p + 4, l=p, nl=1, n=16, cb=4, o=p),        # misaligned tokens
+        dict(t=p, l=p, nl=1, n=16, cb=4, o=p + 8),        # misaligned output
+        dict(t=p, l=0, nl=1, n=16, cb=4, o=p),            # literals announced, none given
+        dict(t=p, l=p, nl=-1, n=16, cb=4, o=p),
+        dict(t=p, l=p, nl=1, n=-1, cb=4, o=p),
+        dict(t=p, l=p, nl=1, n=16, cb=12, o=p),           # cache_bits > MAX_CACHE_BITS
+        dict(t=p, l=p, nl=1, n=16, cb=-1, o=p),
+        dict(t=p, l=p, nl=1, n=1 << 29, cb=4, o=p),       # 32-bit byte offsets
+    ]
+    for a in bad:
+        with pytest.raises(webp_amd.WebPError) as e:
+            webp_amd.vp8l_resolve_device(a["t"], a["l"], a["nl"], a["n"], a["cb"], a["o"])
+        assert e.value.status == webp_amd.Status.INVALID_PARAM, a
+    webp_amd.vp8l_resolve_device(p, 0, 0, 0, 4, p)  # empty: OK, nothing launched
+
+
 def test_go_shim_calls_only_exported_entry_points():
     """go/webp/decode_amd.go (the cgo binding a maintainer of the reference would add; no Go
     toolchain here to compile it) calls only entry points the header declares and the
