@@ -499,6 +499,7 @@ wg::LLTokDesc make_tok(const wg::LLMeta& m, const wg::StagingArena& arena, uint8
   t.n_lits = (int32_t)(m.lits.bytes / 4);
   t.cache_bits = m.cache_bits;
   t.valid = 1;
+  t.trusted = 1;  // vp8l_parse checks every literal index, cache key and distance (host/vp8l_parse.cpp)
   return t;
 }
 

@@ -310,8 +310,11 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
       const bool is_copy = kind == 2, is_cache = kind == 1;
       // out of the stream's bounds: literal index >= n_lits, key >= 1 << cache_bits, distance 0
       // or before the start ((pl - 1) >= pos, unsigned) -- one compare against a per-kind limit
-      const uint32_t lim = kind == 0 ? (uint32_t)D.n_lits : is_cache ? (uint32_t)nkeys : is_copy ? (uint32_t)(base + li) : ~0u;
-      bad |= (is_copy ? pl - 1u : pl) >= lim;
+      // (tokens of the host entropy stage are in bounds by construction: D.trusted skips this)
+      if (!D.trusted) {
+        const uint32_t lim = kind == 0 ? (uint32_t)D.n_lits : is_cache ? (uint32_t)nkeys : is_copy ? (uint32_t)(base + li) : ~0u;
+        bad |= (is_copy ? pl - 1u : pl) >= lim;
+      }
       // copies: in-block source (pl <= li), previous block (li < pl <= li + 4096), older
       const bool inb = is_copy & (pl - 1u < (uint32_t)li);  // (pl = 0 wraps: not in-block)
       const bool farc = is_copy & (pl > (uint32_t)(li + kBlock));
@@ -321,6 +324,7 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
       v[j] = lv_in[j];
       aux[j] = is_cache ? pl & (kSlots - 1) : pl;
     }
+    K7_T(8);
     if (__any(nearm != 0)) {  // copies from the previous block, in LDS
 #pragma unroll
       for (int j = 0; j < kPer; ++j) {
@@ -331,6 +335,7 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
     }
     *reinterpret_cast<uint4*>(&vcur[li0]) = make_uint4(v[0], v[1], v[2], v[3]);
     if (b > 0) store_block(b - 1, vprv);
+    K7_T(15);
     // the next blocks' inputs go out now (tk_in and lv_in are consumed)
     load_tokens(b + 2, tk_in);
     load_lits(tk_nxt, lv_nxt);
@@ -657,10 +662,10 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
   if (tid == 0) {
     k7_cnt[0] = (unsigned long long)nblocks;
     for (int i : {0, 1, 2, 3, 9, 10}) atomicAdd(&g_k7_stats[i], k7_cnt[i]);
-    for (int i : {4, 5, 6, 7, 11, 12, 13, 14}) atomicAdd(&g_k7_stats[i], k7_acc[i]);
+    for (int i : {4, 5, 6, 7, 8, 11, 12, 13, 14, 15}) atomicAdd(&g_k7_stats[i], k7_acc[i]);
   }
   if ((tid & 63) == 0)
-    for (int i : {4, 5, 6, 7, 11, 12, 13, 14}) atomicAdd(&g_k7_wave[wave][i], k7_acc[i]);
+    for (int i : {4, 5, 6, 7, 8, 11, 12, 13, 14, 15}) atomicAdd(&g_k7_wave[wave][i], k7_acc[i]);
 #endif
 }
 

@@ -82,7 +82,8 @@ struct LLTokDesc {
   const uint32_t* lits;    // n_lits literal ARGB values
   uint32_t* coded;         // n_px resolved pixels
   int32_t n_px, n_lits, cache_bits, valid;
-  int32_t pad[2];
+  int32_t trusted;  // tokens from the host entropy stage, which keeps them in bounds (no device check)
+  int32_t pad;
 };
 static_assert(sizeof(LLTokDesc) == 48, "LLTokDesc must be 48 bytes");
 

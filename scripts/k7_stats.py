@@ -28,7 +28,7 @@ def main():
     ms = b.kernel_ms()
     L.wg_debug_k7_stats(st, 1)
     blocks, serial, rounds, windows = st[0], st[1], st[2], st[3]
-    phases = ((14, "tokens (load waits)"), (4, "ranks + barrier"), (11, "registration"), (12, "lookups"), (5, "copies (rounds b)"),
+    phases = ((8, "classify (lit wait)"), (15, "prev-block copies+store"), (14, "issue next loads"), (4, "ranks + barrier"), (11, "registration"), (12, "lookups"), (5, "copies (rounds b)"),
               (13, "slot table"), (6, "serial path"), (7, "store + pipeline"))
     tot = sum(st[i] for i, _ in phases)
     print(f"frames {n}: K7 {ms[4]:.3f} ms; blocks {blocks}, windows/block {windows / blocks:.3f}, "

@@ -61,3 +61,39 @@ def test_k7_rejects_bad_params():
     import webp_amd
     with pytest.raises(webp_amd.WebPError):
         webp_amd.vp8l_resolve_device(0, 0, 0, 16, 4, 0)
+
+
+def _resolve_oob_zero(toks, lits, bits):
+    """The stage entry's documented rule for tokens the host stage never emits (literal index
+    >= n_lits, key >= 1 << cache_bits, distance 0 or before the start): the pixel resolves to 0
+    and, like any pixel, is inserted into the cache (gowebp_amd.h).  A plain loop; small n."""
+    cache = [0] * (1 << bits if bits else 1)
+    out = [0] * toks.size
+    for i, t in enumerate(toks.tolist()):
+        kind, pl = t >> 30, t & 0x3FFFFFFF
+        v = 0
+        if kind == 0:
+            v = int(lits[pl]) if pl < lits.size else 0
+        elif kind == 1:
+            v = cache[pl] if bits and pl < (1 << bits) else 0
+        elif kind == 2:
+            v = out[i - pl] if 1 <= pl <= i else 0
+        out[i] = v
+        if kind != 3 and bits:
+            cache[((v * 0x1E35A7BD) & 0xFFFFFFFF) >> (32 - bits)] = v
+    return np.asarray(out, np.uint32)
+
+
+def test_k7_untrusted_tokens_out_of_bounds():
+    """The stage entry takes caller tokens (not host-validated, unlike the batch path): literal
+    indices past n_lits, keys past the cache, distance 0 and distances before the start resolve
+    to 0 (the serial path), in several blocks and next to ordinary tokens."""
+    toks, lits = k7_streams.make_stream(3 * 4096 + 50, 6, seed=7, p_lit=0.2, p_copy=0.2, dist=(1, "near"), run=6)
+    rng = np.random.default_rng(11)
+    pos = rng.choice(np.arange(10, toks.size), size=40, replace=False)
+    for k, i in enumerate(pos.tolist()):
+        toks[i] = [(0 << 30) | (lits.size + k), (1 << 30) | (64 + k), (2 << 30) | 0, (2 << 30) | (i + 1 + k)][k % 4]
+    want = _resolve_oob_zero(toks, lits, 6)
+    got = device_resolve(toks, lits, 6)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, f"{bad.size} pixels differ, first at {bad[:5]}"
