@@ -97,3 +97,23 @@ def test_k7_untrusted_tokens_out_of_bounds():
     got = device_resolve(toks, lits, 6)
     bad = np.nonzero(got != want)[0]
     assert bad.size == 0, f"{bad.size} pixels differ, first at {bad[:5]}"
+
+
+def test_k7_random_streams():
+    """Randomised token streams (a fixed seed per case): cache sizes 0..11 bits, literal / copy
+    mixes, run lengths and distance classes drawn at random, lengths across block boundaries --
+    each bit-exact against the oracle."""
+    rng = np.random.default_rng(20261017)
+    dist_sets = [(1,), (1, "near"), ("w", "near"), ("far", 1), (4096, 4097, "near"), (1, 2, 3, 4)]
+    for case in range(24):
+        bits = int(rng.integers(0, 12))
+        n = int(rng.integers(1, 3 * 4096 + 200))
+        kw = dict(p_lit=float(rng.uniform(0.01, 0.6)), p_copy=float(rng.uniform(0.0, 0.4)),
+                  dist=dist_sets[int(rng.integers(len(dist_sets)))], run=int(rng.integers(1, 64)),
+                  palette=int(rng.integers(2, 3000)), width=int(rng.integers(16, 2048)),
+                  p_empty=float(rng.choice([0.0, 0.0, 0.002])))
+        toks, lits = k7_streams.make_stream(n, bits, seed=1000 + case, **kw)
+        want = oracle_resolve(toks, lits, bits)
+        got = device_resolve(toks, lits, bits)
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, f"case {case} (n={n}, bits={bits}, {kw}): {bad.size} pixels differ, first at {bad[:5]}"
