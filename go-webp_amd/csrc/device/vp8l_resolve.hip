@@ -41,7 +41,9 @@
 // masks.  A window with a bad token, a lookup of a never-written slot k != 0, or too many
 // rounds is redone, with the rest of its block, exactly in scan order by one lane (the
 // reference loop over the same LDS table): always correct, slow, never taken by encoder
-// output so far.
+// output so far.  (Bad tokens -- out-of-range literal index, key or distance -- are only
+// checked for caller streams of the stage entry; the host entropy stage's streams are in
+// bounds by construction, LLTokDesc::trusted.)
 //
 // Latency: tokens are loaded two blocks ahead and literal values one block ahead, so a block
 // waits on HBM only for copies that reach back more than one block.
@@ -81,8 +83,10 @@ __device__ __forceinline__ int count_below(uint64_t m) {
 // cycles per phase.
 #ifdef WG_K7_STATS
 // counts: 0 blocks, 1 serial windows, 2 rounds, 3 windows, 9 empty-slot lookups, 10 round caps;
-// wave 0's cycles: 14 tokens (waits for the prefetched loads), 4 ranks + barrier, 11 registration, 12 lookups, 5 copies (rounds b), 13 slot
-// table, 6 serial path, 7 stores + pipeline
+// each wave's cycles: 8 token classification (waits for the prefetched literal values), 15
+// previous-block copies + the previous block's store, 14 the next blocks' loads, 4 ranks +
+// barrier, 11 registration, 12 lookups, 5 copies (rounds b), 13 slot table, 6 serial path,
+// 7 end of block
 __device__ unsigned long long g_k7_stats[16];
 __device__ unsigned long long g_k7_wave[kWaves][16];  // per wave (lane 0): the same phase cycles
 #define K7_T(i)                                                      \
