@@ -126,7 +126,9 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
   __shared__ uint8_t st[kBlock];                 // kKnown / kPendCopy / kPendLookup
   __shared__ __attribute__((aligned(16))) uint32_t wsum[kWaves];  // updaters per wave of the block
   __shared__ int first_pend[2];                  // per round parity: first pending copy (local)
-  __shared__ int slow;                           // this window goes serial
+  // this window goes serial; one flag per block parity: with no barrier at a block's end, a
+  // wave already in block b+1 may raise its flag while a slower one has yet to read block b's
+  __shared__ int slow[2];
   __shared__ int orflag[4];                      // sync_or: a ring of flag words
   __shared__ uint2 sscr[kWaves * 64];            // a wave's straddling lookups, compacted (key, rank)
   const LLTokDesc D = kSingle ? single : descs[blockIdx.x];
@@ -153,7 +155,7 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
   }
   if (tid < kSlots / 32) slot_set[tid] = 0;
   if (tid == 0) {
-    slow = 0;
+    slow[0] = slow[1] = 0;
     first_pend[0] = first_pend[1] = kBlock;
   }
   if (tid < 4) orflag[tid] = 0;
@@ -346,7 +348,7 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
     K7_T(14);
     if (bad) {
       if (err) atomicOr(err, 4);
-      slow = 1;
+      slow[b & 1] = 1;
     }
     // ranks: updaters before each pixel, a block-wide prefix count (per-thread count 0..4 in
     // three ballots).  wsum: the wave's updaters, bit 16 a copy reaching back past the last
@@ -527,7 +529,7 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
               const uint32_t k = aux[j];
               if ((empty >> j) & 1u && !((slot_set[k >> 5] >> (k & 31)) & 1u)) {
                 K7_COUNT(9, 1);
-                slow = 1;
+                slow[b & 1] = 1;
               }
             }
           }
@@ -550,7 +552,7 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
         K7_COUNT(2, 1);
         if (r == kMaxRounds) {
           K7_COUNT(10, 1);
-          slow = 1;
+          slow[b & 1] = 1;
           break;  // uniform: any_pc and r are the same in every thread
         }
         const int fp = any_pc ? first_pend[r & 1] : kBlock;
@@ -591,7 +593,7 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
         K7_T(5);
       }
       __syncthreads();  // every lookup has read the slot table; the masks are complete
-      const bool go_serial = slow != 0;
+      const bool go_serial = slow[b & 1] != 0;
       // ---- 3. each key's last updater writes its slot and clears the key's masks
       if (in_win && nkeys) {
         if (!wave_pc) {
@@ -613,7 +615,10 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
         __syncthreads();
         break;
       }
-      __syncthreads();
+      // between windows: the next window's registration follows this one's slot table.  After
+      // the last window no barrier: the next block's rank barrier orders this slot table before
+      // its registration, and nothing before that barrier touches the table, the masks or uval
+      if (q + 1 < nwin) __syncthreads();
       K7_T(13);
     }
     K7_T(5);
@@ -650,7 +655,7 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
           }
           vcur[li] = x;
         }
-        slow = 0;
+        slow[b & 1] = 0;
       }
       __syncthreads();
     }
