@@ -541,7 +541,15 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
           }
       };
       // ---- rounds (one when the window has no pending copy: every lookup resolves in (a))
-      int any_pc = sync_or(pc);
+      // (one window: every thread is in it, so "any pending copy" is the block's flag from the
+      // rank barrier, and a plain barrier orders the registrations before the lookups)
+      int any_pc;
+      if (nwin == 1) {
+        __syncthreads();
+        any_pc = blk_pc;
+      } else {
+        any_pc = sync_or(pc);
+      }
       K7_T(11);
       if (!any_pc) {
         K7_COUNT(2, 1);
