@@ -37,6 +37,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 WORKLOADS = {
     "c2": dict(prefix="c2_1080p", name="c2_1080p_x256", desc="1920x1080 VP8-lossy (deblock on), batch 256"),
     "c3": dict(prefix="c3_4k", name="c3_4k_deblock_x256", desc="3840x2160 VP8-lossy, deblock on, batch 256"),
+    "c3s": dict(prefix="c3s_4k", name="c3s_4k_deblock_x256",
+                desc="3840x2160 VP8-lossy, sigma 18 (~2 bpp: SURVEY 8(d)'s entropy-stress variant of C3), deblock on, "
+                     "batch 256"),
     "c5": dict(prefix="c5_ll2048", name="c5_ll2048_x256",
                desc="2048x2048 VP8L lossless (predictor + cross-color + subtract-green + color cache), batch 256"),
 }
@@ -217,6 +220,99 @@ def cpu_baseline_parallel(datas, seconds, threads):
                        f"(entropy stage + oracle/ CPU restatement), {el:.1f}s")
 
 
+# ------------------------------------------------------------------------------- host cores
+def host_cpus():
+    """CPUs this job may use: the affinity mask, bounded by the cgroup's CPU quota (a GPU box
+    grants a share of a larger machine: os.cpu_count() shows the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def rank_host_threads(requested, world):
+    """Entropy-stage threads of one rank: --host-threads, capped at the job's CPUs / ranks."""
+    return max(1, min(requested, 64, host_cpus() // max(1, world)))
+
+
+def host_info(world, threads):
+    try:
+        nproc = int(subprocess.run(["nproc"], capture_output=True, text=True, timeout=10).stdout.strip())
+    except Exception:
+        nproc = None
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"nproc": nproc, "os_cpu_count": os.cpu_count(), "job_cpus": host_cpus(),
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"), "cpu_model": model, "ranks": world,
+            "host_threads_per_rank": threads}
+
+
+def end_to_end(args, ctx, b, frames, dist, barrier, px_rank, threads):
+    """Host bitstreams in, host RGBA out, on EVERY rank at once (each its own shard and GPU):
+    entropy stage on the rank's host threads + H2D + kernels + D2H, pipelined in chunks
+    (wg_decode_rgba_batch).  Outputs allocated outside the timing: page-locked (written by
+    DMA, the `end_to_end` figure) and pageable numpy memory (`end_to_end_pageable`).  Whole-job
+    value = all ranks' pixels / the slowest rank's time; best of two calls (the first also grows
+    the context's pinned staging and device buffers)."""
+    res = {}
+    for kind in ("pinned", "pageable"):
+        if args.mock:
+            outs = None
+        elif kind == "pinned":
+            import webp_amd
+            outs = [webp_amd.pinned_empty((b.dims(i)[1], b.dims(i)[0], 4)) for i in range(b.n)]
+        else:
+            outs = [np.empty((b.dims(i)[1], b.dims(i)[0], 4), np.uint8) for i in range(b.n)]
+            for o in outs:
+                o.fill(0)  # fault the pages in outside the timing
+        runs = []
+        for _ in range(2):
+            barrier()
+            t_e = time.perf_counter()
+            ctx.decode_batch(frames, out=outs)
+            t_e = time.perf_counter() - t_e
+            t_max, px = reduce_job(dist, "cpu", t_e, px_rank)
+            runs.append((t_max, t_e, ctx.pipeline_stats().as_dict()))
+        t_max, t_mine, ps = min(runs, key=lambda r: r[0])
+        world = 1 if dist is None else dist.get_world_size()
+        res[kind] = {"value": round(px / t_max / 1e6, 1), "unit": "MPix/s", "n_gpus": world,
+                     "seconds": round(t_max, 4), "seconds_first_call": round(runs[0][0], 4),
+                     "host_threads_per_rank": threads, "output_memory": kind,
+                     "breakdown_rank0": {k: (round(v, 4) if isinstance(v, float) else v) for k, v in ps.items()},
+                     "note": "host entropy stage + H2D + kernels + D2H, pipelined in chunks on every rank; "
+                             "host-bound; not the headline value"}
+        del outs
+    return res
+
+
+class _MockContext:
+    """--mock: stand-in for webp_amd.Context's end-to-end entry."""
+
+    def decode_batch(self, frames, out=None):
+        time.sleep(0.003)
+
+    def pipeline_stats(self):
+        class _PS:
+            def as_dict(self):
+                return {"chunks": 1, "wall_s": 0.003}
+        return _PS()
+
+    def close(self):
+        pass
+
+
 # ------------------------------------------------------------------------------- one rank
 class _MockBatch:
     """--mock (CPU tests of the launcher): a stand-in for webp_amd.Batch that sleeps instead of
@@ -249,7 +345,8 @@ def main():
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (host in, host out) leg")
     ap.add_argument("--emit", choices=("fused", "separate"), default="fused",
                     help="lossy RGBA from K1's tail (default) or a separate K2 launch")
-    ap.add_argument("--host-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
+    ap.add_argument("--host-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")),
+                    help="entropy-stage threads per rank, capped at the job's host CPUs / ranks")
     ap.add_argument("--mock", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
@@ -275,15 +372,16 @@ def main():
 
     wl = WORKLOADS[args.workload]
     if args.mock:
-        datas, bpp = [b"mock"], 0.0
-        b, ctx, t_prep, stream = _MockBatch(), None, 0.0, None
+        datas, bpp = _load_frames(wl["prefix"])  # (the CPU baseline legs still run for real)
+        b, ctx, t_prep, stream = _MockBatch(), _MockContext(), 0.0, None
+        frames, ctx_threads = None, rank_host_threads(args.host_threads, world)
         sync = lambda: None  # noqa: E731
     else:
         import webp_amd
         torch.cuda.set_device(local)
         datas, bpp = _load_frames(wl["prefix"])
         frames = shard_frames(datas, rank, args.batch)
-        ctx_threads = max(1, min(args.host_threads, 64))
+        ctx_threads = rank_host_threads(args.host_threads, world)
         ctx = webp_amd.Context(local, host_threads=ctx_threads)
         t_prep = time.perf_counter()
         b = ctx.batch(frames)
@@ -322,6 +420,9 @@ def main():
         stage_ms = b.kernel_ms()[1]
     px_rank = b.pixels
     dt, total_px = reduce_job(dist, "cpu", dt, px_rank * args.steps)
+    e2e = None
+    if not args.no_e2e:
+        e2e = end_to_end(args, ctx, b, frames if not args.mock else None, dist, barrier, px_rank, ctx_threads)
     value = total_px / dt / 1e6
     ranks = [(rank, local, os.getpid())]
     if dist is not None:
@@ -376,37 +477,27 @@ def main():
             out["mock"] = True
         if "yuv_to_rgba_kernel" in roofs:
             out["roofline_yuv_to_rgba"] = roofs["yuv_to_rgba_kernel"]
-        if not args.no_e2e and not args.mock:
-            # secondary figure: host bitstreams in, host RGBA out (entropy stage on the context's
-            # host threads + H2D + kernels + D2H into pageable numpy buffers allocated outside the
-            # timing).  The first call also grows the context's pinned staging and device buffers.
-            outs = [np.empty((b.dims(i)[1], b.dims(i)[0], 4), np.uint8) for i in range(b.n)]
-            runs = []
-            for _ in range(2):
-                t_e = time.perf_counter()
-                ctx.decode_batch(frames, out=outs)
-                runs.append(time.perf_counter() - t_e)
-            t_e = min(runs)
-            out["end_to_end"] = {"value": round(px_rank / t_e / 1e6, 1), "unit": "MPix/s", "n_gpus": 1,
-                                 "seconds": round(t_e, 3), "seconds_first_call": round(runs[0], 3),
-                                 "host_threads": ctx_threads,
-                                 "note": "one batch: host entropy stage + H2D + kernels + D2H (pageable), "
-                                         "host-bound; not the headline value"}
-            del outs
-        if world == 1 and not args.no_cpu_baseline and not args.mock:
+        if e2e is not None:
+            out["end_to_end"] = e2e["pinned"]
+            out["end_to_end_pageable"] = e2e["pageable"]
+        out["host"] = host_info(world, ctx_threads)
+        if not args.no_cpu_baseline:
+            # rank 0 only, on the host cores of this job; the other ranks wait at the final barrier
             cb = cpu_baseline(datas, args.cpu_seconds)
             out["cpu_baseline"] = cb
             out["speedup_vs_cpu_baseline"] = round(value / cb["value"], 1)
             cbd = cpu_baseline_dsp(datas, max(2.0, args.cpu_seconds / 2))
             out["cpu_baseline_dsp"] = cbd
             out["speedup_vs_cpu_dsp"] = round(value / cbd["value"], 1)
-            threads = max(1, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)))
+            threads = max(1, min(64, host_cpus()))  # every CPU of the job
             cba = cpu_baseline_parallel(datas, max(2.0, args.cpu_seconds / 2), threads)
             out["cpu_baseline_all_cores"] = cba
             out["speedup_vs_cpu_all_cores"] = round(value / cba["value"], 1)
             if "end_to_end" in out:
                 out["end_to_end"]["vs_cpu_all_cores"] = round(out["end_to_end"]["value"] / cba["value"], 2)
+                out["end_to_end"]["vs_cpu_1_core"] = round(out["end_to_end"]["value"] / cb["value"], 1)
         print(json.dumps(out), flush=True)
+    barrier()
     b.close()
     if ctx is not None:
         ctx.close()

@@ -10,7 +10,9 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <climits>
+#include <condition_variable>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -36,10 +38,36 @@ namespace {
 
 // Device buffers of finished batches, kept for the next batch of the context (the single-frame
 // and one-shot batch entry points create and destroy a batch per call).  Best fit among
-// buffers at most ~2x the request; beyond kMaxCached bytes the largest are freed.
+// buffers at most ~2x the request.  A context keeps at most a quarter of its device's memory
+// (and never more than kMaxCached) in idle buffers; when hipMalloc fails, EVERY context's cache
+// on that device is emptied before the one retry, so idle buffers of one context never starve
+// another's batch.
+class DeviceCache;
+std::mutex g_caches_mu;
+std::vector<DeviceCache*>* g_caches = new std::vector<DeviceCache*>();  // (never destroyed: exit order)
+void trim_device_caches(int device);
+
 class DeviceCache {
  public:
-  ~DeviceCache() { trim(0); }
+  DeviceCache() = default;
+  ~DeviceCache() {
+    {
+      std::lock_guard<std::mutex> lock(g_caches_mu);
+      auto& v = *g_caches;
+      v.erase(std::remove(v.begin(), v.end(), this), v.end());
+    }
+    trim(0);
+  }
+  // bind to a device (hipSetDevice(device) done by the caller): the idle-memory cap
+  void init(int device) {
+    device_ = device;
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && total_b > 0) cap_ = std::min(kMaxCached, total_b / 4);
+    (void)hipGetLastError();
+    std::lock_guard<std::mutex> lock(g_caches_mu);
+    g_caches->push_back(this);
+  }
+  int device() const { return device_; }
   void* get(size_t bytes) {
     bytes = std::max<size_t>(bytes, 256);
     {
@@ -59,7 +87,7 @@ class DeviceCache {
     void* p = nullptr;
     if (hipMalloc(&p, bytes) != hipSuccess) {
       (void)hipGetLastError();
-      trim(0);  // make room and try once more
+      trim_device_caches(device_);  // make room (every context on this device) and try once more
       if (hipMalloc(&p, bytes) != hipSuccess) {
         (void)hipGetLastError();
         return nullptr;
@@ -78,7 +106,7 @@ class DeviceCache {
         cached_ += caps_[i].cap;
         break;
       }
-    trim_locked(kMaxCached);
+    trim_locked(cap_);
   }
   void trim(size_t keep) {
     std::lock_guard<std::mutex> lock(mu_);
@@ -107,7 +135,15 @@ class DeviceCache {
   std::mutex mu_;
   std::vector<Entry> free_, caps_;  // free list; every buffer this cache allocated (and its size)
   size_t cached_ = 0;
+  size_t cap_ = size_t(8) << 30;  // until init() reads the device's memory
+  int device_ = 0;
 };
+
+void trim_device_caches(int device) {
+  std::lock_guard<std::mutex> lock(g_caches_mu);
+  for (DeviceCache* c : *g_caches)
+    if (c->device() == device) c->trim(0);
+}
 
 void* pinned_alloc(size_t bytes) {
   void* p = nullptr;
@@ -125,10 +161,16 @@ struct wg_ctx {
   int device = 0;
   int host_threads = 1;
   hipStream_t stream = nullptr;
-  std::mutex mu;  // one batch creation at a time (the arena and the pool are shared)
+  std::mutex mu;  // one batch creation (or pipelined decode) at a time: arenas and pool are shared
   std::unique_ptr<wg::WorkerPool> pool;
   std::unique_ptr<wg::StagingArena> arena;
   DeviceCache cache;
+  // the pipelined decode (wg_decode_rgba_batch): a second staging arena and stream, so chunk
+  // k + 1's entropy stage and upload overlap chunk k's kernels and download
+  std::unique_ptr<wg::StagingArena> arena2;
+  hipStream_t stream2 = nullptr;
+  int chunk_frames = 0;  // frames per pipeline chunk, 0 = automatic (wg_ctx_set_chunk_frames)
+  wg_pipeline_stats stats{};  // of the last pipelined decode
   wg::WorkerPool* workers() {
     if (!pool) pool.reset(new wg::WorkerPool(host_threads));
     return pool.get();
@@ -186,20 +228,28 @@ struct wg_batch {
   double k1_fused_bytes = 0;  // K1 with its RGBA tail: inputs + RGBA (planes are an intermediate)
   std::vector<Timing> timings;  // one per run since the last query
   size_t n_runs_pending = 0;
-  hipEvent_t done = nullptr;    // recorded after the batch's latest work, on the stream it ran on
-  bool done_recorded = false;
+  hipStream_t home = nullptr;   // the batch's own stream: uploads, downloads (the context's by default)
+  // one event per stream the batch's work was queued on, recorded after its latest work there:
+  // batch_wait waits for all of them, so runs on several user streams are all complete before
+  // the buffers go back to the cache
+  std::vector<std::pair<hipStream_t, hipEvent_t>> done;
 };
 
 namespace {
 // The single-frame entry points share one lazily created context (device 0 unless
-// wg_set_default_device chose another).
+// wg_set_default_device chose another).  Held by shared_ptr for the length of each call, so
+// wg_set_default_device can replace it while calls are in flight: the old context is destroyed
+// when its last call returns.  (The holder itself is never destroyed: no HIP work at exit.)
 std::mutex g_default_mu;
-wg_ctx* g_default_ctx = nullptr;
+std::shared_ptr<wg_ctx>* g_default_ctx = new std::shared_ptr<wg_ctx>();
 int g_default_device = 0;
-wg_ctx* default_ctx() {
+std::shared_ptr<wg_ctx> default_ctx() {
   std::lock_guard<std::mutex> lock(g_default_mu);
-  if (!g_default_ctx) g_default_ctx = wg_ctx_create(g_default_device, 0);
-  return g_default_ctx;
+  if (!*g_default_ctx) {
+    wg_ctx* c = wg_ctx_create(g_default_device, 0);
+    if (c) g_default_ctx->reset(c, wg_ctx_destroy);
+  }
+  return *g_default_ctx;
 }
 
 void fill_vp8l_info(const wg::VP8LFrame& f, wg_vp8l_info* info, uint32_t* tokens, uint32_t* literals,
@@ -335,15 +385,31 @@ namespace {
 wg_batch* batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t* sizes, int n,
                        const wg_decoder_options* opt, int32_t* status);
 
-// Wait for everything the batch has queued (its latest run on whatever stream it ran on, and
-// the context stream) -- stream-scoped, so other contexts on the device are not serialised.
+// Wait for everything the batch has queued (its home stream and its latest work on every stream
+// it ran on) -- stream-scoped, so other contexts on the device are not serialised.
 hipError_t batch_wait(wg_batch* b) {
-  hipError_t e = hipStreamSynchronize(b->ctx->stream);
-  if (e == hipSuccess && b->done_recorded) e = hipEventSynchronize(b->done);
+  hipError_t e = b->home ? hipStreamSynchronize(b->home) : hipSuccess;
+  for (auto& d : b->done)
+    if (e == hipSuccess) e = hipEventSynchronize(d.second);
   return e;
 }
-void batch_mark_done(wg_batch* b, hipStream_t s) {
-  if (b->done && hipEventRecord(b->done, s) == hipSuccess) b->done_recorded = true;
+// Record the batch's latest work on stream s (the event of that stream, created on first use).
+hipError_t batch_mark_done(wg_batch* b, hipStream_t s) {
+  if (s == b->home) return hipSuccess;  // batch_wait synchronises the home stream itself
+  for (auto& d : b->done)
+    if (d.first == s) return hipEventRecord(d.second, s);
+  hipEvent_t ev = nullptr;
+  hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+  if (e != hipSuccess) return e;
+  b->done.emplace_back(s, ev);
+  return hipEventRecord(ev, s);
+}
+// hipSetDevice with its failure reported (a wrong device would otherwise surface later as a
+// generic launch failure)
+bool set_device(int device) {
+  if (hipSetDevice(device) == hipSuccess) return true;
+  (void)hipGetLastError();
+  return false;
 }
 }  // namespace
 
@@ -352,7 +418,7 @@ extern "C" {
 wg_ctx* wg_ctx_create(int device, int host_threads) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return nullptr;
-  if (hipSetDevice(device) != hipSuccess) return nullptr;
+  if (!set_device(device)) return nullptr;
   wg_ctx* c = new (std::nothrow) wg_ctx();
   if (!c) return nullptr;
   c->device = device;
@@ -367,48 +433,44 @@ wg_ctx* wg_ctx_create(int device, int host_threads) {
     delete c;
     return nullptr;
   }
+  c->cache.init(device);
   return c;
 }
 
 void wg_ctx_destroy(wg_ctx* c) {
   if (!c) return;
-  {
-    std::lock_guard<std::mutex> lock(g_default_mu);
-    if (c == g_default_ctx) g_default_ctx = nullptr;
-  }
-  hipSetDevice(c->device);
-  if (c->stream) hipStreamSynchronize(c->stream);
+  const bool dev_ok = set_device(c->device);
+  if (dev_ok && c->stream) hipStreamSynchronize(c->stream);
+  if (dev_ok && c->stream2) hipStreamSynchronize(c->stream2);
   c->pool.reset();
   c->arena.reset();
+  c->arena2.reset();
   c->cache.trim(0);
   if (c->stream) hipStreamDestroy(c->stream);
+  if (c->stream2) hipStreamDestroy(c->stream2);
   delete c;
 }
 
 int wg_set_default_device(int device) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return WG_STATUS_INVALID_PARAM;
-  wg_ctx* old = nullptr;
+  std::shared_ptr<wg_ctx> old;
   {
     std::lock_guard<std::mutex> lock(g_default_mu);
-    if (g_default_ctx && g_default_ctx->device != device) {
-      old = g_default_ctx;
-      g_default_ctx = nullptr;
-    }
+    if (*g_default_ctx && (*g_default_ctx)->device != device) old.swap(*g_default_ctx);
     g_default_device = device;
   }
-  if (old) wg_ctx_destroy(old);
+  // `old` is destroyed here if no call holds it, else when the last one in flight returns
   return WG_STATUS_OK;
 }
 
 void wg_batch_destroy(wg_batch* b) {
   if (!b) return;
-  hipSetDevice(b->ctx->device);
-  batch_wait(b);  // nothing may still use the buffers handed back to the cache
+  if (set_device(b->ctx->device)) batch_wait(b);  // nothing may still use the buffers handed back to the cache
   for (auto& t : b->timings)
     for (auto& e : t.ev)
       if (e) hipEventDestroy(e);
-  if (b->done) hipEventDestroy(b->done);
+  for (auto& d : b->done) hipEventDestroy(d.second);
   DeviceCache& c = b->ctx->cache;
   c.put(b->d_desc);
   c.put(b->d_lldesc);
@@ -514,22 +576,24 @@ double ll_bytes(const wg::LLMeta& m) {
   return bytes;
 }
 
-wg_batch* batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t* sizes, int n,
-                       const wg_decoder_options* opt, int32_t* status) {
+using BatchPtr = std::unique_ptr<wg_batch, BatchDeleter>;
+
+// Host half of a batch: every frame's host stages into `arena` (on the context's pool; the
+// caller holds ctx->mu), the layout of the planes / RGBA and the algorithmic bytes per kernel.
+// status[i] = frame i's status.  Nothing touches the device.
+BatchPtr batch_parse(wg_ctx* ctx, wg::StagingArena& arena, hipStream_t home, const uint8_t* const* data,
+                     const size_t* sizes, int n, const wg_decoder_options* opt, int32_t* status) {
   if (status)
     for (int i = 0; i < n; ++i) status[i] = WG_STATUS_OK;
-  std::lock_guard<std::mutex> lock(ctx->mu);
-  if (hipSetDevice(ctx->device) != hipSuccess) return nullptr;
-  std::unique_ptr<wg_batch, BatchDeleter> bp(new wg_batch());
+  BatchPtr bp(new wg_batch());
   wg_batch* b = bp.get();
   b->ctx = ctx;
+  b->home = home;
   b->n = n;
   b->opt = *opt;
   const int32_t flags = (opt->bypass_filtering ? WG_FLAG_BYPASS_FILTERING : 0) |
                         (opt->no_fancy_upsampling ? WG_FLAG_NO_FANCY_UPSAMPLING : 0);
   b->flags = flags;
-  if (hipEventCreateWithFlags(&b->done, hipEventDisableTiming) != hipSuccess) b->done = nullptr;
-  wg::StagingArena& arena = *ctx->arena;
   arena.begin_batch();
   wg::parse_all(data, sizes, n, *opt, ctx->workers(), &arena, b->fp);
   b->in_bytes = std::max<size_t>(arena.layout(), kAlign);
@@ -629,12 +693,18 @@ wg_batch* batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t* si
   b->kbytes[4] = k7;
   b->plane_bytes = std::max<size_t>(pl_b, kAlign);
   b->rgba_bytes = std::max<size_t>(rg_b, kAlign);
-  auto fail = [&](int st) {
-    if (status)
-      for (int i = 0; i < n; ++i)
-        if (status[i] == WG_STATUS_OK) status[i] = st;
-    return (wg_batch*)nullptr;  // bp's deleter hands every buffer back
-  };
+  return bp;
+}
+
+// Device half: buffers (from the context's cache), descriptors, and the H2D copies of the staged
+// inputs, all queued on the batch's home stream; the arena may be reused once they complete.
+// OUT_OF_MEMORY if a buffer or a copy could not be had (the batch then holds what it got: its
+// deleter hands it back).
+int batch_upload(wg_batch* b, const wg::StagingArena& arena) {
+  wg_ctx* ctx = b->ctx;
+  const int n = b->n;
+  const int32_t flags = b->flags;
+  const hipStream_t home = b->home;
   DeviceCache& cache = ctx->cache;
   b->d_in = static_cast<uint8_t*>(cache.get(b->in_bytes));
   b->d_planes = static_cast<uint8_t*>(cache.get(b->plane_bytes));
@@ -645,8 +715,8 @@ wg_batch* batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t* si
   b->d_adesc = static_cast<AlphaDesc*>(cache.get(sizeof(AlphaDesc) * (size_t)std::max(b->n_alpha, 1)));
   b->d_err = static_cast<int*>(cache.get(sizeof(int)));
   if (!b->d_in || !b->d_planes || !b->d_rgba || !b->d_desc || !b->d_lldesc || !b->d_tokdesc || !b->d_adesc || !b->d_err ||
-      hipMemsetAsync(b->d_err, 0, sizeof(int), ctx->stream) != hipSuccess)
-    return fail(WG_STATUS_OUT_OF_MEMORY);
+      hipMemsetAsync(b->d_err, 0, sizeof(int), home) != hipSuccess)
+    return WG_STATUS_OUT_OF_MEMORY;
   b->desc.assign((size_t)n, FrameDesc{});
   for (int i = 0; i < n; ++i) {
     FrameParse& f = b->fp[(size_t)i];
@@ -727,35 +797,59 @@ wg_batch* batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t* si
   hipError_t e = hipSuccess;
   for (size_t c = 0; c < arena.n_chunks() && e == hipSuccess; ++c) {
     const wg::StagingArena::Chunk& ch = arena.chunk(c);
-    if (ch.used) e = hipMemcpyAsync(b->d_in + ch.dev_base, ch.p, ch.used, hipMemcpyHostToDevice, ctx->stream);
+    if (ch.used) e = hipMemcpyAsync(b->d_in + ch.dev_base, ch.p, ch.used, hipMemcpyHostToDevice, home);
   }
   if (e == hipSuccess && b->any_crop) {
     b->d_desc2 = static_cast<FrameDesc*>(cache.get(sizeof(FrameDesc) * (size_t)n));
     e = b->d_desc2 ? hipMemcpyAsync(b->d_desc2, b->desc2.data(), sizeof(FrameDesc) * (size_t)n, hipMemcpyHostToDevice,
-                                    ctx->stream)
+                                    home)
                    : hipErrorOutOfMemory;
   }
   if (e == hipSuccess)
     e = hipMemcpyAsync(b->d_desc, b->desc.data(), sizeof(FrameDesc) * (size_t)n, hipMemcpyHostToDevice,
-                       ctx->stream);
+                       home);
   // K3 launches one kernel per variant over a contiguous group of descriptors
   std::stable_sort(b->lldesc.begin(), b->lldesc.end(),
                    [](const LLDesc& a, const LLDesc& c) { return a.pad1[0] < c.pad1[0]; });
   for (const LLDesc& l : b->lldesc) b->ll_groups[l.pad1[0]]++;
   if (e == hipSuccess && !b->lldesc.empty())
     e = hipMemcpyAsync(b->d_lldesc, b->lldesc.data(), sizeof(LLDesc) * b->lldesc.size(), hipMemcpyHostToDevice,
-                       ctx->stream);
+                       home);
   if (e == hipSuccess && !b->tokdesc.empty())
     e = hipMemcpyAsync(b->d_tokdesc, b->tokdesc.data(), sizeof(wg::LLTokDesc) * b->tokdesc.size(),
-                       hipMemcpyHostToDevice, ctx->stream);
+                       hipMemcpyHostToDevice, home);
   if (e == hipSuccess && !b->adesc.empty())
     e = hipMemcpyAsync(b->d_adesc, b->adesc.data(), sizeof(AlphaDesc) * b->adesc.size(), hipMemcpyHostToDevice,
-                       ctx->stream);
-  // the staging memory is reused by the next batch: the copies complete here
-  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+                       home);
   if (e != hipSuccess) {
     (void)hipGetLastError();
-    return fail(WG_STATUS_OUT_OF_MEMORY);
+    return WG_STATUS_OUT_OF_MEMORY;
+  }
+  return WG_STATUS_OK;
+}
+
+wg_batch* batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t* sizes, int n,
+                       const wg_decoder_options* opt, int32_t* status) {
+  if (status)
+    for (int i = 0; i < n; ++i) status[i] = WG_STATUS_OK;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  if (!set_device(ctx->device)) {
+    if (status)
+      for (int i = 0; i < n; ++i) status[i] = WG_STATUS_INVALID_PARAM;
+    return nullptr;
+  }
+  BatchPtr bp = batch_parse(ctx, *ctx->arena, ctx->stream, data, sizes, n, opt, status);
+  int st = batch_upload(bp.get(), *ctx->arena);
+  // the staging memory is reused by the next batch: the copies complete here
+  if (st == WG_STATUS_OK && hipStreamSynchronize(ctx->stream) != hipSuccess) {
+    (void)hipGetLastError();
+    st = WG_STATUS_OUT_OF_MEMORY;
+  }
+  if (st != WG_STATUS_OK) {
+    if (status)
+      for (int i = 0; i < n; ++i)
+        if (status[i] == WG_STATUS_OK) status[i] = st;
+    return nullptr;  // bp's deleter hands every buffer back
   }
   return bp.release();
 }
@@ -766,8 +860,8 @@ extern "C" {
 int wg_batch_run(wg_batch* b, void* stream) {
   if (!b) return WG_STATUS_INVALID_PARAM;
   if (b->n_valid == 0) return WG_STATUS_OK;
-  hipSetDevice(b->ctx->device);
-  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : b->ctx->stream;
+  if (!set_device(b->ctx->device)) return WG_STATUS_INVALID_PARAM;
+  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : b->home;
   if (b->n_runs_pending >= b->timings.size()) {
     Timing t;
     for (auto& e : t.ev)
@@ -828,8 +922,7 @@ int wg_batch_run(wg_batch* b, void* stream) {
     if (e != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
   }
   hipEventRecord(t.ev[kStages], s);
-  batch_mark_done(b, s);
-  return WG_STATUS_OK;
+  return batch_mark_done(b, s) == hipSuccess ? WG_STATUS_OK : WG_STATUS_OUT_OF_MEMORY;
 }
 
 int wg_batch_kernel_ms(const wg_batch* bc, float* ms, int n_ms) {
@@ -874,18 +967,18 @@ int wg_batch_set_emit(wg_batch* b, int separate) {
   b->fused = !separate;
   for (FrameDesc& d : b->desc)
     if (d.valid) d.flags = b->fused ? (d.flags | wg::kFrameEmitRgba) : (d.flags & ~wg::kFrameEmitRgba);
-  hipSetDevice(b->ctx->device);
+  if (!set_device(b->ctx->device)) return WG_STATUS_INVALID_PARAM;
   hipError_t e = hipMemcpyAsync(b->d_desc, b->desc.data(), sizeof(FrameDesc) * (size_t)b->n, hipMemcpyHostToDevice,
-                                b->ctx->stream);
-  if (e == hipSuccess) e = hipStreamSynchronize(b->ctx->stream);
+                                b->home);
+  if (e == hipSuccess) e = hipStreamSynchronize(b->home);
   return e == hipSuccess ? WG_STATUS_OK : WG_STATUS_USER_ABORT;
 }
 
 int wg_batch_run_emit(wg_batch* b, void* stream) {
   if (!b) return WG_STATUS_INVALID_PARAM;
   if (b->n_lossy == 0 || b->any_crop) return WG_STATUS_OK;
-  hipSetDevice(b->ctx->device);
-  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : b->ctx->stream;
+  if (!set_device(b->ctx->device)) return WG_STATUS_INVALID_PARAM;
+  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : b->home;
   if (b->n_runs_pending >= b->timings.size()) {
     Timing t;
     for (auto& e : t.ev)
@@ -899,8 +992,8 @@ int wg_batch_run_emit(wg_batch* b, void* stream) {
   hipError_t e = wg::launch_yuv_to_rgba(b->d_desc, nullptr, b->n, b->max_out_w, b->max_out_h,
                                         (b->flags & WG_FLAG_NO_FANCY_UPSAMPLING) ? 0 : 1, s);
   for (int k = kStageK2 + 1; k <= kStages; ++k) hipEventRecord(t.ev[k], s);
-  batch_mark_done(b, s);
-  return e == hipSuccess ? WG_STATUS_OK : WG_STATUS_UNSUPPORTED_FEATURE;
+  if (e != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
+  return batch_mark_done(b, s) == hipSuccess ? WG_STATUS_OK : WG_STATUS_OUT_OF_MEMORY;
 }
 
 int wg_batch_size(const wg_batch* b) { return b ? b->n : 0; }
@@ -923,7 +1016,7 @@ int wg_batch_frame_status(const wg_batch* b, int i) {
 namespace {
 // Wait for the batch's work and check the kernels' error word.
 int batch_sync(wg_batch* b) {
-  hipSetDevice(b->ctx->device);
+  if (!set_device(b->ctx->device)) return WG_STATUS_INVALID_PARAM;
   hipError_t e = batch_wait(b);
   int err = 0;
   if (e == hipSuccess) e = hipMemcpy(&err, b->d_err, sizeof(int), hipMemcpyDeviceToHost);
@@ -948,12 +1041,229 @@ int download_rgba_all(wg_batch* b, uint8_t* const* out, const int32_t* strides, 
       continue;
     }
     e = hipMemcpy2DAsync(out[i], strides[i], window_ptr(b, i), b->desc[(size_t)i].rgba_stride, 4 * (size_t)f.out_w,
-                         f.out_h, hipMemcpyDeviceToHost, b->ctx->stream);
+                         f.out_h, hipMemcpyDefault, b->home);
   }
-  const hipError_t se = hipStreamSynchronize(b->ctx->stream);
+  const hipError_t se = hipStreamSynchronize(b->home);
   return (e != hipSuccess || se != hipSuccess) ? WG_STATUS_USER_ABORT : WG_STATUS_OK;
 }
 }  // namespace
+
+}  // extern "C"
+
+namespace {
+
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// One chunk of a pipelined decode: frames [a, a + n) of the call, parsed into staging arena
+// `arena` and run on stream `s`.  ev: 0/1 around the upload (1 = the arena is free again),
+// 2/3 around the download (3 = everything of the chunk is complete).
+struct PipeChunk {
+  int a = 0, n = 0, arena = 0;
+  hipStream_t s = nullptr;
+  BatchPtr b;
+  hipEvent_t ev[4] = {};
+  bool uploaded = false, up_ok = false, ran = false;
+};
+
+// Queue the chunk's RGBA windows to the caller's buffers on its stream (asynchronous for pinned
+// memory; the runtime stages pageable memory itself).  Frames with bad arguments get
+// INVALID_PARAM; the copies' own failure USER_ABORT.
+void pipe_download(PipeChunk& c, uint8_t* const* out, const int32_t* strides, int32_t* status, double* bytes) {
+  wg_batch* b = c.b.get();
+  hipEventRecord(c.ev[2], c.s);
+  for (int j = 0; j < c.n; ++j) {
+    const int i = c.a + j;
+    if (status[i] != WG_STATUS_OK) continue;
+    const FrameParse& f = b->fp[(size_t)j];
+    if (out[i] == nullptr || strides[i] < 4 * f.out_w) {
+      status[i] = WG_STATUS_INVALID_PARAM;
+      continue;
+    }
+    if (hipMemcpy2DAsync(out[i], strides[i], window_ptr(b, j), b->desc[(size_t)j].rgba_stride, 4 * (size_t)f.out_w,
+                         f.out_h, hipMemcpyDefault, c.s) != hipSuccess) {
+      (void)hipGetLastError();
+      status[i] = WG_STATUS_USER_ABORT;
+      continue;
+    }
+    *bytes += 4.0 * f.out_w * f.out_h;
+  }
+  hipEventRecord(c.ev[3], c.s);
+}
+
+// Wait for a chunk, fold its timings into the stats, check the kernels' error word, release it.
+void pipe_finish(PipeChunk& c, int32_t* status, wg_pipeline_stats* ps) {
+  if (c.ran) {
+    hipEventSynchronize(c.ev[3]);
+    float ms[5] = {};
+    const int st = wg_batch_kernel_ms(c.b.get(), ms, 5);  // (reads the error word)
+    for (float m : ms) ps->kernel_ms += m;
+    float a = 0;
+    if (hipEventElapsedTime(&a, c.ev[0], c.ev[1]) == hipSuccess) ps->h2d_ms += a;
+    if (hipEventElapsedTime(&a, c.ev[2], c.ev[3]) == hipSuccess) ps->d2h_ms += a;
+    (void)hipGetLastError();
+    if (st != WG_STATUS_OK)
+      for (int j = 0; j < c.n; ++j)
+        if (status[c.a + j] == WG_STATUS_OK) status[c.a + j] = st;
+  } else if (c.uploaded && c.b) {
+    hipStreamSynchronize(c.s);  // (an error path: whatever of the chunk was queued has finished)
+  }
+  if (c.b) c.b->home = nullptr;  // complete: destroying it must not wait for later chunks on the stream
+  c.b.reset();
+  for (hipEvent_t& e : c.ev)
+    if (e) {
+      hipEventDestroy(e);
+      e = nullptr;
+    }
+}
+
+// wg_decode_rgba_batch: chunked, two staging arenas and two streams.  The calling thread runs
+// the entropy stage of chunk after chunk (with the context's pool); a device thread uploads
+// chunk k, launches its kernels, then queues chunk k - 1's download and retires chunk k - 2, so
+// the host stage of one chunk, the kernels of the next and the transfers of a third overlap.
+int decode_pipelined(wg_ctx* ctx, const uint8_t* const* data, const size_t* sizes, int n, uint8_t* const* out,
+                     const int32_t* strides, int32_t* status, int32_t flags) {
+  const double t_start = now_s();
+  wg_decoder_options o{};
+  o.colorspace = 1;  // MODE_RGBA
+  o.bypass_filtering = !!(flags & WG_FLAG_BYPASS_FILTERING);
+  o.no_fancy_upsampling = !!(flags & WG_FLAG_NO_FANCY_UPSAMPLING);
+  for (int i = 0; i < n; ++i) status[i] = WG_STATUS_OK;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  if (!set_device(ctx->device)) {
+    for (int i = 0; i < n; ++i) status[i] = WG_STATUS_INVALID_PARAM;
+    return WG_STATUS_INVALID_PARAM;
+  }
+  // chunks: a fixed frame count, or about an eighth of the batch's pixels (>= 64 MPix each)
+  std::vector<int> bounds{0};
+  if (ctx->chunk_frames > 0) {
+    for (int a = ctx->chunk_frames; a < n; a += ctx->chunk_frames) bounds.push_back(a);
+  } else {
+    std::vector<double> px((size_t)n, 0.0);
+    double total = 0;
+    for (int i = 0; i < n; ++i) {
+      wg_features f{};
+      if (data[i] && wg_get_features(data[i], sizes[i], &f) == WG_STATUS_OK) px[(size_t)i] = (double)f.width * f.height;
+      total += px[(size_t)i];
+    }
+    const double target = std::max(64e6, total / 8);
+    double acc = 0;
+    for (int i = 0; i < n; ++i) {
+      acc += px[(size_t)i];
+      if (acc >= target && i + 1 < n) {
+        bounds.push_back(i + 1);
+        acc = 0;
+      }
+    }
+  }
+  bounds.push_back(n);
+  const int K = (int)bounds.size() - 1;
+  wg_pipeline_stats ps{};
+  ps.frames = n;
+  ps.chunks = K;
+  ps.host_threads = ctx->workers()->threads();
+  if (K > 1) {
+    if (!ctx->arena2) ctx->arena2.reset(new wg::StagingArena(pinned_alloc, pinned_free));
+    if (!ctx->stream2 && hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking) != hipSuccess) {
+      (void)hipGetLastError();
+      ctx->stream2 = nullptr;
+      return WG_STATUS_OUT_OF_MEMORY;
+    }
+  }
+  wg::StagingArena* arenas[2] = {ctx->arena.get(), ctx->arena2 ? ctx->arena2.get() : ctx->arena.get()};
+  hipStream_t streams[2] = {ctx->stream, ctx->stream2 ? ctx->stream2 : ctx->stream};
+  std::vector<PipeChunk> ch((size_t)K);
+  for (int k = 0; k < K; ++k) {
+    PipeChunk& c = ch[(size_t)k];
+    c.a = bounds[(size_t)k];
+    c.n = bounds[(size_t)k + 1] - c.a;
+    c.arena = k & 1;
+    c.s = streams[k & 1];
+    for (hipEvent_t& e : c.ev)
+      if (hipEventCreate(&e) != hipSuccess) {
+        (void)hipGetLastError();
+        for (PipeChunk& d : ch)
+          for (hipEvent_t& x : d.ev)
+            if (x) hipEventDestroy(x), x = nullptr;
+        return WG_STATUS_OUT_OF_MEMORY;
+      }
+  }
+  std::mutex qmu;
+  std::condition_variable qcv;
+  int parsed = 0, uploaded = 0;  // chunks handed to / uploaded by the device thread
+  auto device_side = [&] {
+    set_device(ctx->device);
+    for (int k = 0; k < K; ++k) {
+      {
+        std::unique_lock<std::mutex> ql(qmu);
+        qcv.wait(ql, [&] { return parsed > k; });
+      }
+      PipeChunk& c = ch[(size_t)k];
+      int st = WG_STATUS_OUT_OF_MEMORY;  // (no batch: its host stage ran out of memory)
+      hipEventRecord(c.ev[0], c.s);
+      if (c.b) st = guarded([&] { return batch_upload(c.b.get(), *arenas[c.arena]); });
+      hipEventRecord(c.ev[1], c.s);
+      c.up_ok = st == WG_STATUS_OK;
+      {
+        std::lock_guard<std::mutex> ql(qmu);
+        c.uploaded = true;
+        uploaded = k + 1;
+      }
+      qcv.notify_all();
+      if (st == WG_STATUS_OK) st = wg_batch_run(c.b.get(), c.s);
+      c.ran = st == WG_STATUS_OK;
+      if (st != WG_STATUS_OK)
+        for (int j = 0; j < c.n; ++j)
+          if (status[c.a + j] == WG_STATUS_OK) status[c.a + j] = st;
+      if (k >= 1 && ch[(size_t)k - 1].ran) pipe_download(ch[(size_t)k - 1], out, strides, status, &ps.d2h_bytes);
+      if (k >= 2) pipe_finish(ch[(size_t)k - 2], status, &ps);
+    }
+    if (ch[(size_t)K - 1].ran) pipe_download(ch[(size_t)K - 1], out, strides, status, &ps.d2h_bytes);
+    for (int k = std::max(0, K - 2); k < K; ++k) pipe_finish(ch[(size_t)k], status, &ps);
+  };
+  std::thread dev;
+  if (K > 1) dev = std::thread(device_side);
+  double t_parsed = t_start;
+  for (int k = 0; k < K; ++k) {
+    PipeChunk& c = ch[(size_t)k];
+    if (k >= 2) {  // the chunk two back used this arena: its upload must have completed
+      const double t0 = now_s();
+      {
+        std::unique_lock<std::mutex> ql(qmu);
+        qcv.wait(ql, [&] { return uploaded > k - 2; });
+      }
+      if (ch[(size_t)k - 2].up_ok) hipEventSynchronize(ch[(size_t)k - 2].ev[1]);
+      ps.parse_wait_s += now_s() - t0;
+    }
+    const double t0 = now_s();
+    try {
+      c.b = batch_parse(ctx, *arenas[c.arena], c.s, data + c.a, sizes + c.a, c.n, &o, status + c.a);
+      ps.h2d_bytes += (double)c.b->in_bytes;
+    } catch (const std::exception&) {  // host-side vectors: the chunk's frames fail, the others go on
+      c.b.reset();
+      for (int j = 0; j < c.n; ++j) status[c.a + j] = WG_STATUS_OUT_OF_MEMORY;
+    }
+    ps.parse_s += now_s() - t0;
+    t_parsed = now_s();
+    {
+      std::lock_guard<std::mutex> ql(qmu);
+      parsed = k + 1;
+    }
+    qcv.notify_all();
+  }
+  if (K > 1) dev.join();
+  else device_side();
+  const double t_end = now_s();
+  ps.drain_s = t_end - t_parsed;
+  ps.wall_s = t_end - t_start;
+  ctx->stats = ps;
+  return WG_STATUS_OK;
+}
+
+}  // namespace
+
+extern "C" {
 
 int wg_batch_download_rgba(wg_batch* b, int i, uint8_t* rgba, int stride) {
   if (!b || i < 0 || i >= b->n || !rgba) return WG_STATUS_INVALID_PARAM;
@@ -963,7 +1273,7 @@ int wg_batch_download_rgba(wg_batch* b, int i, uint8_t* rgba, int stride) {
   int st = batch_sync(b);
   if (st != WG_STATUS_OK) return st;
   const hipError_t e = hipMemcpy2D(rgba, stride, window_ptr(b, i), b->desc[i].rgba_stride, 4 * (size_t)f.out_w,
-                                   f.out_h, hipMemcpyDeviceToHost);
+                                   f.out_h, hipMemcpyDefault);
   return e == hipSuccess ? WG_STATUS_OK : WG_STATUS_USER_ABORT;
 }
 
@@ -988,11 +1298,11 @@ int wg_batch_download(wg_batch* b, int i, uint8_t* out, int stride) {
   hipError_t e = d_out && d_ed ? hipSuccess : hipErrorOutOfMemory;
   if (e == hipSuccess) {
     ed.dst = d_out;
-    e = hipMemcpyAsync(d_ed, &ed, sizeof(ed), hipMemcpyHostToDevice, b->ctx->stream);
+    e = hipMemcpyAsync(d_ed, &ed, sizeof(ed), hipMemcpyHostToDevice, b->home);
   }
-  if (e == hipSuccess) e = wg::launch_emit(d_ed, 1, f.out_w * f.out_h, b->ctx->stream);
-  if (e == hipSuccess) e = hipMemcpy2DAsync(out, stride, d_out, row, row, f.out_h, hipMemcpyDeviceToHost, b->ctx->stream);
-  const hipError_t se = hipStreamSynchronize(b->ctx->stream);  // before the buffers go back
+  if (e == hipSuccess) e = wg::launch_emit(d_ed, 1, f.out_w * f.out_h, b->home);
+  if (e == hipSuccess) e = hipMemcpy2DAsync(out, stride, d_out, row, row, f.out_h, hipMemcpyDeviceToHost, b->home);
+  const hipError_t se = hipStreamSynchronize(b->home);  // before the buffers go back
   if (e == hipSuccess) e = se;
   cache.put(d_out);
   cache.put(d_ed);
@@ -1004,7 +1314,7 @@ int wg_batch_download_yuv(wg_batch* b, int i, uint8_t* y, uint8_t* u, uint8_t* v
   if (b->fp[i].status != WG_STATUS_OK) return b->fp[i].status;
   if (b->fp[i].lossless) return WG_STATUS_UNSUPPORTED_FEATURE;  // VP8L has no YUV planes
   const FrameDesc& d = b->desc[i];
-  hipSetDevice(b->ctx->device);
+  if (!set_device(b->ctx->device)) return WG_STATUS_INVALID_PARAM;
   hipError_t e = batch_wait(b);
   const int uw = (d.width + 1) / 2, uh = (d.height + 1) / 2;
   if (e == hipSuccess && y) e = hipMemcpy2D(y, d.width, d.y, d.y_stride, d.width, d.height, hipMemcpyDeviceToHost);
@@ -1016,12 +1326,26 @@ int wg_batch_download_yuv(wg_batch* b, int i, uint8_t* y, uint8_t* u, uint8_t* v
 int wg_decode_rgba_batch(wg_ctx* ctx, const uint8_t* const* data, const size_t* sizes, int n,
                          uint8_t* const* rgba, const int32_t* strides, int32_t* status, int32_t flags) {
   if (!ctx || !data || !sizes || !rgba || !strides || !status || n <= 0) return WG_STATUS_INVALID_PARAM;
-  wg_batch* b = wg_batch_create(ctx, data, sizes, n, flags, status);
-  if (!b) return WG_STATUS_OUT_OF_MEMORY;
-  int st = wg_batch_run(b, nullptr);
-  if (st == WG_STATUS_OK) st = download_rgba_all(b, rgba, strides, status);
-  wg_batch_destroy(b);
-  return st;
+  return guarded([&] { return decode_pipelined(ctx, data, sizes, n, rgba, strides, status, flags); });
+}
+
+int wg_ctx_set_chunk_frames(wg_ctx* ctx, int frames) {
+  if (!ctx || frames < 0) return WG_STATUS_INVALID_PARAM;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  ctx->chunk_frames = frames;
+  return WG_STATUS_OK;
+}
+
+int wg_ctx_pipeline_stats(const wg_ctx* ctx, wg_pipeline_stats* out) {
+  if (!ctx || !out) return WG_STATUS_INVALID_PARAM;
+  std::lock_guard<std::mutex> lock(const_cast<wg_ctx*>(ctx)->mu);
+  *out = ctx->stats;
+  return WG_STATUS_OK;
+}
+
+void* wg_host_alloc(size_t bytes) { return bytes ? pinned_alloc(bytes) : nullptr; }
+void wg_host_free(void* p) {
+  if (p) pinned_free(p);
 }
 
 int wg_decode_rgba_batch_multi(wg_ctx* const* ctxs, int n_ctx, const uint8_t* const* data, const size_t* sizes,
@@ -1125,14 +1449,14 @@ int wg_decode_into(const uint8_t* data, size_t size, const wg_decoder_options* o
   }
   if (bpp && w > 0 && h > 0 && (stride < bpp * w || (size_t)stride * (h - 1) + (size_t)bpp * w > cap))
     return WG_STATUS_INVALID_PARAM;
-  wg_ctx* ctx = default_ctx();
+  const std::shared_ptr<wg_ctx> ctx = default_ctx();  // held until this call returns
   if (!ctx) return WG_STATUS_UNSUPPORTED_FEATURE;  // no GPU: no CPU fallback by design
   const uint8_t* d[1] = {data};
   const size_t s[1] = {size};
   uint8_t* o[1] = {out};
   const int32_t str[1] = {stride};
   int32_t fs[1] = {0};
-  st = wg_decode_batch(ctx, d, s, 1, opt, o, str, fs);
+  st = wg_decode_batch(ctx.get(), d, s, 1, opt, o, str, fs);
   return st != WG_STATUS_OK ? st : fs[0];
 }
 
@@ -1143,14 +1467,14 @@ int wg_decode_rgba_into(const uint8_t* data, size_t size, uint8_t* rgba, size_t 
   if (st != WG_STATUS_OK) return st;
   if (stride < 4 * f.width || (size_t)stride * (f.height - 1) + 4 * (size_t)f.width > cap)
     return WG_STATUS_INVALID_PARAM;
-  wg_ctx* ctx = default_ctx();
+  const std::shared_ptr<wg_ctx> ctx = default_ctx();  // held until this call returns
   if (!ctx) return WG_STATUS_UNSUPPORTED_FEATURE;  // no GPU: no CPU fallback by design
   const uint8_t* d[1] = {data};
   const size_t s[1] = {size};
   uint8_t* o[1] = {rgba};
   const int32_t str[1] = {stride};
   int32_t fs[1] = {0};
-  st = wg_decode_rgba_batch(ctx, d, s, 1, o, str, fs, flags);
+  st = wg_decode_rgba_batch(ctx.get(), d, s, 1, o, str, fs, flags);
   return st != WG_STATUS_OK ? st : fs[0];
 }
 
@@ -1253,7 +1577,7 @@ int wg_anim_decode(wg_ctx* ctx, const uint8_t* data, size_t size, uint8_t* canva
   uint8_t* d_canvases = nullptr;
   {
     std::lock_guard<std::mutex> lock(ctx->mu);
-    hipSetDevice(ctx->device);
+    if (st == WG_STATUS_OK && !set_device(ctx->device)) st = WG_STATUS_INVALID_PARAM;
     hipError_t e = st == WG_STATUS_OK ? hipSuccess : hipErrorUnknown;
     if (e == hipSuccess) {
       d_fd = static_cast<AnimFrameDesc*>(ctx->cache.get(sizeof(AnimFrameDesc) * (size_t)n));

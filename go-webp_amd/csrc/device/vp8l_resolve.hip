@@ -534,7 +534,11 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
             }
           }
           if (act) *reinterpret_cast<uint4*>(&vcur[li0]) = make_uint4(v[0], v[1], v[2], v[3]);
-          if (kRounds && act) {  // copies in (b) read these states, after the barrier
+          // copies in (b) read these states, after the barrier -- also those of a LATER window
+          // of the block: a window without pending copies of its own resolves its lookups on
+          // the no-rounds path, and an in-block copy further on may have one as its source
+          // (blk_pc is block-uniform; without it such a copy could never resolve)
+          if ((kRounds || blk_pc) && act) {
 #pragma unroll
             for (int j = 0; j < kPer; ++j)
               if ((act >> j) & 1u) st[li0 + j] = kKnown;

@@ -20,6 +20,7 @@ __all__ = [
     "Status", "WebPError", "FLAG_BYPASS_FILTERING", "FLAG_NO_FANCY_UPSAMPLING", "Features",
     "lib", "features", "decode_config", "decode", "Context", "Batch", "vp8_parse", "vp8l_parse", "MB_DTYPE",
     "VP8Info", "VP8LInfo", "VP8LCoded", "device_count", "yuv420_to_rgba_device", "vp8l_resolve_device", "MultiContext", "set_default_device",
+    "pinned_empty", "PipelineStats",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -113,6 +114,46 @@ class VP8LInfo(C.Structure):
                 ("cache_bits", C.c_int32), ("num_literals", C.c_int32)]
 
 
+class PipelineStats(C.Structure):
+    """wg_pipeline_stats: where the last pipelined decode_batch's time went."""
+    _fields_ = [("frames", C.c_int32), ("chunks", C.c_int32), ("host_threads", C.c_int32), ("reserved", C.c_int32),
+                ("wall_s", C.c_double), ("parse_s", C.c_double), ("parse_wait_s", C.c_double),
+                ("h2d_ms", C.c_double), ("kernel_ms", C.c_double), ("d2h_ms", C.c_double),
+                ("h2d_bytes", C.c_double), ("d2h_bytes", C.c_double), ("drain_s", C.c_double)]
+
+    def as_dict(self):
+        return {name: getattr(self, name) for name, _ in self._fields_ if name != "reserved"}
+
+
+class _PinnedBlock:
+    """Owner of one wg_host_alloc block (freed with the last array that views it)."""
+
+    def __init__(self, nbytes):
+        self.ptr = lib().wg_host_alloc(max(1, nbytes))
+        if not self.ptr:
+            raise WebPError(Status.OUT_OF_MEMORY, f"wg_host_alloc({nbytes})")
+        self.nbytes = nbytes
+
+    def __del__(self):
+        try:
+            if self.ptr:
+                lib().wg_host_free(self.ptr)
+                self.ptr = None
+        except Exception:
+            pass
+
+
+def pinned_empty(shape, dtype=np.uint8):
+    """An uninitialised ndarray in page-locked host memory (wg_host_alloc): decode outputs there
+    are written by DMA instead of the HIP runtime's staged copies."""
+    dtype = np.dtype(dtype)
+    nbytes = int(np.prod(shape)) * dtype.itemsize
+    blk = _PinnedBlock(nbytes)
+    buf = (C.c_uint8 * max(1, nbytes)).from_address(blk.ptr)
+    buf._owner = blk  # the ctypes buffer keeps the block alive; the array keeps the buffer
+    return np.frombuffer(buf, dtype=dtype, count=int(np.prod(shape))).reshape(shape)
+
+
 class VP8LCoded:
     """A lossless image after the host prefix-code walk: one token per coded pixel
     (tokens: (height, coded_width) uint32; bits 31..30 = 0 literal index, 1 color-cache key,
@@ -170,6 +211,10 @@ _SIGS = {
     "wg_set_default_device": (C.c_int, [C.c_int]),
     "wg_vp8l_resolve_device": (C.c_int, [_P, _P, C.c_int, C.c_int, C.c_int, _P, _P]),
     "wg_decode_rgba_batch_multi": (C.c_int, [_P, C.c_int, _P, _P, C.c_int, _P, _P, _P, C.c_int32]),
+    "wg_ctx_set_chunk_frames": (C.c_int, [_P, C.c_int]),
+    "wg_ctx_pipeline_stats": (C.c_int, [_P, _P]),
+    "wg_host_alloc": (_P, [C.c_size_t]),
+    "wg_host_free": (None, [_P]),
 }
 EXPORTED = tuple(_SIGS)
 
@@ -499,9 +544,24 @@ class Context:
             raise WebPError(st, "wg_anim_decode")
         return canv, ts
 
+    def set_chunk_frames(self, frames):
+        """Frames per pipeline chunk of decode_batch (0 = automatic)."""
+        st = lib().wg_ctx_set_chunk_frames(self._h, frames)
+        if st != Status.OK:
+            raise WebPError(st, "wg_ctx_set_chunk_frames")
+
+    def pipeline_stats(self):
+        """PipelineStats of the last decode_batch (wg_ctx_pipeline_stats)."""
+        ps = PipelineStats()
+        st = lib().wg_ctx_pipeline_stats(self._h, C.byref(ps))
+        if st != Status.OK:
+            raise WebPError(st, "wg_ctx_pipeline_stats")
+        return ps
+
     def decode_batch(self, datas, flags=0, out=None):
         """Decode a list of WebP files; returns (list of RGBA arrays or None, status array).
-        `out`: optional preallocated (H, W, 4) uint8 arrays, one per input."""
+        `out`: optional preallocated (H, W, 4) uint8 arrays, one per input (pinned_empty()
+        arrays are written by DMA).  Pipelined in chunks (wg_decode_rgba_batch)."""
         bufs, ptrs, sizes = _ptr_arrays(datas)
         n = len(bufs)
         outs, optr, strides = _rgba_outs(bufs, out)

@@ -120,12 +120,42 @@ typedef struct wg_ctx wg_ctx;
 wg_ctx* wg_ctx_create(int device, int host_threads);
 void wg_ctx_destroy(wg_ctx* ctx);
 
-/* Decode n independent frames in one batch: entropy stage on host threads, then one
- * launch of each DSP kernel over the whole batch.  Per-frame status in status[i]; a bad
- * frame does not abort the batch.  Returns OK if the batch ran (check status[]). */
+/* Decode n independent frames: entropy stage on host threads, the DSP kernels on the device,
+ * RGBA back to rgba[i].  Per-frame status in status[i]; a bad frame does not abort the batch.
+ * Returns OK if the batch ran (check status[]).  Pipelined: the frames go in chunks (see
+ * wg_ctx_set_chunk_frames), and chunk k + 1's entropy stage (host threads) and upload overlap
+ * chunk k's kernels and download (two staging arenas, two streams) -- the parse / finish
+ * overlap of libwebp's threaded decode (frame_dec.c.go:505-534, 611-667) at batch scale.  Each
+ * frame's result is that of a one-batch decode.  Output memory from wg_host_alloc (pinned) is
+ * written by DMA; any other memory through the HIP runtime's staged copies. */
 int wg_decode_rgba_batch(wg_ctx* ctx, const uint8_t* const* data, const size_t* sizes, int n,
                          uint8_t* const* rgba, const int32_t* strides, int32_t* status,
                          int32_t flags);
+
+/* Frames per pipeline chunk of wg_decode_rgba_batch (0 = automatic: about an eighth of the
+ * batch's pixels, at least 64 MPix per chunk; n >= the batch = no pipelining).  INVALID_PARAM
+ * for a negative count.  No libwebp counterpart. */
+int wg_ctx_set_chunk_frames(wg_ctx* ctx, int frames);
+
+/* Where the time of the context's last wg_decode_rgba_batch went.  Host times are wall clock
+ * on the calling thread; device times are HIP events summed over the chunks (the stages of
+ * different chunks overlap, so they need not add up to wall_s). */
+typedef struct {
+  int32_t frames, chunks, host_threads, reserved;
+  double wall_s;         /* the whole call                                                    */
+  double parse_s;        /* entropy stage of every chunk (caller thread + pool)             */
+  double parse_wait_s;   /* of wall_s: the caller waiting for a staging arena to come free  */
+  double h2d_ms, kernel_ms, d2h_ms;  /* device side, summed over chunks                    */
+  double h2d_bytes, d2h_bytes;
+  double drain_s;        /* after the last chunk's entropy stage: waiting for the device  */
+} wg_pipeline_stats;
+int wg_ctx_pipeline_stats(const wg_ctx* ctx, wg_pipeline_stats* out);
+
+/* Page-locked host memory for output buffers (hipHostMalloc): the device writes it by DMA.
+ * NULL on failure.  Free with wg_host_free.  (The Go shim backs image.RGBA.Pix with it in
+ * DecodeBatchInto.) */
+void* wg_host_alloc(size_t bytes);
+void wg_host_free(void* p);
 
 /* Multi-GPU batch: the n frames are split into n_ctx contiguous shards, shard k
  * decoded by wg_decode_rgba_batch on ctxs[k] (normally one context per device), all shards
@@ -191,7 +221,9 @@ int64_t wg_batch_pixels(const wg_batch* b);
 
 /* Copy results of frame i back to host: RGBA of the output window (stride >= 4*width; no flip,
  * whatever the batch's colorspace), the batch's colorspace / flip via K6 (wg_batch_download,
- * stride >= bpp*width), and/or the full frame's Y/U/V planes (strides width, (width+1)/2). */
+ * stride >= bpp*width), and/or the full frame's Y/U/V planes (strides width, (width+1)/2).
+ * wg_batch_download_rgba's destination may also be device memory (e.g. a torch tensor on the
+ * batch's device): the copy is then device to device and the frame never crosses PCIe. */
 int wg_batch_download_rgba(wg_batch* b, int i, uint8_t* rgba, int stride);
 int wg_batch_download(wg_batch* b, int i, uint8_t* out, int stride);
 int wg_batch_download_yuv(wg_batch* b, int i, uint8_t* y, uint8_t* u, uint8_t* v); /* lossy only */

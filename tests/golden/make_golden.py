@@ -712,6 +712,9 @@ BENCH_CASES = [
 ]
 # section bench_c5x: the other C5 seeds (K = 8 distinct lossless frames, like C2 / C3)
 BENCH_C5X = [("c5_ll2048", 2048, 2048, list(range(1, 8)), {"lossless": 1}, "corr")]
+# section bench_c3s: SURVEY §8(d)'s entropy-stress variant of C3 (sigma = 18, ~2 bpp: dense
+# coefficients, i4-heavy), 8 seeds, the C3 encoder settings
+BENCH_C3S = [("c3s_4k", 2160, 3840, list(range(8)), {"filter_type": 1, "filter_strength": 60}, "synth18")]
 
 
 def sha(a):
@@ -722,14 +725,14 @@ def main(argv):
     """argv: sections to (re)generate among lossy, lossy_extra, lossless, alpha, modes, anim, bench (default: all);
     the manifest entries of the other sections are kept."""
     sections = set(argv) or {"lossy", "lossy_extra", "lossless", "alpha", "modes", "anim", "bench", "bench_c5x",
-                             "fuzz"}
+                             "bench_c3s", "fuzz"}
     os.makedirs(os.path.join(HERE, "lossy"), exist_ok=True)
     os.makedirs(os.path.join(HERE, "lossless"), exist_ok=True)
     os.makedirs(os.path.join(HERE, "bench"), exist_ok=True)
     mpath = os.path.join(HERE, "manifest.json")
     manifest = json.load(open(mpath)) if os.path.exists(mpath) else {}
     manifest["libwebp"] = "1.6.0 (Pillow 12.2.0 bundle, plain-C DSP)"
-    for sec in sections - {"bench_c5x"}:  # (bench_c5x adds to "bench")
+    for sec in sections - {"bench_c5x", "bench_c3s"}:  # (bench_c5x / bench_c3s add to "bench")
         manifest[sec] = {}
     manifest.setdefault("bench", {})
     if "alpha" in sections:
@@ -823,10 +826,12 @@ def main(argv):
             manifest["anim"][name] = dict(bytes=len(data), info=info, frames=flags)
             print(name, len(data), info, [(f["x"], f["y"], f["w"], f["h"], f["dispose_bg"], f["no_blend"])
                                           for f in flags], flush=True)
-    bench = (BENCH_CASES if "bench" in sections else []) + (BENCH_C5X if "bench_c5x" in sections else [])
+    bench = ((BENCH_CASES if "bench" in sections else []) + (BENCH_C5X if "bench_c5x" in sections else []) +
+             (BENCH_C3S if "bench_c3s" in sections else []))
     for name, H, W, seeds, kw, gen in bench:
         for s in seeds:
-            img = synth(H, W, s, 6) if gen == "synth6" else corr_luma(H, W, s)
+            img = (synth(H, W, s, 6) if gen == "synth6" else synth(H, W, s, 18) if gen == "synth18"
+                   else corr_luma(H, W, s))
             lossless = kw.get("lossless", 0)
             data = encode(img, **kw)
             r = decode_all(data, lossy=not lossless)

@@ -100,6 +100,51 @@ def make_stream(n, bits, seed, p_lit=0.035, p_copy=0.0, dist=(1,), palette=256, 
     return toks, np.asarray(lits if lits else [0], np.uint32)
 
 
+def make_cross_window_stream(blocks, seed, bits=11, p_lit=0.4, p_copy=0.12):
+    """-> (tokens, lits): blocks of 4096 pixels whose first half holds only literals and cache
+    lookups and whose second half adds in-block copies whose SOURCE is one of the first half's
+    lookups.  At cache_bits 11 K7's rank masks hold 256 updaters per window, so with ~40 %
+    literals a block runs as several windows: the early windows have no pending copy (their
+    lookups resolve on the no-rounds path) and a later window's copies read those lookups'
+    states -- the case that must not fall into the round cap / serial path."""
+    rng = np.random.default_rng(seed)
+    nk = 1 << bits
+    cache = [0] * nk
+    keys, written = [], set()
+    vals, toks, lits = [], [], []
+
+    def insert(v):
+        h = hash_px(v, bits)
+        if h not in written:
+            written.add(h)
+            keys.append(h)
+        cache[h] = v
+
+    for b in range(blocks):
+        base = 4096 * b
+        lookup_pos = []
+        for li in range(4096):
+            i = base + li
+            r = rng.random()
+            if i == 0 or not keys or r < p_lit:
+                v = int(rng.integers(1, 1 << 32))
+                toks.append((LIT << 30) | len(lits))
+                lits.append(v)
+            elif li >= 2048 and lookup_pos and r < p_lit + p_copy:
+                src = lookup_pos[int(rng.integers(len(lookup_pos)))]
+                toks.append((COPY << 30) | (i - src))
+                v = vals[src]
+            else:
+                k = keys[int(rng.integers(len(keys)))]
+                toks.append((CACHE << 30) | k)
+                v = cache[k]
+                if li < 2048:
+                    lookup_pos.append(i)
+            vals.append(v)
+            insert(v)
+    return np.asarray(toks, np.uint32), np.asarray(lits, np.uint32)
+
+
 # (name, n_px, cache_bits, kwargs): each aims at one path of K7
 CASES = [
     ("c5like", 3 * 4096 + 123, 10, dict(p_lit=0.035, palette=300)),

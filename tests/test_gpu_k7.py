@@ -57,6 +57,51 @@ def test_k7_c5_streams():
         assert np.array_equal(got, want), f"s{s}: {(got != want).sum()} pixels differ"
 
 
+_STATS_CHILD = r"""
+import ctypes as C, sys, numpy as np, torch
+sys.path[:0] = [sys.argv[1], sys.argv[2]]
+import webp_amd, k7_streams
+toks, lits = k7_streams.make_cross_window_stream(4, seed=5)
+dt = torch.from_numpy(toks.view(np.int32)).cuda()
+dl = torch.from_numpy(lits.view(np.int32)).cuda()
+out = torch.empty(toks.size, dtype=torch.int32, device="cuda")
+L = webp_amd.lib()
+st = (C.c_ulonglong * (16 * 17))()
+L.wg_debug_k7_stats(st, 1)
+webp_amd.vp8l_resolve_device(dt.data_ptr(), dl.data_ptr(), lits.size, toks.size, 11, out.data_ptr())
+torch.cuda.synchronize()
+L.wg_debug_k7_stats(st, 1)
+print("K7STATS", st[0], st[1], st[2], st[3], st[9], st[10])
+"""
+
+
+def test_k7_cross_window_lookup_sources():
+    """Blocks that run as several windows (cache_bits 11: 256 ranks per window) where a later
+    window's in-block copies take their value from lookups of an earlier window that had no
+    pending copy (so its lookups resolved on the no-rounds path): bit-exact against the oracle,
+    and -- through the measurement build's counters, when it has been built -- no window hits
+    the round cap or falls to the serial path (the performance cliff the lookups' missing
+    'known' state used to cause)."""
+    import subprocess
+    import sys
+    toks, lits = k7_streams.make_cross_window_stream(4, seed=5)
+    want = oracle_resolve(toks, lits, 11)
+    got = device_resolve(toks, lits, 11)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, f"{bad.size} pixels differ, first at {bad[:5]}"
+    timing = os.path.join(ROOT, "go-webp_amd", "webp_amd", "libgowebp_amd_timing.so")
+    if not os.path.exists(timing):
+        pytest.skip("measurement build (make VARIANT=timing) absent: counters not checked")
+    env = dict(os.environ, WG_LIB_VARIANT="timing")
+    r = subprocess.run([sys.executable, "-c", _STATS_CHILD, os.path.join(ROOT, "go-webp_amd"),
+                        os.path.join(ROOT, "tests")], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith("K7STATS")][-1]
+    blocks, serial, rounds, windows, empty, caps = map(int, line.split()[1:])
+    assert blocks == 4 and windows > blocks, line  # the stream really runs as several windows
+    assert caps == 0 and serial == 0, f"round caps {caps}, serial windows {serial} ({line})"
+
+
 def test_k7_rejects_bad_params():
     import webp_amd
     with pytest.raises(webp_amd.WebPError):

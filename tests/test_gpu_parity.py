@@ -66,9 +66,10 @@ def test_batch_all_fixtures_vs_golden_and_oracle(ctx, flags, emit):
 
 
 @pytest.mark.parametrize("emit", ["fused", "separate", "stage"])
-@pytest.mark.parametrize("prefix", ["c1_512", "c2_1080p", "c3_4k"])
+@pytest.mark.parametrize("prefix", ["c1_512", "c2_1080p", "c3_4k", "c3s_4k"])
 def test_bench_frames_sha256(ctx, prefix, emit):
-    """Full-size bench configs (C1 512^2, C2 1080p, C3 4K deblocked): every frame's
+    """Full-size bench configs (C1 512^2, C2 1080p, C3 4K deblocked, and c3s: C3's entropy-stress
+    variant at sigma 18, ~2 bpp, dense coefficients and mostly i4 MBs): every frame's
     Y/U/V and RGBA SHA-256 equals libwebp's, whichever kernel emits the RGBA (K1's tail,
     K2 in the batch run, or the stage entry wg_batch_run_emit after a planes-only run)."""
     m = manifest()["bench"]
@@ -92,6 +93,26 @@ def test_bench_frames_sha256(ctx, prefix, emit):
         assert _sha(u) == ent["u"], p
         assert _sha(v) == ent["v"], p
         assert _sha(b.rgba(i)) == ent["rgba"], p
+    b.close()
+
+
+@pytest.mark.parametrize("flags", [webp_amd.FLAG_BYPASS_FILTERING, webp_amd.FLAG_NO_FANCY_UPSAMPLING])
+def test_c3s_dense_frames_other_paths(ctx, flags):
+    """The c3s frames (dense coefficients, i4-heavy) with the loop filter bypassed and with
+    point-sampled RGBA: planes and RGBA SHA-256 equal libwebp's for all eight seeds."""
+    m = manifest()["bench"]
+    paths = bench_files("c3s_4k")
+    assert len(paths) == 8
+    b = ctx.batch([open(p, "rb").read() for p in paths], flags)
+    assert (b.status == 0).all()
+    b.run()
+    bypass = flags & webp_amd.FLAG_BYPASS_FILTERING
+    sfx = "_nofilter" if bypass else ""
+    for i, p in enumerate(paths):
+        ent = m[p.rsplit("/", 1)[1]]["sha256"]
+        y, u, v = b.yuv(i)
+        assert (_sha(y), _sha(u), _sha(v)) == (ent["y" + sfx], ent["u" + sfx], ent["v" + sfx]), p
+        assert _sha(b.rgba(i)) == ent["rgba_nofilter" if bypass else "rgba_point"], p
     b.close()
 
 

@@ -87,8 +87,14 @@ def test_bench_spawns_one_rank_per_gpu(n):
     LOCAL_RANK (= device), whole-job pixels summed over the ranks.  --mock replaces the
     device decode by a sleep, so this runs on CPU; the barrier and reduction are the real
     gloo ones."""
-    out = _run_bench(["--gpus", str(n), "--mock", "--steps", "3", "--warmup", "1"])
+    out = _run_bench(["--gpus", str(n), "--mock", "--steps", "3", "--warmup", "1", "--cpu-seconds", "0.5"])
     assert out["n_gpus"] == n and out["mock"] is True
+    # the end-to-end leg runs on every rank and is reduced like `value`; the CPU baseline and
+    # the host's core counts stay in N > 1 lines
+    assert out["end_to_end"]["n_gpus"] == n and out["end_to_end_pageable"]["n_gpus"] == n
+    assert out["cpu_baseline"]["value"] > 0 and out["cpu_baseline_all_cores"]["cores"] >= 1
+    assert out["host"]["nproc"] >= 1 and out["host"]["ranks"] == n
+    assert 1 <= out["host"]["host_threads_per_rank"] <= max(1, out["host"]["job_cpus"] // n)
     ranks = out["ranks"]
     assert sorted(r["rank"] for r in ranks) == list(range(n))
     assert sorted(r["local_rank"] for r in ranks) == list(range(n))
@@ -102,5 +108,6 @@ def test_bench_spawns_one_rank_per_gpu(n):
 def test_bench_under_external_launcher_env():
     """Under torch.distributed.run the launcher's WORLD_SIZE / RANK / LOCAL_RANK are used and
     nothing is spawned: a single process with WORLD_SIZE=1 reports n_gpus == 1."""
-    out = _run_bench(["--mock", "--steps", "2", "--warmup", "1"], {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    out = _run_bench(["--mock", "--steps", "2", "--warmup", "1", "--no-cpu-baseline"],
+                     {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert out["n_gpus"] == 1 and len(out["ranks"]) == 1

@@ -207,10 +207,10 @@ def test_bench_c1_frame_sha256():
     assert hashlib.sha256(out["y"].tobytes()).hexdigest() == ent["y"]
 
 
-@pytest.mark.parametrize("prefix", ["c2_1080p", "c3_4k"])
+@pytest.mark.parametrize("prefix", ["c2_1080p", "c3_4k", "c3s_4k"])
 def test_bench_frames_sha256(prefix):
-    """The bench bitstreams (C2 1080p, C3 4K deblocked) decode bit-exactly on the CPU
-    checker; the GPU parity tests compare against the same SHA-256s."""
+    """The bench bitstreams (C2 1080p, C3 4K deblocked, c3s: C3 at sigma 18, ~2 bpp) decode
+    bit-exactly on the CPU checker; the GPU parity tests compare against the same SHA-256s."""
     import hashlib
     m = manifest()["bench"]
     for path in bench_files(prefix)[:2]:
