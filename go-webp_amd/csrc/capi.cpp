@@ -1147,13 +1147,19 @@ int decode_pipelined(wg_ctx* ctx, const uint8_t* const* data, const size_t* size
       if (data[i] && wg_get_features(data[i], sizes[i], &f) == WG_STATUS_OK) px[(size_t)i] = (double)f.width * f.height;
       total += px[(size_t)i];
     }
-    const double target = std::max(64e6, total / 8);
-    double acc = 0;
+    // Only the last chunk's device work (upload, kernels, download) is exposed after the host
+    // stage ends, so the batch's last 2T of pixels go in halving chunks: R/2, R/4, R/8, R/8.
+    const double T = std::max(64e6, total / 8);
+    double target = T, acc = 0, consumed = 0, tail_r = 0;
+    int tail = 0;
     for (int i = 0; i < n; ++i) {
       acc += px[(size_t)i];
       if (acc >= target && i + 1 < n) {
         bounds.push_back(i + 1);
+        consumed += acc;
         acc = 0;
+        if (tail == 0 && total - consumed <= 2 * T) tail_r = total - consumed;
+        if (tail_r > 0 && tail < 3) target = tail_r / (double)(2 << tail++);
       }
     }
   }

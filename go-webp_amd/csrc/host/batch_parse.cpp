@@ -97,7 +97,13 @@ bool stage_ll(const VP8LFrame& f, StagingArena* arena, StagingArena::Cursor* cur
 
 // Per worker thread: the lossless entropy stage's output, reused frame after frame (its
 // vectors keep their capacity, so a batch does not page-fault fresh heap memory per frame).
+// Capacity beyond kKeepLLBytes (a 16k x 16k frame's tokens are 1 GB) is released once the
+// frame is staged, so pool threads and callers' threads do not hold it for good.
 thread_local VP8LFrame tl_lf;
+constexpr size_t kKeepLLBytes = size_t(64) << 20;
+void trim_ll(VP8LFrame& f) {
+  if ((f.tokens.capacity() + f.lits.capacity()) * 4 > kKeepLLBytes) f = VP8LFrame();
+}
 
 }  // namespace
 
@@ -162,7 +168,9 @@ int parse_one(const uint8_t* data, size_t size, const wg_decoder_options& opt, S
       const int64_t bottom = opt.use_cropping ? (int64_t)opt.crop_top + opt.crop_height : fp->height;
       if ((uint64_t)bottom * (uint64_t)lf.coded_width > (uint64_t)lf.fail_pixel) return st;
     }
-    return stage_ll(lf, arena, cur, &fp->ll) ? WG_STATUS_OK : WG_STATUS_OUT_OF_MEMORY;
+    const bool staged = stage_ll(lf, arena, cur, &fp->ll);
+    trim_ll(lf);
+    return staged ? WG_STATUS_OK : WG_STATUS_OUT_OF_MEMORY;
   }
   const int flags = opt.bypass_filtering ? WG_FLAG_BYPASS_FILTERING : 0;
   // crop bottom in int64, clamped to the frame: an adversarial crop_top + crop_height must
@@ -202,7 +210,9 @@ int parse_one(const uint8_t* data, size_t size, const wg_decoder_options& opt, S
       init_fails = ast == WG_STATUS_OUT_OF_MEMORY;
       afail = af.fail_pixel;
       acw = af.coded_width;
-      if (!init_fails && !stage_ll(af, arena, cur, &fp->al)) return WG_STATUS_OUT_OF_MEMORY;
+      const bool staged = init_fails || stage_ll(af, arena, cur, &fp->al);
+      trim_ll(af);
+      if (!staged) return WG_STATUS_OUT_OF_MEMORY;
     } else if (!arena->put(cur, ad + 1, (size_t)fp->width * fp->height, &fp->araw)) {
       return WG_STATUS_OUT_OF_MEMORY;
     }

@@ -101,8 +101,21 @@ class StagingArena {
     if (c->chunk) c->chunk->busy = false;
     c->chunk = nullptr;
   }
-  // Start a batch: every chunk empty (the previous batch's upload has completed).
+  // Start a batch: every chunk empty (the previous batch's upload has completed).  Dedicated
+  // chunks of oversized frames (larger than the standard chunk) are freed rather than kept, so
+  // one huge frame does not pin its memory for the life of the context.
   void begin_batch() {
+    size_t w = 0;
+    for (size_t r = 0; r < chunks_.size(); ++r) {
+      if (chunks_[r]->cap > chunk_bytes_) {
+        free_(chunks_[r]->p);
+        continue;
+      }
+      chunks_[w] = std::move(chunks_[r]);
+      chunks_[w]->index = (int32_t)w;
+      ++w;
+    }
+    chunks_.resize(w);
     for (auto& ch : chunks_) {
       ch->used = 0;
       ch->busy = false;

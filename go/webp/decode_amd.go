@@ -10,9 +10,10 @@
 // it copies inputs into its own pinned staging and writes outputs before returning.
 //
 // Layout assumed by the #cgo lines: the header under third_party/gowebp_amd/include and the
-// library under third_party/gowebp_amd/lib, next to this file.  This image has no Go
-// toolchain, so the file is not compiled here; every C entry point it calls is exercised
-// through the same ABI by tests/ (ctypes).
+// library under third_party/gowebp_amd/lib, next to this file.  Neither this image nor the
+// MI355X box has a Go toolchain (probed: profiles/r04/box_env_probe.txt), so the file is not
+// compiled here; every C entry point it calls is exercised through the same ABI by tests/
+// (ctypes), and tests/test_capi.py checks that each one it names is declared and exported.
 package webp
 
 /*
@@ -208,8 +209,9 @@ func (a *batchArgs) free() {
 	a.raw = nil
 }
 
-// DecodeBatch decodes independent frames in one batch (entropy stage on the context's host
-// threads, one launch per DSP kernel).  Per-frame errors do not abort the batch.
+// DecodeBatch decodes independent frames (entropy stage on the context's host threads, the DSP
+// kernels on the device, pipelined in chunks: wg_decode_rgba_batch).  Per-frame errors do not
+// abort the batch.
 func (d *Decoder) DecodeBatch(frames [][]byte) ([]*image.NRGBA, []error) {
 	if len(frames) == 0 {
 		return nil, nil
@@ -218,6 +220,76 @@ func (d *Decoder) DecodeBatch(frames [][]byte) ([]*image.NRGBA, []error) {
 	st := C.wg_decode_rgba_batch(d.ctx, &a.dataP[0], &a.sizes[0], C.int(a.n), &a.outP[0], &a.strides[0],
 		&a.status[0], 0)
 	return a.finish(st, "DecodeBatch")
+}
+
+// SetChunkFrames sets the pipeline chunk of DecodeBatch (wg_ctx_set_chunk_frames; 0 = automatic).
+func (d *Decoder) SetChunkFrames(frames int) error {
+	return statusErr(C.wg_ctx_set_chunk_frames(d.ctx, C.int(frames)), "SetChunkFrames")
+}
+
+// Stats: where the last DecodeBatch's time went (wg_ctx_pipeline_stats).
+func (d *Decoder) Stats() (C.wg_pipeline_stats, error) {
+	var ps C.wg_pipeline_stats
+	err := statusErr(C.wg_ctx_pipeline_stats(d.ctx, &ps), "Stats")
+	return ps, err
+}
+
+// PinnedNRGBA is an *image.NRGBA whose Pix lives in page-locked C memory (wg_host_alloc): the
+// device writes it by DMA.  Being C memory it needs no runtime.Pinner; release it with Free.
+type PinnedNRGBA struct {
+	*image.NRGBA
+	p unsafe.Pointer
+}
+
+func NewPinnedNRGBA(w, h int) (*PinnedNRGBA, error) {
+	p := C.wg_host_alloc(C.size_t(4 * w * h))
+	if p == nil {
+		return nil, &StatusError{Code: int(C.WG_STATUS_OUT_OF_MEMORY), What: "NewPinnedNRGBA"}
+	}
+	pix := unsafe.Slice((*byte)(p), 4*w*h)
+	return &PinnedNRGBA{NRGBA: &image.NRGBA{Pix: pix, Stride: 4 * w, Rect: image.Rect(0, 0, w, h)}, p: p}, nil
+}
+
+func (m *PinnedNRGBA) Free() {
+	if m.p != nil {
+		C.wg_host_free(m.p)
+		m.p, m.NRGBA = nil, nil
+	}
+}
+
+// DecodeBatchInto decodes frames[i] into dst[i] (reused across calls, e.g. PinnedNRGBA
+// buffers of a serving loop); dst[i] must match frame i's size.  Per-frame errors.
+func (d *Decoder) DecodeBatchInto(frames [][]byte, dst []*PinnedNRGBA) []error {
+	n := len(frames)
+	errs := make([]error, n)
+	if n == 0 || len(dst) != n {
+		return errs
+	}
+	a := &batchArgs{n: n}
+	defer a.free()
+	a.dataP = cAlloc[*C.uint8_t](a, n)
+	a.outP = cAlloc[*C.uint8_t](a, n)
+	a.sizes = cAlloc[C.size_t](a, n)
+	a.strides = cAlloc[C.int32_t](a, n)
+	a.status = cAlloc[C.int32_t](a, n)
+	for i, f := range frames {
+		if len(f) > 0 {
+			a.pinner.Pin(&f[0])
+		}
+		a.dataP[i], a.sizes[i] = cBytes(f)
+		a.outP[i] = (*C.uint8_t)(dst[i].p) // C memory: no pinning needed
+		a.strides[i] = C.int32_t(dst[i].Stride)
+	}
+	st := C.wg_decode_rgba_batch(d.ctx, &a.dataP[0], &a.sizes[0], C.int(n), &a.outP[0], &a.strides[0],
+		&a.status[0], 0)
+	for i := range errs {
+		if err := statusErr(st, "DecodeBatchInto"); err != nil {
+			errs[i] = err
+		} else {
+			errs[i] = statusErr(C.int(a.status[i]), fmt.Sprintf("frame %d", i))
+		}
+	}
+	return errs
 }
 
 // MultiDecoder shards frames across several contexts, normally one per GPU (SURVEY §8(e)):

@@ -73,9 +73,10 @@ int wg_decode_rgba_into(const uint8_t* data, size_t size, uint8_t* rgba, size_t 
                         int stride, int flags);
 
 /* The HIP device of the context behind the single-frame entry points (wg_decode_rgba_into,
- * wg_decode_into): 0 by default.  Replaces that context if it exists on another device (no
- * call may be in flight).  INVALID_PARAM for a device that does not exist.  No libwebp
- * counterpart (libwebp has no devices). */
+ * wg_decode_into): 0 by default.  Replaces that context if it exists on another device; calls
+ * in flight finish on the context they started with, which is destroyed when the last of them
+ * returns.  INVALID_PARAM for a device that does not exist.  No libwebp counterpart (libwebp
+ * has no devices). */
 int wg_set_default_device(int device);
 
 /* ---- output options (WebPDecoderConfig subset, pkg/libwebp/webp/decode.go:59-83) --------- */
