@@ -165,10 +165,11 @@ struct wg_ctx {
   std::unique_ptr<wg::WorkerPool> pool;
   std::unique_ptr<wg::StagingArena> arena;
   DeviceCache cache;
-  // the pipelined decode (wg_decode_rgba_batch): a second staging arena and stream, so chunk
-  // k + 1's entropy stage and upload overlap chunk k's kernels and download
-  std::unique_ptr<wg::StagingArena> arena2;
-  hipStream_t stream2 = nullptr;
+  // the pipelined decode (wg_decode_rgba_batch): a second staging arena, and two work streams
+  // (kernels + download of alternate chunks) next to `stream`, which carries every chunk's
+  // upload -- so an upload never queues behind an earlier chunk's download
+  std::unique_ptr<wg::StagingArena> arena_ring[2];  // with `arena`, a ring of three
+  hipStream_t work[2] = {nullptr, nullptr};
   int chunk_frames = 0;  // frames per pipeline chunk, 0 = automatic (wg_ctx_set_chunk_frames)
   wg_pipeline_stats stats{};  // of the last pipelined decode
   wg::WorkerPool* workers() {
@@ -441,13 +442,15 @@ void wg_ctx_destroy(wg_ctx* c) {
   if (!c) return;
   const bool dev_ok = set_device(c->device);
   if (dev_ok && c->stream) hipStreamSynchronize(c->stream);
-  if (dev_ok && c->stream2) hipStreamSynchronize(c->stream2);
+  for (hipStream_t w : c->work)
+    if (dev_ok && w) hipStreamSynchronize(w);
   c->pool.reset();
   c->arena.reset();
-  c->arena2.reset();
+  for (auto& a : c->arena_ring) a.reset();
   c->cache.trim(0);
   if (c->stream) hipStreamDestroy(c->stream);
-  if (c->stream2) hipStreamDestroy(c->stream2);
+  for (hipStream_t w : c->work)
+    if (w) hipStreamDestroy(w);
   delete c;
 }
 
@@ -581,21 +584,38 @@ using BatchPtr = std::unique_ptr<wg_batch, BatchDeleter>;
 // Host half of a batch: every frame's host stages into `arena` (on the context's pool; the
 // caller holds ctx->mu), the layout of the planes / RGBA and the algorithmic bytes per kernel.
 // status[i] = frame i's status.  Nothing touches the device.
-BatchPtr batch_parse(wg_ctx* ctx, wg::StagingArena& arena, hipStream_t home, const uint8_t* const* data,
-                     const size_t* sizes, int n, const wg_decoder_options* opt, int32_t* status) {
-  if (status)
-    for (int i = 0; i < n; ++i) status[i] = WG_STATUS_OK;
+// An empty batch of n frames (their FrameParse records default-initialised).
+BatchPtr batch_init(wg_ctx* ctx, hipStream_t home, int n, const wg_decoder_options* opt) {
   BatchPtr bp(new wg_batch());
   wg_batch* b = bp.get();
   b->ctx = ctx;
   b->home = home;
   b->n = n;
   b->opt = *opt;
-  const int32_t flags = (opt->bypass_filtering ? WG_FLAG_BYPASS_FILTERING : 0) |
-                        (opt->no_fancy_upsampling ? WG_FLAG_NO_FANCY_UPSAMPLING : 0);
-  b->flags = flags;
+  b->flags = (opt->bypass_filtering ? WG_FLAG_BYPASS_FILTERING : 0) |
+             (opt->no_fancy_upsampling ? WG_FLAG_NO_FANCY_UPSAMPLING : 0);
+  b->fp.assign((size_t)n, FrameParse{});
+  return bp;
+}
+
+void batch_layout(wg_batch* b, wg::StagingArena& arena, int32_t* status);
+
+BatchPtr batch_parse(wg_ctx* ctx, wg::StagingArena& arena, hipStream_t home, const uint8_t* const* data,
+                     const size_t* sizes, int n, const wg_decoder_options* opt, int32_t* status) {
+  if (status)
+    for (int i = 0; i < n; ++i) status[i] = WG_STATUS_OK;
+  BatchPtr bp = batch_init(ctx, home, n, opt);
   arena.begin_batch();
-  wg::parse_all(data, sizes, n, *opt, ctx->workers(), &arena, b->fp);
+  wg::parse_all(data, sizes, n, *opt, ctx->workers(), &arena, bp->fp);
+  batch_layout(bp.get(), arena, status);
+  return bp;
+}
+
+// After every frame of the batch is parsed into `arena`: the arena's chunks laid out back to back
+// for the device, the layout of the planes / RGBA and the algorithmic bytes per kernel;
+// status[i] = frame i's status.
+void batch_layout(wg_batch* b, wg::StagingArena& arena, int32_t* status) {
+  const int n = b->n;
   b->in_bytes = std::max<size_t>(arena.layout(), kAlign);
   // layout of the planes / RGBA, and the algorithmic bytes per kernel
   size_t pl_b = 0, rg_b = 0;
@@ -693,7 +713,6 @@ BatchPtr batch_parse(wg_ctx* ctx, wg::StagingArena& arena, hipStream_t home, con
   b->kbytes[4] = k7;
   b->plane_bytes = std::max<size_t>(pl_b, kAlign);
   b->rgba_bytes = std::max<size_t>(rg_b, kAlign);
-  return bp;
 }
 
 // Device half: buffers (from the context's cache), descriptors, and the H2D copies of the staged
@@ -1108,6 +1127,7 @@ void pipe_finish(PipeChunk& c, int32_t* status, wg_pipeline_stats* ps) {
         if (status[c.a + j] == WG_STATUS_OK) status[c.a + j] = st;
   } else if (c.uploaded && c.b) {
     hipStreamSynchronize(c.s);  // (an error path: whatever of the chunk was queued has finished)
+    if (c.b->home) hipStreamSynchronize(c.b->home);
   }
   if (c.b) c.b->home = nullptr;  // complete: destroying it must not wait for later chunks on the stream
   c.b.reset();
@@ -1118,10 +1138,11 @@ void pipe_finish(PipeChunk& c, int32_t* status, wg_pipeline_stats* ps) {
     }
 }
 
-// wg_decode_rgba_batch: chunked, two staging arenas and two streams.  The calling thread runs
-// the entropy stage of chunk after chunk (with the context's pool); a device thread uploads
-// chunk k, launches its kernels, then queues chunk k - 1's download and retires chunk k - 2, so
-// the host stage of one chunk, the kernels of the next and the transfers of a third overlap.
+// wg_decode_rgba_batch: chunked, two staging arenas and two streams.  The calling thread and the
+// context's pool run the entropy stage over all frames; a device thread uploads chunk k as soon
+// as its last frame is parsed, launches its kernels, then queues chunk k - 1's download and
+// retires chunk k - 2, so the host stage of one chunk, the kernels of the next and the transfers
+// of a third overlap.
 int decode_pipelined(wg_ctx* ctx, const uint8_t* const* data, const size_t* sizes, int n, uint8_t* const* out,
                      const int32_t* strides, int32_t* status, int32_t flags) {
   const double t_start = now_s();
@@ -1170,21 +1191,28 @@ int decode_pipelined(wg_ctx* ctx, const uint8_t* const* data, const size_t* size
   ps.chunks = K;
   ps.host_threads = ctx->workers()->threads();
   if (K > 1) {
-    if (!ctx->arena2) ctx->arena2.reset(new wg::StagingArena(pinned_alloc, pinned_free));
-    if (!ctx->stream2 && hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking) != hipSuccess) {
-      (void)hipGetLastError();
-      ctx->stream2 = nullptr;
-      return WG_STATUS_OUT_OF_MEMORY;
-    }
+    for (auto& a : ctx->arena_ring)
+      if (!a) a.reset(new wg::StagingArena(pinned_alloc, pinned_free));
+    for (hipStream_t& w : ctx->work)
+      if (!w && hipStreamCreateWithFlags(&w, hipStreamNonBlocking) != hipSuccess) {
+        (void)hipGetLastError();
+        w = nullptr;
+        return WG_STATUS_OUT_OF_MEMORY;
+      }
   }
-  wg::StagingArena* arenas[2] = {ctx->arena.get(), ctx->arena2 ? ctx->arena2.get() : ctx->arena.get()};
-  hipStream_t streams[2] = {ctx->stream, ctx->stream2 ? ctx->stream2 : ctx->stream};
+  // staging arenas in a ring of three: chunk k parses into arena k % 3 once chunk k - 3's upload
+  // from it has completed
+  constexpr int kRing = 3;
+  wg::StagingArena* arenas[kRing] = {ctx->arena.get(), K > 1 ? ctx->arena_ring[0].get() : nullptr,
+                                     K > 1 ? ctx->arena_ring[1].get() : nullptr};
+  // one chunk: everything on the context stream; else uploads on it, the rest on a work stream
+  hipStream_t streams[2] = {K > 1 ? ctx->work[0] : ctx->stream, K > 1 ? ctx->work[1] : ctx->stream};
   std::vector<PipeChunk> ch((size_t)K);
   for (int k = 0; k < K; ++k) {
     PipeChunk& c = ch[(size_t)k];
     c.a = bounds[(size_t)k];
     c.n = bounds[(size_t)k + 1] - c.a;
-    c.arena = k & 1;
+    c.arena = k % kRing;
     c.s = streams[k & 1];
     for (hipEvent_t& e : c.ev)
       if (hipEventCreate(&e) != hipSuccess) {
@@ -1195,26 +1223,39 @@ int decode_pipelined(wg_ctx* ctx, const uint8_t* const* data, const size_t* size
         return WG_STATUS_OUT_OF_MEMORY;
       }
   }
+  // every chunk's batch up front (an allocation failure fails the call before any thread starts)
+  std::vector<int> chunk_of((size_t)n);
+  for (int k = 0; k < K; ++k) {
+    ch[(size_t)k].b = batch_init(ctx, ctx->stream, ch[(size_t)k].n, &o);  // home: the upload stream
+    for (int j = 0; j < ch[(size_t)k].n; ++j) chunk_of[(size_t)(ch[(size_t)k].a + j)] = k;
+  }
   std::mutex qmu;
   std::condition_variable qcv;
-  int parsed = 0, uploaded = 0;  // chunks handed to / uploaded by the device thread
+  // per chunk, under qmu: its arena is being readied / is ready; its frames are all parsed; its
+  // upload has been queued (the arena is reusable once ev[1] completes)
+  std::vector<char> started((size_t)K, 0), ready((size_t)K, 0), parsed((size_t)K, 0), uploaded((size_t)K, 0);
+  std::unique_ptr<std::atomic<int>[]> left(new std::atomic<int>[(size_t)K]);
+  for (int k = 0; k < K; ++k) left[k].store(ch[(size_t)k].n);
   auto device_side = [&] {
     set_device(ctx->device);
     for (int k = 0; k < K; ++k) {
       {
         std::unique_lock<std::mutex> ql(qmu);
-        qcv.wait(ql, [&] { return parsed > k; });
+        qcv.wait(ql, [&] { return parsed[(size_t)k] != 0; });
       }
       PipeChunk& c = ch[(size_t)k];
-      int st = WG_STATUS_OUT_OF_MEMORY;  // (no batch: its host stage ran out of memory)
-      hipEventRecord(c.ev[0], c.s);
-      if (c.b) st = guarded([&] { return batch_upload(c.b.get(), *arenas[c.arena]); });
-      hipEventRecord(c.ev[1], c.s);
+      hipEventRecord(c.ev[0], ctx->stream);
+      int st = guarded([&] { return batch_upload(c.b.get(), *arenas[c.arena]); });
+      hipEventRecord(c.ev[1], ctx->stream);
       c.up_ok = st == WG_STATUS_OK;
+      if (st == WG_STATUS_OK && c.s != ctx->stream && hipStreamWaitEvent(c.s, c.ev[1], 0) != hipSuccess) {
+        (void)hipGetLastError();
+        st = WG_STATUS_USER_ABORT;
+      }
       {
         std::lock_guard<std::mutex> ql(qmu);
         c.uploaded = true;
-        uploaded = k + 1;
+        uploaded[(size_t)k] = 1;
       }
       qcv.notify_all();
       if (st == WG_STATUS_OK) st = wg_batch_run(c.b.get(), c.s);
@@ -1230,34 +1271,49 @@ int decode_pipelined(wg_ctx* ctx, const uint8_t* const* data, const size_t* size
   };
   std::thread dev;
   if (K > 1) dev = std::thread(device_side);
-  double t_parsed = t_start;
-  for (int k = 0; k < K; ++k) {
+  // The entropy stage as ONE pool run over all frames, claimed in order: a chunk's stragglers
+  // overlap the next chunk's frames (no barrier per chunk).  A chunk's first frame readies its
+  // arena (chunk k - 3, on the same arena, uploaded); its last frame lays it out and hands it to
+  // the device thread.
+  wg::WorkerPool* pool = ctx->workers();
+  std::vector<wg::StagingArena::Cursor> cursors[kRing];
+  for (auto& cv : cursors) cv.resize((size_t)pool->threads() + 1);
+  const double t_parse0 = now_s();
+  pool->run(n, [&](int i, int worker) {
+    const int k = chunk_of[(size_t)i];
     PipeChunk& c = ch[(size_t)k];
-    if (k >= 2) {  // the chunk two back used this arena: its upload must have completed
-      const double t0 = now_s();
-      {
-        std::unique_lock<std::mutex> ql(qmu);
-        qcv.wait(ql, [&] { return uploaded > k - 2; });
-      }
-      if (ch[(size_t)k - 2].up_ok) hipEventSynchronize(ch[(size_t)k - 2].ev[1]);
-      ps.parse_wait_s += now_s() - t0;
-    }
-    const double t0 = now_s();
-    try {
-      c.b = batch_parse(ctx, *arenas[c.arena], c.s, data + c.a, sizes + c.a, c.n, &o, status + c.a);
-      ps.h2d_bytes += (double)c.b->in_bytes;
-    } catch (const std::exception&) {  // host-side vectors: the chunk's frames fail, the others go on
-      c.b.reset();
-      for (int j = 0; j < c.n; ++j) status[c.a + j] = WG_STATUS_OUT_OF_MEMORY;
-    }
-    ps.parse_s += now_s() - t0;
-    t_parsed = now_s();
     {
-      std::lock_guard<std::mutex> ql(qmu);
-      parsed = k + 1;
+      std::unique_lock<std::mutex> ql(qmu);
+      if (!started[(size_t)k]) {
+        started[(size_t)k] = 1;
+        const double t0 = now_s();
+        if (k >= kRing) {
+          qcv.wait(ql, [&] { return uploaded[(size_t)(k - kRing)] != 0; });
+          ql.unlock();
+          if (ch[(size_t)(k - kRing)].up_ok) hipEventSynchronize(ch[(size_t)(k - kRing)].ev[1]);
+          ql.lock();
+        }
+        arenas[c.arena]->begin_batch();
+        ready[(size_t)k] = 1;
+        ps.parse_wait_s += now_s() - t0;
+        qcv.notify_all();
+      } else {
+        qcv.wait(ql, [&] { return ready[(size_t)k] != 0; });
+      }
     }
-    qcv.notify_all();
-  }
+    wg::parse_frame(data[i], sizes[i], o, arenas[c.arena], &cursors[c.arena][(size_t)worker],
+                    &c.b->fp[(size_t)(i - c.a)]);
+    if (left[k].fetch_sub(1) == 1) {
+      for (auto& cu : cursors[c.arena]) arenas[c.arena]->release(&cu);
+      batch_layout(c.b.get(), *arenas[c.arena], status + c.a);
+      std::lock_guard<std::mutex> ql(qmu);
+      ps.h2d_bytes += (double)c.b->in_bytes;
+      parsed[(size_t)k] = 1;
+      qcv.notify_all();
+    }
+  });
+  const double t_parsed = now_s();
+  ps.parse_s = t_parsed - t_parse0;
   if (K > 1) dev.join();
   else device_side();
   const double t_end = now_s();

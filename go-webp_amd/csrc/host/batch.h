@@ -67,6 +67,10 @@ int apply_output_options(const wg_decoder_options& opt, FrameParse* f);
 int parse_one(const uint8_t* data, size_t size, const wg_decoder_options& opt, StagingArena* arena,
               StagingArena::Cursor* cur, FrameParse* fp);
 
+// parse_one with its failure handling: a failed frame keeps only its status (nothing throws).
+void parse_frame(const uint8_t* data, size_t size, const wg_decoder_options& opt, StagingArena* arena,
+                 StagingArena::Cursor* cur, FrameParse* f);
+
 // parse_one over n frames on the pool (one frame per task).  A failed frame keeps only its
 // status; nothing throws.
 void parse_all(const uint8_t* const* data, const size_t* sizes, int n, const wg_decoder_options& opt,

@@ -226,23 +226,26 @@ int parse_one(const uint8_t* data, size_t size, const wg_decoder_options& opt, S
   return st;
 }
 
+void parse_frame(const uint8_t* data, size_t size, const wg_decoder_options& opt, StagingArena* arena,
+                 StagingArena::Cursor* cur, FrameParse* f) {
+  if (data == nullptr) {
+    f->status = WG_STATUS_INVALID_PARAM;
+    return;
+  }
+  f->status = guarded([&] { return parse_one(data, size, opt, arena, cur, f); });
+  if (f->status != WG_STATUS_OK) {  // drop partial host data
+    const int st = f->status;
+    *f = FrameParse();
+    f->status = st;
+  }
+}
+
 void parse_all(const uint8_t* const* data, const size_t* sizes, int n, const wg_decoder_options& opt,
                WorkerPool* pool, StagingArena* arena, std::vector<FrameParse>& out) {
   out.assign((size_t)n, FrameParse{});
   std::vector<StagingArena::Cursor> cursors((size_t)pool->threads() + 1);
   pool->run(n, [&](int i, int worker) {
-    FrameParse& f = out[(size_t)i];
-    if (data[i] == nullptr) {
-      f.status = WG_STATUS_INVALID_PARAM;
-      return;
-    }
-    StagingArena::Cursor* cur = &cursors[(size_t)worker];
-    f.status = guarded([&] { return parse_one(data[i], sizes[i], opt, arena, cur, &f); });
-    if (f.status != WG_STATUS_OK) {  // drop partial host data
-      const int st = f.status;
-      f = FrameParse();
-      f.status = st;
-    }
+    parse_frame(data[i], sizes[i], opt, arena, &cursors[(size_t)worker], &out[(size_t)i]);
   });
   for (auto& c : cursors) arena->release(&c);
 }
