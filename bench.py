@@ -69,6 +69,38 @@ def _traffic(workload):
         return None
 
 
+def _valu_ceiling():
+    """Static-mix VALU issue ceilings per kernel (scripts/valu_ceiling.py), if present."""
+    p = os.path.join(ROOT, "profiles", "valu_ceiling.json")
+    try:
+        with open(p) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return {}
+
+
+CUS = 256  # MI355X compute units (4 SIMDs each)
+
+
+def valu_roof(kernel, workload, ms, n_workgroups):
+    """The instruction-issue ceiling of a kernel that is not HBM-bound: measured VALU
+    wave-instructions per launch (committed SQ_INSTS_VALU, profiles/pmc_traffic.json) over the
+    SIMDs its workgroups occupy and this run's launch time, against the probe-based ceiling for
+    its instruction mix (profiles/valu_ceiling.json); plus VALUUtilization (active lanes)."""
+    tr = ((_traffic(workload) or {}).get(kernel) or {}).get("valu")
+    ce = _valu_ceiling().get(kernel)
+    if not tr or not ce or ms <= 0:
+        return None
+    simds = 4 * min(CUS, max(1, n_workgroups))
+    ach = tr["insts_valu"] / (simds * ms * 1e6)
+    peak = ce["ceiling_valu_per_ns_per_simd"]
+    return {"bound": "valu", "achieved": round(ach, 4), "peak": peak, "unit": "VALU wave-instr / ns / SIMD",
+            "frac": round(ach / peak, 4), "insts_valu_per_launch": tr["insts_valu"], "simds": simds,
+            "valu_utilization": tr.get("valu_utilization"),
+            "note": "issue rate from the committed SQ_INSTS_VALU (rocprofv3 --pmc) over this run's launch time; "
+                    "peak = probe-measured issue cost of the kernel's static instruction mix (DESIGN.md 4)"}
+
+
 def shard_frames(datas, rank, batch):
     """Frames of one rank: `batch` frames cycling the distinct bitstreams, offset by rank
     (independent frames, no exchange between ranks -- SURVEY §8(e))."""
@@ -440,6 +472,10 @@ def main():
                     "avg_launch_ms": round(ms, 4)}
         ran = [k for k in range(len(KERNELS)) if kms[k] > 0]
         roofs = {KERNELS[k]: roof(kby[k], kms[k], KERNELS[k]) for k in ran}
+        for k in ran:  # the second ceiling: instruction issue (K2 spreads over every CU)
+            vr = valu_roof(KERNELS[k], wl["name"], kms[k], CUS if k == 1 else args.batch)
+            if vr:
+                roofs[KERNELS[k]]["valu"] = vr
         dominant = roofs[KERNELS[max(ran, key=lambda k: kms[k])]] if ran else None
         if dominant and dominant["kernel"] == "vp8_recon_filter_kernel":
             # measured limiter: instruction issue / latency on the frame's CU, not HBM
@@ -448,6 +484,9 @@ def main():
             roofs["yuv_to_rgba_kernel"] = dict(roof(kby[1], stage_ms, "yuv_to_rgba_kernel"),
                                                note="stage timed alone over the same planes; in the "
                                                     "timed steps K1's tail performs it (--emit fused)")
+            vr = valu_roof("yuv_to_rgba_kernel", wl["name"], stage_ms, CUS)
+            if vr:
+                roofs["yuv_to_rgba_kernel"]["valu"] = vr
         out = {
             "metric": "decoded MPixels/sec at 1/2/4/8 GPUs; % HBM roofline (YUV->RGBA)",
             "value": round(value, 1),

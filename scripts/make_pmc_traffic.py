@@ -36,15 +36,28 @@ def per_kernel(d):
             if g == top:
                 acc[(key, name)].append(v)
     out = {}
+    avg = lambda key, name: sum(acc[(key, name)]) / len(acc[(key, name)]) if acc.get((key, name)) else None  # noqa: E731
     for key in KERNELS:
         fetch = acc.get((key, "FETCH_SIZE"))
         write = acc.get((key, "WRITE_SIZE"))
-        if not fetch or not write:
-            continue
-        fb = 2.0 * 1024 * sum(fetch) / len(fetch)
-        wb = 1024.0 * sum(write) / len(write)
-        out[key] = {"bytes": int(fb + wb), "read_bytes": int(fb), "write_bytes": int(wb),
-                    "launches": len(fetch), "source": os.path.relpath(d, ROOT)}
+        ent = {}
+        if fetch and write:
+            fb = 2.0 * 1024 * sum(fetch) / len(fetch)
+            wb = 1024.0 * sum(write) / len(write)
+            ent = {"bytes": int(fb + wb), "read_bytes": int(fb), "write_bytes": int(wb),
+                   "launches": len(fetch), "source": os.path.relpath(d, ROOT)}
+        # instruction issue (SQ counters, per launch): VALU wave-instructions, and the share of
+        # lanes active in them, VALUUtilization = SQ_THREAD_CYCLES_VALU / (64 SQ_ACTIVE_INST_VALU)
+        valu, act, thr = avg(key, "SQ_INSTS_VALU"), avg(key, "SQ_ACTIVE_INST_VALU"), avg(key, "SQ_THREAD_CYCLES_VALU")
+        if valu:
+            ent["valu"] = {"insts_valu": int(valu), "insts_salu": int(avg(key, "SQ_INSTS_SALU") or 0),
+                           "insts_lds": int(avg(key, "SQ_INSTS_LDS") or 0),
+                           "valu_utilization": round(thr / (64.0 * act), 4) if thr and act else None,
+                           "wait_any_frac": round(avg(key, "SQ_WAIT_ANY") / avg(key, "SQ_WAVE_CYCLES"), 4)
+                           if avg(key, "SQ_WAIT_ANY") and avg(key, "SQ_WAVE_CYCLES") else None,
+                           "source": os.path.relpath(d, ROOT)}
+        if ent:
+            out[key] = ent
     return out
 
 
@@ -53,9 +66,13 @@ def main():
     data = json.load(open(path)) if os.path.exists(path) else {}
     args = sys.argv[1:]
     for name, d in zip(args[0::2], args[1::2]):
-        data[name] = per_kernel(d)
+        new = per_kernel(d)
+        for k, v in new.items():  # a pass set with only traffic (or only SQ counters) keeps the other
+            data.setdefault(name, {}).setdefault(k, {}).update(v)
     data["_note"] = ("HBM bytes per launch: 2*FETCH_SIZE + WRITE_SIZE (KiB->B), rocprofv3 --pmc in separate "
-                     "passes (scripts/profile.sh); FETCH_SIZE doubling per MI355X_MICROARCH.md gfx950 note")
+                     "passes (scripts/profile.sh); FETCH_SIZE doubling per MI355X_MICROARCH.md gfx950 note. "
+                     "valu: SQ instruction counters per launch; valu_utilization = SQ_THREAD_CYCLES_VALU / "
+                     "(64 * SQ_ACTIVE_INST_VALU)")
     json.dump(data, open(path, "w"), indent=1, sort_keys=True)
     print(json.dumps(data, indent=1, sort_keys=True))
 
