@@ -262,6 +262,31 @@ int get_coeffs(BoolReader* br, const BandProbas* const* prob, int ctx, const int
   return get_coeffs_t<false>(br, prob, ctx, dq, n, out);
 }
 
+// GetCoeffs entered after its first "not the last coefficient" bit (p[0] of coefficient n
+// read as 1): the same token walk as get_coeffs_t from the zero-run loop on.  The sparse path
+// reads that first bit itself, so a block whose first token is EOB (two thirds of c3's
+// blocks) costs one bit -- no call, no zeroing of its slot.
+int get_coeffs_after_first(BoolReader* br, const BandProbas* const* prob, const uint8_t* p, const int* dq, int n,
+                           int16_t* out) {
+  for (;;) {
+    while (!br->get_bit(p[1])) {  // sequence of zero coeffs
+      p = prob[++n]->p[0];
+      if (n == 16) return 16;
+    }
+    const BandProbas* const p_ctx = prob[n + 1];
+    int v;
+    if (!br->get_bit(p[2])) {
+      v = 1;
+      p = p_ctx->p[1];
+    } else {
+      v = get_large_value(br, p);
+      p = p_ctx->p[2];
+    }
+    out[kZigzagColMajor[n]] = (int16_t)(br->get_signed(v) * dq[n > 0]);  // wraps
+    if (++n == 16 || !br->get_bit(p[0])) return n;  // previous coeff was last non-zero coeff
+  }
+}
+
 inline uint32_t nz_code_bits(uint32_t nz_coeffs, int nz, int dc_nz) {  // vp8_dec.go:588-598
   nz_coeffs <<= 2;
   nz_coeffs |= (nz > 3) ? 3 : (nz > 1) ? 2 : dc_nz;
@@ -493,12 +518,16 @@ uint32_t parse_residuals_sparse(Decoder* d, MBCtx* mb, MBCtx* left_mb, BoolReade
     uint32_t nz_coeffs = 0;
     for (int x = 0; x < 4; ++x) {
       int16_t* ob = out + 16 * nb;
-      std::memset(ob, 0, 32);
       const int ctx = l + (tnz & 1);
-      const int nz = get_coeffs_t<true>(token_br, ac_proba, ctx, d->dq_y1[seg], first, ob);
+      const uint8_t* p0 = ac_proba[first]->p[ctx];
+      int nz = first;
+      if (token_br->get_bit(p0[0])) {
+        std::memset(ob, 0, 32);
+        nz = get_coeffs_after_first(token_br, ac_proba, p0, d->dq_y1[seg], first, ob);
+      }
       l = (nz > first);
       tnz = (uint8_t)((tnz >> 1) | (l << 7));
-      nz_coeffs = nz_code_bits(nz_coeffs, nz, (first ? dcs[4 * y + x] : ob[0]) != 0);
+      nz_coeffs = nz_code_bits(nz_coeffs, nz, (first ? dcs[4 * y + x] : nz > 0 ? ob[0] : 0) != 0);
       // (nz == first: no coefficient was decoded; past it one may still wrap to 0 in int16)
       if (nz > first && block_nonzero(ob)) {
         mask |= 1u << (4 * y + x);
@@ -518,12 +547,16 @@ uint32_t parse_residuals_sparse(Decoder* d, MBCtx* mb, MBCtx* left_mb, BoolReade
       int l = lnz & 1;
       for (int x = 0; x < 2; ++x) {
         int16_t* ob = out + 16 * nb;
-        std::memset(ob, 0, 32);
         const int ctx = l + (tnz & 1);
-        const int nz = get_coeffs_t<true>(token_br, bands[2], ctx, d->dq_uv[seg], 0, ob);
+        const uint8_t* p0 = bands[2][0]->p[ctx];
+        int nz = 0;
+        if (token_br->get_bit(p0[0])) {
+          std::memset(ob, 0, 32);
+          nz = get_coeffs_after_first(token_br, bands[2], p0, d->dq_uv[seg], 0, ob);
+        }
         l = (nz > 0);
         tnz = (uint8_t)((tnz >> 1) | (l << 3));
-        nz_coeffs = nz_code_bits(nz_coeffs, nz, ob[0] != 0);
+        nz_coeffs = nz_code_bits(nz_coeffs, nz, nz > 0 && ob[0] != 0);
         if (nz > 0 && block_nonzero(ob)) {
           mask |= 1u << (16 + 2 * ch + 2 * y + x);
           ++nb;
