@@ -1131,11 +1131,8 @@ void pipe_finish(PipeChunk& c, int32_t* status, wg_pipeline_stats* ps) {
   }
   if (c.b) c.b->home = nullptr;  // complete: destroying it must not wait for later chunks on the stream
   c.b.reset();
-  for (hipEvent_t& e : c.ev)
-    if (e) {
-      hipEventDestroy(e);
-      e = nullptr;
-    }
+  // (the events outlive the chunk: a pool thread readying arena k mod 3 for chunk k + 3 may still be
+  // waiting on ev[1]; decode_pipelined destroys them once every thread is done)
 }
 
 // wg_decode_rgba_batch: chunked, two staging arenas and two streams.  The calling thread and the
@@ -1316,6 +1313,9 @@ int decode_pipelined(wg_ctx* ctx, const uint8_t* const* data, const size_t* size
   ps.parse_s = t_parsed - t_parse0;
   if (K > 1) dev.join();
   else device_side();
+  for (PipeChunk& c : ch)
+    for (hipEvent_t& e : c.ev)
+      if (e) hipEventDestroy(e), e = nullptr;
   const double t_end = now_s();
   ps.drain_s = t_end - t_parsed;
   ps.wall_s = t_end - t_start;

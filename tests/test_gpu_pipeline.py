@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 
 import webp_amd
-from oracle_lib import load_lossy, load_lossless
+from oracle_lib import load_alpha, load_lossless, load_lossy
 from test_gpu_multi import _c2_frames
 
 pytestmark = pytest.mark.gpu
@@ -82,5 +82,31 @@ def test_bad_frames_and_mixed_content_across_chunks():
         assert _sha(got[0]) == want[0] and _sha(got[5]) == want[2] and _sha(got[8]) == want[3]
         assert np.array_equal(got[2], gold["rgba"]) and np.array_equal(got[6], gold["rgba"])
         assert np.array_equal(got[4], llgold["rgba"]) and np.array_equal(got[9], llgold["rgba"])
+    finally:
+        ctx.close()
+
+
+def test_alpha_and_wide_frames_across_chunks():
+    """VP8+ALPH frames (K4 after K1 / K3 in each chunk) and frames wider than K1's LDS column
+    store (its global-column instantiation) in chunks of one to three frames: every frame equals
+    libwebp's RGBA."""
+    names = ["a_ll_best_g_96x64", "a_raw_h_71x33", "a_ll_g_120x1100", "a_ll_q50_80x80"]
+    alpha = [load_alpha(n) for n in names]
+    wide = [load_lossy(n) for n in ("wide_9617x40", "wide_16383x17_simple")]
+    frames_c2, want_c2 = _c2_frames(2)
+    datas = [alpha[0][0], wide[0][0], frames_c2[0], alpha[1][0], alpha[2][0], wide[1][0], alpha[3][0],
+             frames_c2[1]]
+    golds = [alpha[0][1]["rgba"], wide[0][1]["rgba"], None, alpha[1][1]["rgba"], alpha[2][1]["rgba"],
+             wide[1][1]["rgba"], alpha[3][1]["rgba"], None]
+    ctx = webp_amd.Context(0, host_threads=3)
+    try:
+        for chunk in (1, 2, 3):
+            ctx.set_chunk_frames(chunk)
+            got, st = ctx.decode_batch(datas)
+            assert (st == 0).all(), (chunk, st)
+            for i, (g, want) in enumerate(zip(got, golds)):
+                if want is not None:
+                    assert np.array_equal(g, want), (chunk, i)
+            assert _sha(got[2]) == want_c2[0] and _sha(got[7]) == want_c2[1]
     finally:
         ctx.close()
