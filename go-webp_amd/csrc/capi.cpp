@@ -1153,7 +1153,7 @@ int decode_pipelined(wg_ctx* ctx, const uint8_t* const* data, const size_t* size
     for (int i = 0; i < n; ++i) status[i] = WG_STATUS_INVALID_PARAM;
     return WG_STATUS_INVALID_PARAM;
   }
-  // chunks: a fixed frame count, or about an eighth of the batch's pixels (>= 64 MPix each)
+  // chunks: a fixed frame count, or about a sixteenth of the batch's pixels (>= 32 MPix each)
   std::vector<int> bounds{0};
   if (ctx->chunk_frames > 0) {
     for (int a = ctx->chunk_frames; a < n; a += ctx->chunk_frames) bounds.push_back(a);
@@ -1167,7 +1167,7 @@ int decode_pipelined(wg_ctx* ctx, const uint8_t* const* data, const size_t* size
     }
     // Only the last chunk's device work (upload, kernels, download) is exposed after the host
     // stage ends, so the batch's last 2T of pixels go in halving chunks: R/2, R/4, R/8, R/8.
-    const double T = std::max(64e6, total / 8);
+    const double T = std::max(32e6, total / 16);
     double target = T, acc = 0, consumed = 0, tail_r = 0;
     int tail = 0;
     for (int i = 0; i < n; ++i) {

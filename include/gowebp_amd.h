@@ -133,9 +133,9 @@ int wg_decode_rgba_batch(wg_ctx* ctx, const uint8_t* const* data, const size_t* 
                          uint8_t* const* rgba, const int32_t* strides, int32_t* status,
                          int32_t flags);
 
-/* Frames per pipeline chunk of wg_decode_rgba_batch (0 = automatic: about an eighth of the
- * batch's pixels, at least 64 MPix per chunk; n >= the batch = no pipelining).  INVALID_PARAM
- * for a negative count.  No libwebp counterpart. */
+/* Frames per pipeline chunk of wg_decode_rgba_batch (0 = automatic: about a sixteenth of the
+ * batch's pixels, at least 32 MPix per chunk, the last chunks halving; n >= the batch = no
+ * pipelining).  INVALID_PARAM for a negative count.  No libwebp counterpart. */
 int wg_ctx_set_chunk_frames(wg_ctx* ctx, int frames);
 
 /* Where the time of the context's last wg_decode_rgba_batch went.  Host times are wall clock
