@@ -403,6 +403,7 @@ def main():
             dist.barrier()
 
     wl = WORKLOADS[args.workload]
+    oversubscribed = False
     if args.mock:
         datas, bpp = _load_frames(wl["prefix"])  # (the CPU baseline legs still run for real)
         b, ctx, t_prep, stream = _MockBatch(), _MockContext(), 0.0, None
@@ -410,11 +411,16 @@ def main():
         sync = lambda: None  # noqa: E731
     else:
         import webp_amd
-        torch.cuda.set_device(local)
+        # one GPU per rank; more ranks than GPUs (a rehearsal of the multi-rank path on a small box)
+        # share devices round-robin and say so in the line (`oversubscribed`: not a scaling figure)
+        ndev = torch.cuda.device_count()
+        device = local % max(1, ndev)
+        oversubscribed = world > ndev
+        torch.cuda.set_device(device)
         datas, bpp = _load_frames(wl["prefix"])
         frames = shard_frames(datas, rank, args.batch)
         ctx_threads = rank_host_threads(args.host_threads, world)
-        ctx = webp_amd.Context(local, host_threads=ctx_threads)
+        ctx = webp_amd.Context(device, host_threads=ctx_threads)
         t_prep = time.perf_counter()
         b = ctx.batch(frames)
         t_prep = time.perf_counter() - t_prep
@@ -514,6 +520,9 @@ def main():
         }
         if args.mock:
             out["mock"] = True
+        if oversubscribed:
+            out["oversubscribed"] = ("more ranks than GPUs: ranks share devices round-robin; a rehearsal of the "
+                                     "multi-rank path, not a scaling figure")
         if "yuv_to_rgba_kernel" in roofs:
             out["roofline_yuv_to_rgba"] = roofs["yuv_to_rgba_kernel"]
         if e2e is not None:
