@@ -498,8 +498,16 @@ uint32_t parse_residuals_sparse(Decoder* d, MBCtx* mb, MBCtx* left_mb, BoolReade
     mb->nz_dc = left_mb->nz_dc = (nz > 0);
     if (block_nonzero(y2)) {
       // nz <= 1: libwebp's shortcut (dc[0] + 3) >> 3 for all 16, which is what the full
-      // transform gives for a DC-only input (vp8_dec.go:620-628)
-      transform_wht_colmajor(y2, dcs);
+      // transform gives for a DC-only input (vp8_dec.go:620-628) -- taken here too when only the
+      // DC is non-zero (the common case), the full transform otherwise
+      uint64_t w[4];
+      std::memcpy(w, y2, 32);
+      if ((w[0] & ~0xffffull) == 0 && (w[1] | w[2] | w[3]) == 0) {
+        const int16_t dc0 = (int16_t)((y2[0] + 3) >> 3);
+        for (int i = 0; i < 16; ++i) dcs[i] = dc0;
+      } else {
+        transform_wht_colmajor(y2, dcs);
+      }
       mask |= kY2Bit;
       nb = 1;
     } else {
