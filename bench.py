@@ -396,7 +396,18 @@ def main():
     if world > 1:
         import datetime
         import torch.distributed as dist
-        dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=600))
+        # Gloo reports each rank's connections on the C-level stdout: route them to stderr so that
+        # stdout carries only rank 0's JSON line (the driver's contract)
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=600))
+            dist.barrier()
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
 
     def barrier():
         if dist is not None:
