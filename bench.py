@@ -493,10 +493,12 @@ def main():
             vr = valu_roof(KERNELS[k], wl["name"], kms[k], CUS if k == 1 else args.batch)
             if vr:
                 roofs[KERNELS[k]]["valu"] = vr
+                # the ceiling the kernel is closest to (the contract's `bound` names the HBM roofline)
+                roofs[KERNELS[k]]["binding"] = "valu" if vr["frac"] > roofs[KERNELS[k]]["frac"] else "hbm"
         dominant = roofs[KERNELS[max(ran, key=lambda k: kms[k])]] if ran else None
         if dominant and dominant["kernel"] == "vp8_recon_filter_kernel":
             # measured limiter: instruction issue / latency on the frame's CU, not HBM
-            dominant["limiter"] = "per-wave issue and latency on the frame's CU (DESIGN.md §4)"
+            dominant["limiter"] = "VALU instruction issue on the frame's CU (roofline.valu; DESIGN.md §4)"
         if stage_ms > 0:
             roofs["yuv_to_rgba_kernel"] = dict(roof(kby[1], stage_ms, "yuv_to_rgba_kernel"),
                                                note="stage timed alone over the same planes; in the "
@@ -504,6 +506,8 @@ def main():
             vr = valu_roof("yuv_to_rgba_kernel", wl["name"], stage_ms, CUS)
             if vr:
                 roofs["yuv_to_rgba_kernel"]["valu"] = vr
+                roofs["yuv_to_rgba_kernel"]["binding"] = ("valu" if vr["frac"] > roofs["yuv_to_rgba_kernel"]["frac"]
+                                                          else "hbm")
         out = {
             "metric": "decoded MPixels/sec at 1/2/4/8 GPUs; % HBM roofline (YUV->RGBA)",
             "value": round(value, 1),
