@@ -337,7 +337,8 @@ __device__ __forceinline__ int absd(int a, int b, int c = 0) {
 // KIND 0: simple (NeedsFilter + DoFilter2, dec.c.go:552-586);
 // KIND 1: complex MB edge (FilterLoop26: hev ? DoFilter2 : DoFilter6, :592-606);
 // KIND 2: complex inner edge (FilterLoop24: hev ? DoFilter2 : DoFilter4, :608-622).
-// Branch-free: every variant is computed and selected.  t2 = 2*thresh + 1.
+// The masks are computed for every line; the complex kinds then update the samples under the
+// lane mask of the lines that filter (see below).  t2 = 2*thresh + 1.
 template <int KIND>
 __device__ __forceinline__ void filter_line(Line& l, int t2, int it, int hev_t) {
   const int d0 = l.q0 - l.p0;
@@ -345,11 +346,12 @@ __device__ __forceinline__ void filter_line(Line& l, int t2, int it, int hev_t) 
   const bool edge_ok = absd(l.p1, l.q1, 4 * absd(l.p0, l.q0)) <= t2;
   // DoFilter2 (24-bit multiplies: a 32-bit 3*d0 + sp became a quarter-rate v_mad_u64_u32)
   const int a = __mul24(d0, 3) + sp;
-  const int f2p0 = clamp255(l.p0 + sclip2((a + 3) >> 3));
-  const int f2q0 = clamp255(l.q0 - sclip2((a + 4) >> 3));
+  auto f2p0 = [&] { return clamp255(l.p0 + sclip2((a + 3) >> 3)); };
+  auto f2q0 = [&] { return clamp255(l.q0 - sclip2((a + 4) >> 3)); };
   if (KIND == 0) {
-    l.p0 = edge_ok ? f2p0 : l.p0;
-    l.q0 = edge_ok ? f2q0 : l.q0;
+    const int np0 = f2p0(), nq0 = f2q0();
+    l.p0 = edge_ok ? np0 : l.p0;
+    l.q0 = edge_ok ? nq0 : l.q0;
     return;
   }
   const int dp = absd(l.p1, l.p0), dq = absd(l.q1, l.q0);
@@ -358,6 +360,48 @@ __device__ __forceinline__ void filter_line(Line& l, int t2, int it, int hev_t) 
   const bool on = edge_ok & (max(in_p, in_q) <= it);  // & not &&: no short-circuit branch
   const bool hv = max(dp, dq) > hev_t;
   const bool f2 = on & hv, fx = on & !hv;
+#ifndef WG_FILTER_SELECT  // (measurement build: the round-3 select form)
+  // Exec-masked updates instead of selects: the new values are written under the lane mask of
+  // the lines that filter, so no v_cndmask per sample (a "complex" op: twice the issue cost of
+  // a plain one) -- the mask costs a few scalar instructions per region instead.  The empty asm
+  // keeps each region a branch (the compiler would flatten it back into selects).
+  if (KIND == 1) {  // DoFilter6, or DoFilter2 on hev lines
+    if (on) {
+      asm volatile("");
+      if (hv) {  // (DoFilter2 computed only where some line of the wave needs it)
+        asm volatile("");
+        const int np0 = f2p0(), nq0 = f2q0();
+        l.p0 = np0;
+        l.q0 = nq0;
+      } else {
+        asm volatile("");
+        const int w = sclip1(a);
+        const int a1 = (__mul24(w, 27) + 63) >> 7, a2 = (__mul24(w, 18) + 63) >> 7, a3 = (__mul24(w, 9) + 63) >> 7;
+        l.p2 = clamp255(l.p2 + a3);
+        l.p1 = clamp255(l.p1 + a2);
+        l.p0 = clamp255(l.p0 + a1);
+        l.q0 = clamp255(l.q0 - a1);
+        l.q1 = clamp255(l.q1 - a2);
+        l.q2 = clamp255(l.q2 - a3);
+      }
+    }
+  } else {
+    if (on) {
+      asm volatile("");
+      const int a = __mul24(d0, 3) + (hv ? sp : 0);
+      const int a1 = sclip2((a + 4) >> 3), a2 = sclip2((a + 3) >> 3), a3 = (a1 + 1) >> 1;
+      l.p0 = clamp255(l.p0 + a2);
+      l.q0 = clamp255(l.q0 - a1);
+      if (!hv) {
+        asm volatile("");
+        l.p1 = clamp255(l.p1 + a3);
+        l.q1 = clamp255(l.q1 - a3);
+      }
+    }
+  }
+  (void)f2;
+  (void)fx;
+#else
   if (KIND == 1) {  // DoFilter6
     const int w = sclip1(a);
     const int a1 = (__mul24(w, 27) + 63) >> 7, a2 = (__mul24(w, 18) + 63) >> 7, a3 = (__mul24(w, 9) + 63) >> 7;
@@ -367,8 +411,9 @@ __device__ __forceinline__ void filter_line(Line& l, int t2, int it, int hev_t) 
     l.p1 = fx ? np1 : l.p1;
     l.q1 = fx ? nq1 : l.q1;
     l.q2 = fx ? nq2 : l.q2;
-    l.p0 = fx ? np0 : (f2 ? f2p0 : l.p0);
-    l.q0 = fx ? nq0 : (f2 ? f2q0 : l.q0);
+    const int g0 = f2p0(), h0 = f2q0();
+    l.p0 = fx ? np0 : (f2 ? g0 : l.p0);
+    l.q0 = fx ? nq0 : (f2 ? h0 : l.q0);
   } else {  // DoFilter4, or DoFilter2 on hev lines: both are p0 += sclip2((a+3)>>3),
             // q0 -= sclip2((a+4)>>3) with a = 3*(q0-p0) [+ sclip1(p1-q1) when hev]
     const int a = __mul24(d0, 3) + (hv ? sp : 0);
@@ -380,6 +425,7 @@ __device__ __forceinline__ void filter_line(Line& l, int t2, int it, int hev_t) 
     l.p0 = on ? np0 : l.p0;
     l.q0 = on ? nq0 : l.q0;
   }
+#endif
 }
 
 // One edge on eight consecutive samples v[0..7] = p3..q3 held in registers.
