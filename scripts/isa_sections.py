@@ -79,11 +79,13 @@ def main():
             cnt.setdefault(cur, collections.Counter())[cls] += 1
             if cls == "valu":
                 cnt[cur]["units"] += valu_units(op)
+                if op.startswith(("v_readlane", "v_writelane")):
+                    cnt[cur]["spill"] += 1  # SGPR spills through VGPR lanes
     tot = collections.Counter()
     for k, v in cnt.items():
-        print(f"{k:10s} " + " ".join(f"{c}={v[c]:g}" for c in ("valu", "units", "salu", "lds", "vmem")))
+        print(f"{k:10s} " + " ".join(f"{c}={v[c]:g}" for c in ("valu", "units", "salu", "lds", "vmem", "spill")))
         tot += v
-    print("total      " + " ".join(f"{c}={tot[c]:g}" for c in ("valu", "units", "salu", "lds", "vmem")), meta)
+    print("total      " + " ".join(f"{c}={tot[c]:g}" for c in ("valu", "units", "salu", "lds", "vmem", "spill")), meta)
 
 
 if __name__ == "__main__":
