@@ -892,22 +892,21 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
           {
             uint8_t* org = ws + Y_OFF + 4 * by * BPS + 4 * bx;
             const uint32_t ew = e[j];
-            const int kind = ew >> 24;
-            const int a = org[(int8_t)(ew & 0xff)];
-            const int b = org[(int8_t)((ew >> 8) & 0xff)];
-            const int c = org[(int8_t)((ew >> 16) & 0xff)];
             int v;
-            if (kind == 3) {  // DC4
+            if (ew == 0xC0000000u) {  // DC4 (pred4_table.inc: the one DC word)
               const uint32_t s = __builtin_amdgcn_sad_u8(ld32(org - BPS), 0, 0);
               v = (int)(s + org[-1] + org[BPS - 1] + org[2 * BPS - 1] + org[3 * BPS - 1] + 4) >> 3;
             } else {
+              const int a = org[(int8_t)(ew & 0xff)];
+              const int b = org[(int8_t)((ew >> 8) & 0xff)];
+              const int c = org[(int8_t)((ew >> 16) & 0xff)];
               // v_lerp_u8 averages bytes, rounding up where its third operand's bit is set:
-              // AVG2 = (a + b + 1) >> 1 in one instruction, AVG3 = (a + 2b + c + 2) >> 2 =
-              // (((a + c) >> 1) + b + 1) >> 1 in two (exact: tests/test_oracle.py::test_avg3_lerp_identity)
+              // AVG3 = (a + 2b + c + 2) >> 2 = (((a + c) >> 1) + b + 1) >> 1 in two instructions
+              // (exact: tests/test_oracle.py::test_avg3_lerp_identity); AVG2(a, b) is stored as
+              // AVG3(a, b, a).  TM words are the negative ones.
               const int avg3 = (int)__builtin_amdgcn_lerp(__builtin_amdgcn_lerp(a, c, 0u), b, 1u);
-              const int avg2 = (int)__builtin_amdgcn_lerp(a, b, 1u);
               const int tm = clamp255(a + b - c);
-              v = (kind & 2) ? tm : (kind & 1) ? avg2 : avg3;
+              v = (int)ew < 0 ? tm : avg3;
             }
             org[ppy * BPS + ppx] = (uint8_t)clamp255(v + rs[j]);
           }

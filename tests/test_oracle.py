@@ -87,6 +87,9 @@ def test_avg3_lerp_identity():
     floor average of a and c, then the rounding-up average with b -- exact for all bytes."""
     a, b, c = np.meshgrid(np.arange(256), np.arange(256), np.arange(256), indexing="ij")
     np.testing.assert_array_equal((((a + c) >> 1) + b + 1) >> 1, (a + 2 * b + c + 2) >> 2)
+    # AVG2 (a + b + 1) >> 1 is stored as AVG3(a, b, a) in pred4_table.inc
+    np.testing.assert_array_equal((a[:, :, 0] + 2 * b[:, :, 0] + a[:, :, 0] + 2) >> 2,
+                                  (a[:, :, 0] + b[:, :, 0] + 1) >> 1)
 
 
 def test_transform_shortcuts_exact():
@@ -254,16 +257,16 @@ def test_pred4_table_matches_oracle_predictors():
                 for x in range(4):
                     w = tab[mode * 16 + y * 4 + x]
                     kind = w >> 24
+                    assert kind in (0x00, 0x80, 0xC0), hex(w)
                     offs = [((w >> (8 * k)) & 0xff) for k in range(3)]
                     offs = [o - 256 if o >= 128 else o for o in offs]
                     a, b, c = (int(flat[org + o]) for o in offs)
-                    if kind == 0:
+                    if kind == 0x00:
                         v = (a + 2 * b + c + 2) >> 2
-                    elif kind == 1:
-                        v = (a + b + 1) >> 1
-                    elif kind == 2:
+                    elif kind == 0x80:
                         v = min(max(a + b - c, 0), 255)
                     else:
+                        assert w == 0xC0000000  # the kernel tests DC by the whole word
                         top = sum(int(flat[org - BPS + k]) for k in range(4))
                         left = sum(int(flat[org + k * BPS - 1]) for k in range(4))
                         v = (top + left + 4) >> 3
