@@ -8,7 +8,7 @@
 namespace wg {
 
 // K1: fused reconstruction + loop filter, one 1024-thread workgroup per frame.
-size_t vp8_recon_lds_bytes(int mb_w, int slot_waves);
+size_t vp8_recon_lds_bytes(int mb_w);
 int vp8_recon_max_mb_w();
 // d_err: device int, OR-ed with 1 if a wave gave up waiting (bounded spin).
 hipError_t launch_vp8_recon_filter(const FrameDesc* d_frames, int n_frames, int max_mb_w, bool lds_frames,

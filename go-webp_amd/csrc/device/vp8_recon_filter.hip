@@ -43,7 +43,6 @@
 // exactly once, when final.  MB records and coefficients are software-pipelined: record
 // x+2 is loaded at the top of MB x's step, the coefficients of x+1 right after x's IDCT.
 #include <hip/hip_runtime.h>
-#include <algorithm>
 #include <type_traits>
 #include <stdint.h>
 #include <stdlib.h>
@@ -62,15 +61,7 @@ constexpr int kRows = 4;       // MB rows per wave (a quad); 16 lanes per MB
 #ifndef WG_K1_MAX_RECON
 #define WG_K1_MAX_RECON 12
 #endif
-constexpr int kMaxRecon = WG_K1_MAX_RECON;  // waves that reconstruct round-robin: LDS slots for 4 x 12 MB rows
-// "Late" waves: up to two more waves, each with its own four MB-row slots, that take the frame's
-// LAST quads (one each) instead of the round-robin waves.  Without them the last quads start
-// only when a round-robin wave finishes its previous quad (c3: quads 32-33 at 76 % of the span),
-// then run alone at the chain's solo pace while the other waves idle; a late wave starts its
-// quad as soon as the chain allows (it spins on the previous quad's progress until then).
-// At most 14 waves with slots: the progress ring's bound (kernel comment at the quad loop).
-constexpr int kMaxLate = 4;
-constexpr int kMaxSlotWaves = 14;
+constexpr int kMaxRecon = WG_K1_MAX_RECON;  // waves that may reconstruct: LDS slots for 4 x 12 MB rows
 constexpr int BPS = 32;        // libwebp workspace stride (vp8/constants.go BPS)
 constexpr int Y_OFF = BPS * 1 + 8;
 constexpr int U_OFF = Y_OFF + BPS * 16 + BPS;
@@ -593,11 +584,9 @@ __device__ __forceinline__ void emit_tail(const FrameDesc& F, uint32_t* progress
 // 4k+g -> 4k+g+1) by the fences of lds_sync, across waves by the release/acquire progress
 // counters -- at workgroup scope the AMDGPU memory model orders global accesses of one CU
 // the same way (its L1 is shared by the workgroup), no extra s_waitcnt needed.
-// slot_waves: waves with LDS slots (the round-robin waves R plus the late waves; the launch sizes
-// the LDS for that many).
 template <bool kGlobalCols>
 __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc* __restrict__ frames, int* err,
-                                                                int lead_arg, int recon_waves_arg, int slot_waves) {
+                                                                int lead_arg, int recon_waves_arg) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   // Progress counters as a typed __shared__ array + relaxed workgroup atomics, so the spin
   // is a ds_read (lgkmcnt) -- a volatile generic pointer became a flat load whose
@@ -634,7 +623,7 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
   using ColPtr = std::conditional_t<kGlobalCols, gptr<uint8_t>, uint8_t*>;
   ColPtr cols;
   if constexpr (kGlobalCols) cols = as_global(F->cols);
-  else cols = lds + kHdrBytes + __mul24(slot_waves, kRows * kSlotBytes);
+  else cols = lds + kHdrBytes + kMaxRecon * kRows * kSlotBytes;
   // per MB column c: cols + c*kColBytes: [0..15] ytop Y, [16..23] U, [24..31] V, [32..159] fbot
   if (threadIdx.x < kWaves) progress[threadIdx.x] = 0;
   if (threadIdx.x == 0) recon_done = next_unit = 0;
@@ -642,30 +631,16 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
   if (emit) __builtin_amdgcn_s_setprio(2);  // reconstruction is the critical path; the tail's conversion yields
   const int nquads = (mb_h + kRows - 1) / kRows;
   // Waves that reconstruct (quads k = wave, wave + R, ...); with the RGBA tail the others
-  // convert bands from the start.  R + late waves <= 14 (the LDS slots) also keeps the progress
-  // ring safe: quad k + 16 can only write slot k & 15 while quad k + 1 still reads it if quads
-  // k + 1 .. k + 16 all run at once (each waits for its predecessor to start, and a quad
-  // completes only after its predecessor's last progress), i.e. on 16 waves.
+  // convert bands from the start.  R <= kMaxRecon (the LDS slots) also keeps the progress
+  // ring safe: quad k + 16 only starts on a wave that has completed a quad > k, so quad k
+  // is complete whenever its slot holds a later quad's value.
   const int R = recon_waves_arg > 0 ? min(recon_waves_arg, kMaxRecon) : kMaxRecon;
-  // late waves R .. R + L - 1 take the last L quads, one each (only when there are more quads than
-  // round-robin waves); the round-robin waves take quads 0 .. nquads - L - 1
-  const int L = min(max(slot_waves - R, 0), max(nquads - R, 0));
-  const int nq_rr = nquads - L;
-  int k_first = nquads, k_end = nquads, k_step = 1;  // (no quads: a converting wave)
-  if (wave < R) {
-    k_first = wave;
-    k_end = nq_rr;
-    k_step = R;
-  } else if (wave < R + L) {
-    k_first = nq_rr + (wave - R);
-    k_end = k_first + 1;
-  }
   for (int t = threadIdx.x; t < 160; t += blockDim.x) tab[t] = kPred4Table[t];
   K1_TIMELINE_START();
   __syncthreads();
 
   bool aborted = false;  // a progress wait timed out (error flagged): stop waiting
-  for (int k = k_first; k < k_end; k += k_step) {
+  for (int k = wave; wave < R && k < nquads; k += R) {
     const int y = kRows * k + g;
     const bool row_ok = y < mb_h;
     const bool has_next = kRows * (k + 1) < mb_h;  // a later quad waits on this one's last row
@@ -1155,12 +1130,10 @@ extern "C" int wg_debug_k1_quads(unsigned long long* out, int n_frames) {
 }
 #endif
 
-size_t vp8_recon_lds_bytes(int mb_w, int slot_waves) {
-  return (size_t)kHdrBytes + (size_t)slot_waves * kRows * kSlotBytes + (size_t)mb_w * kColBytes;
+size_t vp8_recon_lds_bytes(int mb_w) {
+  return (size_t)kHdrBytes + (size_t)kMaxRecon * kRows * kSlotBytes + (size_t)mb_w * kColBytes;
 }
 
-// (the column store's LDS width limit with the round-robin waves' slots alone; the late waves'
-// slots are added only where they fit)
 int vp8_recon_max_mb_w() { return (int)((163840 - kHdrBytes - kMaxRecon * kRows * kSlotBytes) / kColBytes); }
 
 hipError_t launch_vp8_recon_filter(const FrameDesc* d_frames, int n_frames, int max_mb_w, bool lds_frames,
@@ -1176,38 +1149,32 @@ hipError_t launch_vp8_recon_filter(const FrameDesc* d_frames, int n_frames, int 
     const char* e = getenv("WG_K1_RECON_WAVES");
     return e ? atoi(e) : 0;
   }();
-  // WG_K1_LATE_WAVES: late waves (0 .. 4, default 0 until measured; A/B runs)
-  static const int late_waves = [] {
-    const char* e = getenv("WG_K1_LATE_WAVES");
-    return e ? std::min(std::max(atoi(e), 0), kMaxLate) : 0;
-  }();
-  const int R = recon_waves > 0 ? std::min(recon_waves, kMaxRecon) : kMaxRecon;
-  // as many late waves as the LDS holds next to the frames' column store
-  auto slots_for = [&](int mb_w) {
-    int late = std::min(late_waves, kMaxSlotWaves - R);
-    while (late > 0 && vp8_recon_lds_bytes(mb_w, R + late) > 163840) --late;
-    return R + late;
-  };
-  auto launch = [&](auto kernel, int mb_w, size_t& configured) -> hipError_t {
-    const int slot_waves = slots_for(mb_w);
-    const size_t lds = vp8_recon_lds_bytes(mb_w, slot_waves);
+  if (lds_frames) {
+    const size_t lds = vp8_recon_lds_bytes(max_mb_w);
+    static size_t configured = 0;
     if (lds > 65536 && lds > configured) {
-      const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+      const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&vp8_recon_filter_kernel<false>),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       if (e != hipSuccess) return e;
       configured = lds;
     }
-    hipLaunchKernelGGL(kernel, dim3(n_frames), dim3(1024), lds, stream, d_frames, d_err, lead, R, slot_waves);
-    return hipGetLastError();
-  };
-  if (lds_frames) {
-    static size_t configured = 0;
-    const hipError_t e = launch(&vp8_recon_filter_kernel<false>, max_mb_w, configured);
+    hipLaunchKernelGGL(vp8_recon_filter_kernel<false>, dim3(n_frames), dim3(1024), lds, stream, d_frames, d_err,
+                       lead, recon_waves);
+    const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
   if (wide_frames) {
-    static size_t configured = 0;
-    return launch(&vp8_recon_filter_kernel<true>, 0, configured);
+    const size_t lds = vp8_recon_lds_bytes(0);
+    static bool configured = false;
+    if (lds > 65536 && !configured) {
+      const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&vp8_recon_filter_kernel<true>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (e != hipSuccess) return e;
+      configured = true;
+    }
+    hipLaunchKernelGGL(vp8_recon_filter_kernel<true>, dim3(n_frames), dim3(1024), lds, stream, d_frames, d_err,
+                       lead, recon_waves);
+    return hipGetLastError();
   }
   return hipSuccess;
 }
