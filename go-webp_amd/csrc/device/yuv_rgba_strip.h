@@ -23,7 +23,8 @@
 // chroma plane, 1 KB of RGBA): full cache lines, no partial-line write amplification.
 // A group needs chroma columns cb-1 .. cb+2 (cb = x/2); the outer two come from the
 // neighbouring lanes as one packed U/V dword through ds_bpermute, and only the wave's
-// edge lanes load them.  Algorithmic traffic: W*H + 2*ceil(W/2)*ceil(H/2) bytes in,
+// edge lanes load them.  Each chroma row's taps are built once (make_cols) and serve two
+// pairs, as the far row of the first and the near row of the second.  Algorithmic traffic: W*H + 2*ceil(W/2)*ceil(H/2) bytes in,
 // 4*W*H bytes out.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -65,15 +66,20 @@ __device__ __forceinline__ uint32_t sat_x4(u16x2 a) {
   return r;
 }
 
-// VP8YuvToRgba (conversion.go:28-49, A = 0xff) of two pixels; y, u, v hold one 8-bit
-// sample per 16-bit half.  Returns the two RGBA dwords.
-__device__ __forceinline__ uint2 yuv_to_rgba2(u16x2 y, u16x2 u, u16x2 v) {
-  const u16x2 y1 = y * splat(74) + ((y * splat(133)) >> 8);                            // MultHi(y, 19077)
-  const uint32_t r = sat_x4(sat_sub(y1 + v * splat(102) + ((v * splat(37)) >> 8), 14234));  // + MultHi(v, 26149)
-  const u16x2 gu = u * splat(25) + ((u * splat(19)) >> 8);                             // MultHi(u, 6419)
-  const u16x2 gv = v * splat(52) + (v >> 5);                                           // MultHi(v, 13320)
-  const uint32_t g = sat_x4(sat_sub(sat_sub(y1 + splat(8708), gu), gv));
-  const uint32_t b = sat_x4(sat_sub(y1 + u * splat(129) + ((u * splat(26)) >> 8), 17685));  // + MultHi(u, 33050)
+// VP8YuvToRgba (conversion.go:28-49, A = 0xff) of two pixels; yl holds y + 32000 per 16-bit
+// half (luma_lanes), u and v one 8-bit sample each.  Returns the two RGBA dwords.
+//
+// y1g = MultHi(y, 19077) + 8708 -- G's constant, folded into R's and B's subtrahends -- costs
+// no add: two wrapping v_pk_mad_u16 on the biased lane, (133 yl + 4864) mod 2^16 = 133 y + 1024
+// (so t4 = ((133 y) >> 8) + 4) and 74 yl mod 2^16 = 74 y + 8704.  y1g + MultHi(v, 26149) and
+// y1g + MultHi(u, 33050) stay below 2^16 (tests/test_oracle.py::test_packed_yuv_formulas).
+__device__ __forceinline__ uint2 yuv_to_rgba2(u16x2 yl, u16x2 u, u16x2 v) {
+  const u16x2 y1g = yl * splat(74) + ((yl * splat(133) + splat(4864)) >> 8);  // MultHi(y, 19077) + 8708
+  const uint32_t r = sat_x4(sat_sub(y1g + v * splat(102) + ((v * splat(37)) >> 8), 14234 + 8708));  // + MultHi(v, 26149)
+  const u16x2 gu = u * splat(25) + ((u * splat(19)) >> 8);                                 // MultHi(u, 6419)
+  const u16x2 gv = v * splat(52) + (v >> 5);                                               // MultHi(v, 13320)
+  const uint32_t g = sat_x4(sat_sub(sat_sub(y1g, gu), gv));
+  const uint32_t b = sat_x4(sat_sub(y1g + u * splat(129) + ((u * splat(26)) >> 8), 17685 + 8708));  // + MultHi(u, 33050)
   // the channel values are the high bytes of the 16-bit lanes: t = R0 G0 R1 G1; px = R G B 0xff
   // (perm selector 0x0d = 0xff)
   const uint32_t t = __builtin_amdgcn_perm(g, r, 0x07030501u);
@@ -85,6 +91,12 @@ __device__ __forceinline__ u16x2 bytes2(uint32_t w, int i, int j) {
   return as_u16x2(__builtin_amdgcn_perm(0u, w, 0x0c000c00u | (uint32_t)i | ((uint32_t)j << 16)));
 }
 
+// luma bytes i and j of w as yuv_to_rgba2's lanes y + 32000: the high byte 0x7d comes from
+// v_perm's other source (selector 4 = its byte 0), so the bias costs nothing
+__device__ __forceinline__ u16x2 luma_lanes(uint32_t w, int i, int j) {
+  return as_u16x2(__builtin_amdgcn_perm(0x7d7d7d7du, w, 0x04000400u | (uint32_t)i | ((uint32_t)j << 16)));
+}
+
 __device__ __forceinline__ uint32_t bperm(uint32_t v, int src_lane) {
   return (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane << 2, (int)v);
 }
@@ -92,88 +104,117 @@ __device__ __forceinline__ uint32_t bperm(uint32_t v, int src_lane) {
 // One chroma row as loaded by a lane: per group k the packed dword
 // U[cb] | U[cb+1] << 8 | V[cb] << 16 | V[cb+1] << 24 (cb = group's first chroma column,
 // cb+1 already replicated at the right edge), plus the wave-edge bytes: lane 0 holds
-// the column left of its group 0, lane 63 the column right of its group 3 (same packing,
-// U in byte 0, V in byte 2).
+// the column left of its group 0 as U << 8 | V << 24 (the bytes a left neighbour's dword
+// has them in), lane 63 the column right of its group 3 as U | V << 16.
 struct ChromaRaw {
   uint32_t p[kGroups];
   uint32_t edge;
 };
 
-// Per group, the 4 chroma columns cb-1 .. cb+2 with edge replication:
-// u = U[cb-1] | U[cb] << 8 | U[cb+1] << 16 | U[cb+2] << 24, v likewise.
-struct ChromaWin {
-  uint32_t u[kGroups], v[kGroups];
+// One chroma row's taps per group k, the four columns cb-1 .. cb+2 (edge-replicated) of U and
+// V as 16-bit pairs (cb-1, cb+1) and (cb, cb+2): plain, for the row's turn as the NEAR row,
+// and plus 2, for its turn as the FAR row (upsample4's rounding term).  A row is built once,
+// when it is the current row, and carried into the next pair as the previous row.
+struct ChromaCols {
+  u16x2 u02[kGroups], u13[kGroups], v02[kGroups], v13[kGroups];
+  u16x2 u02f[kGroups], u13f[kGroups], v02f[kGroups], v13f[kGroups];
 };
 
-__device__ __forceinline__ ChromaRaw load_chroma(gptr<const uint8_t> ur, gptr<const uint8_t> vr, int cb0, int uv_w,
-                                                 int lane, bool row_ok) {
+// A plane as a buffer resource (readfirstlane'd base: the planes are per frame, uniform, but
+// where the compiler cannot prove it a VGPR descriptor would wrap every access in a
+// readfirstlane waterfall loop).  Loads past num_records read 0: rows outside the frame are
+// loaded at kOffDrop instead of being branched around, and no load needs 64-bit addresses.
+constexpr uint32_t kOffDrop = 0x80000000u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const void* base, int bytes) {
+  const uint64_t b = reinterpret_cast<uint64_t>(base);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)b);
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0,
+                                           __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
+// Chroma row `row` (row_ok false: zeros) for the lane's groups: one 16-bit load per plane and
+// group at voffset cb0 + row * uvs + 128 k.  Columns at or past uv_w hold other bytes (never
+// used: make_cols replicates the edge, and pixels past the width are not stored), except the
+// replicated U[cb+1] of an odd width's last group.
+__device__ __forceinline__ ChromaRaw load_chroma(__amdgpu_buffer_rsrc_t ud, __amdgpu_buffer_rsrc_t vd,
+                                                 gptr<const uint8_t> U, gptr<const uint8_t> V, int row, int uvs,
+                                                 int cb0, int uv_w, int lane, bool row_ok) {
   ChromaRaw r;
+  const uint32_t off = row_ok ? (uint32_t)(cb0 + row * uvs) : kOffDrop;
 #pragma unroll
   for (int k = 0; k < kGroups; ++k) {
     const int cb = cb0 + 128 * k;
-    uint32_t u = 0, v = 0;
-    if (row_ok && cb < uv_w) {
-      u = *reinterpret_cast<gptr<const uint16_t>>(ur + cb);
-      v = *reinterpret_cast<gptr<const uint16_t>>(vr + cb);
-      if (cb + 1 >= uv_w) {  // odd width: column cb+1 replicates cb
-        u = (u & 0xff) * 0x101u;
-        v = (v & 0xff) * 0x101u;
-      }
+    uint32_t u = __builtin_amdgcn_raw_buffer_load_b16(ud, off + 128 * k, 0, 0);
+    uint32_t v = __builtin_amdgcn_raw_buffer_load_b16(vd, off + 128 * k, 0, 0);
+    if (cb + 1 == uv_w) {  // odd width: column cb+1 replicates cb
+      u = (u & 0xff) * 0x101u;
+      v = (v & 0xff) * 0x101u;
     }
     r.p[k] = u | (v << 16);
   }
   r.edge = 0;
   if (row_ok) {
     const int ce = lane == 0 ? cb0 - 1 : cb0 + 128 * (kGroups - 1) + 2;
-    if ((lane == 0 && ce >= 0) || (lane == 63 && ce < uv_w)) r.edge = ur[ce] | ((uint32_t)vr[ce] << 16);
+    if ((lane == 0 && ce >= 0) || (lane == 63 && ce < uv_w)) {
+      const size_t o = (size_t)row * uvs + ce;
+      r.edge = (U[o] | ((uint32_t)V[o] << 16)) << (lane == 0 ? 8 : 0);
+    }
   }
   return r;
 }
 
-__device__ __forceinline__ ChromaWin make_win(const ChromaRaw& r, int cb0, int uv_w, int lane) {
-  ChromaWin w;
+// The taps straight from the packed dwords by v_perm: s = this group's dword, L = the left
+// neighbour's (U[cb-1] in byte 1, V[cb-1] in byte 3), R = the right neighbour's (U[cb+2] in
+// byte 0, V[cb+2] in byte 2) -- neighbour lanes through ds_bpermute, lane 63 / lane 0
+// forwarding the adjacent group's dword so the rotation across the wave boundary lands on
+// the right column; the frame's edges replicate s's own columns.
+__device__ __forceinline__ ChromaCols make_cols(const ChromaRaw& r, int cb0, int uv_w, int lane) {
+  ChromaCols c;
   const int from_l = (lane + 63) & 63, from_r = (lane + 1) & 63;
 #pragma unroll
   for (int k = 0; k < kGroups; ++k) {
     const int cb = cb0 + 128 * k;
-    // neighbour lanes' packed dwords; lane 63 / lane 0 forward the adjacent group's so the
-    // rotation across the wave boundary lands on the right column.
-    uint32_t lp = bperm(lane == 63 && k > 0 ? r.p[k - 1] : r.p[k], from_l) >> 8;  // U[cb-1] b0, V[cb-1] b2
-    uint32_t rp = bperm(lane == 0 && k + 1 < kGroups ? r.p[k + 1] : r.p[k], from_r);  // U[cb+2] b0, V b2
-    if (lane == 0 && k == 0) lp = r.edge;
-    if (lane == 63 && k == kGroups - 1) rp = r.edge;
     const uint32_t s = r.p[k];
-    uint32_t ul = lp & 0xff, vl = (lp >> 16) & 0xff;
-    uint32_t ur = rp & 0xff, vr = (rp >> 16) & 0xff;
-    if (cb == 0) {
-      ul = s & 0xff;
-      vl = (s >> 16) & 0xff;
-    }
-    if (cb + 2 >= uv_w) {
-      ur = (s >> 8) & 0xff;
-      vr = s >> 24;
-    }
-    w.u[k] = ul | ((s & 0xffff) << 8) | (ur << 24);
-    w.v[k] = vl | ((s >> 16) << 8) | (vr << 24);
+    uint32_t L = bperm(lane == 63 && k > 0 ? r.p[k - 1] : s, from_l);
+    uint32_t R = bperm(lane == 0 && k + 1 < kGroups ? r.p[k + 1] : s, from_r);
+    if (k == 0 && lane == 0) L = cb0 == 0 ? s << 8 : r.edge;  // (cb == 0: U[cb-1] := U[cb])
+    if (k == kGroups - 1 && lane == 63) R = r.edge;
+    if (cb + 2 >= uv_w) R = s >> 8;  // U[cb+2] := U[cb+1]
+    c.u02[k] = as_u16x2(__builtin_amdgcn_perm(s, L, 0x0c050c01u));  // U[cb-1], U[cb+1]
+    c.u13[k] = as_u16x2(__builtin_amdgcn_perm(R, s, 0x0c040c00u));  // U[cb],   U[cb+2]
+    c.v02[k] = as_u16x2(__builtin_amdgcn_perm(s, L, 0x0c070c03u));  // V[cb-1], V[cb+1]
+    c.v13[k] = as_u16x2(__builtin_amdgcn_perm(R, s, 0x0c060c02u));  // V[cb],   V[cb+2]
+    c.u02f[k] = c.u02[k] + splat(2);
+    c.u13f[k] = c.u13[k] + splat(2);
+    c.v02f[k] = c.v02[k] + splat(2);
+    c.v13f[k] = c.v13[k] + splat(2);
   }
-  return w;
+  return c;
 }
 
-// 4 pixels of group k: near/far chroma windows (n, f), luma dword.  Per chroma plane the
-// vertical blend a[j] = 3*n[j] + f[j] is computed as two packed pairs (a0, a2), (a1, a3);
-// pixel 2c takes (3*a[near] + a[far] + 8) >> 4 with far = c-1, pixel 2c+1 far = c+1.
-__device__ __forceinline__ void upsample4(uint32_t n, uint32_t f, u16x2& p01, u16x2& p23) {
-  const u16x2 a02 = as_u16x2(n & 0x00ff00ffu) * splat(3) + as_u16x2(f & 0x00ff00ffu);
-  const u16x2 a13 = bytes2(n, 1, 3) * splat(3) + bytes2(f, 1, 3);
-  p01 = (a13.xx * splat(3) + (a02 + splat(8))) >> 4;  // (3a1 + a0 + 8, 3a1 + a2 + 8) >> 4
-  p23 = (a02.yy * splat(3) + (a13 + splat(8))) >> 4;  // (3a2 + a1 + 8, 3a2 + a3 + 8) >> 4
+// 4 pixels of one plane from the near row's taps (n02, n13) and the far row's plus 2 (f02, f13):
+// the vertical blend a[j] = 3*n[j] + f[j] + 2 as two packed pairs (a0, a2), (a1, a3); pixel 2c
+// takes (3*a[near] + a[far]) >> 4 with far = c-1, pixel 2c+1 far = c+1 -- the 2s make its
+// rounding 8.
+// (The horizontal taps as one v_pk_mad_u16 each, the broadcast half by op_sel: written as vector
+// code the compiler splits them into a multiply and an add.)
+__device__ __forceinline__ void upsample4(u16x2 n02, u16x2 n13, u16x2 f02, u16x2 f13, u16x2& p01, u16x2& p23) {
+  const u16x2 a02 = n02 * splat(3) + f02;
+  const u16x2 a13 = n13 * splat(3) + f13;
+  uint32_t h01, h23;
+  asm("v_pk_mad_u16 %0, %1, 3, %2 op_sel_hi:[0,0,1]" : "=v"(h01) : "v"(as_u32(a13)), "v"(as_u32(a02)));  // a1 * 3 + (a0, a2)
+  asm("v_pk_mad_u16 %0, %1, 3, %2 op_sel:[1,0,0] op_sel_hi:[1,0,1]" : "=v"(h23) : "v"(as_u32(a02)), "v"(as_u32(a13)));  // a2 * 3 + (a1, a3)
+  p01 = as_u16x2(h01) >> 4;  // (3a1 + a0 + 8, 3a1 + a2 + 8) >> 4
+  p23 = as_u16x2(h23) >> 4;  // (3a2 + a1 + 8, 3a2 + a3 + 8) >> 4
 }
 
-__device__ __forceinline__ u32x4 convert_group(uint32_t nu, uint32_t fu, uint32_t nv, uint32_t fv, uint32_t yw) {
+// group k of a row: n = the near row's taps, f = the far row's
+__device__ __forceinline__ u32x4 convert_group(const ChromaCols& n, const ChromaCols& f, int k, uint32_t yw) {
   u16x2 u01, u23, v01, v23;
-  upsample4(nu, fu, u01, u23);
-  upsample4(nv, fv, v01, v23);
-  const uint2 a = yuv_to_rgba2(bytes2(yw, 0, 1), u01, v01), b = yuv_to_rgba2(bytes2(yw, 2, 3), u23, v23);
+  upsample4(n.u02[k], n.u13[k], f.u02f[k], f.u13f[k], u01, u23);
+  upsample4(n.v02[k], n.v13[k], f.v02f[k], f.v13f[k], v01, v23);
+  const uint2 a = yuv_to_rgba2(luma_lanes(yw, 0, 1), u01, v01), b = yuv_to_rgba2(luma_lanes(yw, 2, 3), u23, v23);
   return u32x4{a.x, a.y, b.x, b.y};
 }
 
@@ -184,14 +225,14 @@ __device__ __forceinline__ u32x4 convert_group(uint32_t nu, uint32_t fu, uint32_
 // with the reconstruction's working set; c3 K1 7.71 vs 7.77 ms, same call).
 constexpr int kAuxNt = 2, kAuxSc1 = 16;
 template <int kAux>
-__device__ __forceinline__ void store_group(__amdgpu_buffer_rsrc_t o, uint32_t off, u32x4 px, int nvalid, bool aligned) {
-  if (aligned && nvalid >= 4) {
+__device__ __forceinline__ void store_group(__amdgpu_buffer_rsrc_t o, uint32_t off, u32x4 px, int nvalid, bool full) {
+  if (full) {  // (wave-uniform: every lane's group is whole and the rows 16-byte aligned)
     __builtin_amdgcn_raw_buffer_store_b128(px, o, off, 0, kAux);
-  } else {
-    if (nvalid > 0) __builtin_amdgcn_raw_buffer_store_b32(px.x, o, off, 0, 0);
-    if (nvalid > 1) __builtin_amdgcn_raw_buffer_store_b32(px.y, o, off + 4, 0, 0);
-    if (nvalid > 2) __builtin_amdgcn_raw_buffer_store_b32(px.z, o, off + 8, 0, 0);
-    if (nvalid > 3) __builtin_amdgcn_raw_buffer_store_b32(px.w, o, off + 12, 0, 0);
+  } else {  // dword stores, those past the width dropped through the buffer range
+    __builtin_amdgcn_raw_buffer_store_b32(px.x, o, nvalid > 0 ? off : kOffDrop, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(px.y, o, nvalid > 1 ? off + 4 : kOffDrop, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(px.z, o, nvalid > 2 ? off + 8 : kOffDrop, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(px.w, o, nvalid > 3 ? off + 12 : kOffDrop, 0, 0);
   }
 }
 
@@ -211,7 +252,11 @@ __device__ __forceinline__ void convert_strip(const FrameDesc& F, int tx, int ba
   const int xl = tx * kStripPx + 4 * lane;  // group k pixel x = xl + 256k
   const int cb0 = xl >> 1;
   const bool aligned = ((F.rgba_stride & 15) == 0) && ((reinterpret_cast<uintptr_t>(F.rgba) & 15) == 0);
-  const gptr<const uint8_t> Y = as_global(static_cast<const uint8_t*>(F.y));
+  // per group k, from the wave's first pixel x0 (scalar): some lane's group lies in the frame
+  // (else skipped), every lane's group is whole (one 16-byte store each)
+  const int x0 = tx * kStripPx;
+  auto live = [&](int k) { return x0 + 256 * k < W; };
+  auto full = [&](int k) { return aligned && x0 + 256 * k + 256 <= W; };
   const gptr<const uint8_t> U = as_global(static_cast<const uint8_t*>(F.u));
   const gptr<const uint8_t> V = as_global(static_cast<const uint8_t*>(F.v));
   const int ys = F.y_stride, uvs = F.uv_stride, os = F.rgba_stride;
@@ -225,12 +270,13 @@ __device__ __forceinline__ void convert_strip(const FrameDesc& F, int tx, int ba
   const __amdgpu_buffer_rsrc_t out =
       __builtin_amdgcn_make_buffer_rsrc(obase, 0, __builtin_amdgcn_readfirstlane(os * H), 0x00020000);
 
+  const __amdgpu_buffer_rsrc_t yd = plane_rsrc(F.y, ys * H), ud = plane_rsrc(F.u, uvs * uv_h),
+                               vd = plane_rsrc(F.v, uvs * uv_h);
+  // (a group's bytes past the width are loaded but never stored)
   auto load_luma = [&](int row, uint32_t yw[kGroups]) {
+    const uint32_t off = row >= 0 && row < H ? (uint32_t)(xl + row * ys) : kOffDrop;
 #pragma unroll
-    for (int k = 0; k < kGroups; ++k) {
-      const int x = xl + 256 * k;
-      yw[k] = (row >= 0 && row < H && x < W) ? *reinterpret_cast<gptr<const uint32_t>>(Y + (size_t)row * ys + x) : 0u;
-    }
+    for (int k = 0; k < kGroups; ++k) yw[k] = __builtin_amdgcn_raw_buffer_load_b32(yd, off + 256 * k, 0, 0);
   };
 
   if (kFancy) {
@@ -239,32 +285,36 @@ __device__ __forceinline__ void convert_strip(const FrameDesc& F, int tx, int ba
     if (p0 >= npairs) return;
     const int p1 = min(p0 + kPairs, npairs);
     const int rp = max(p0 - 1, 0), rc = min(p0, uv_h - 1);
-    const ChromaRaw raw_prev = load_chroma(U + (size_t)rp * uvs, V + (size_t)rp * uvs, cb0, uv_w, lane, true);
-    ChromaRaw raw_cur = load_chroma(U + (size_t)rc * uvs, V + (size_t)rc * uvs, cb0, uv_w, lane, true);
-    ChromaWin wp = make_win(raw_prev, cb0, uv_w, lane);
-    for (int p = p0; p < p1; ++p) {
+    const ChromaRaw raw_prev = load_chroma(ud, vd, U, V, rp, uvs, cb0, uv_w, lane, true);
+    ChromaRaw raw_cur = load_chroma(ud, vd, U, V, rc, uvs, cb0, uv_w, lane, true);
+    ChromaCols ca = make_cols(raw_prev, cb0, uv_w, lane);
+    // one pair: rows 2p-1 (near = chroma row p-1, far = row p) and 2p (near = row p, far = row
+    // p-1); returns row p's taps for the next pair.  (Unrolled by two, so the carried taps would
+    // alternate between register sets instead of being copied, the loop measured no faster and
+    // its code grew K1 by 8 KB: not kept.)
+    auto pair_step = [&](int p, const ChromaCols& prv) __attribute__((always_inline)) {
       const int ya = 2 * p - 1, yb = 2 * p;
       uint32_t yA[kGroups], yB[kGroups];
       load_luma(ya, yA);
       load_luma(yb, yB);
       const int rn = min(p + 1, uv_h - 1);  // chroma row for the next pair
-      const ChromaRaw raw_next = load_chroma(U + (size_t)rn * uvs, V + (size_t)rn * uvs, cb0, uv_w, lane, p + 1 < p1);
-      const ChromaWin wc = make_win(raw_cur, cb0, uv_w, lane);
+      const ChromaRaw raw_next = load_chroma(ud, vd, U, V, rn, uvs, cb0, uv_w, lane, p + 1 < p1);
+      const ChromaCols cur = make_cols(raw_cur, cb0, uv_w, lane);
 #pragma unroll
       for (int k = 0; k < kGroups; ++k) {
         const int x = xl + 256 * k;
-        const int nvalid = W - x;
-        if (nvalid <= 0) continue;
-        if (ya >= 0)  // near = chroma row p-1, far = row p
-          store_group<kAux>(out, (uint32_t)(ya * os + 4 * x), convert_group(wp.u[k], wc.u[k], wp.v[k], wc.v[k], yA[k]), nvalid,
-                      aligned);
-        if (yb < H)  // near = chroma row p, far = row p-1
-          store_group<kAux>(out, (uint32_t)(yb * os + 4 * x), convert_group(wc.u[k], wp.u[k], wc.v[k], wp.v[k], yB[k]), nvalid,
-                      aligned);
+        if (!live(k)) continue;
+        if (ya >= 0) store_group<kAux>(out, (uint32_t)(ya * os + 4 * x), convert_group(prv, cur, k, yA[k]), W - x, full(k));
+        if (yb < H) store_group<kAux>(out, (uint32_t)(yb * os + 4 * x), convert_group(cur, prv, k, yB[k]), W - x, full(k));
       }
-      wp = wc;
       raw_cur = raw_next;
-    }
+      // K1's tail yields the SIMD for a moment after each pair: its denser packed code otherwise
+      // takes issue slots from the reconstructing waves, the frame's critical path (same-call
+      // A/B, no sleep / sleep 4 / 16: c3 7.59 / 7.58 / 7.62 ms, c3s 8.24 / 8.22 / 8.19 ms)
+      if (kAux == kAuxSc1) __builtin_amdgcn_s_sleep(4);
+      return cur;
+    };
+    for (int p = p0; p < p1; ++p) ca = pair_step(p, ca);
   } else {
     // point sampling: rows 2p and 2p+1 both use chroma row p (WebPSamplerProcessPlane)
     const int npairs = (H + 1) >> 1;
@@ -275,12 +325,11 @@ __device__ __forceinline__ void convert_strip(const FrameDesc& F, int tx, int ba
       uint32_t yA[kGroups], yB[kGroups];
       load_luma(2 * p, yA);
       load_luma(2 * p + 1, yB);
-      const ChromaRaw c = load_chroma(U + (size_t)p * uvs, V + (size_t)p * uvs, cb0, uv_w, lane, true);
+      const ChromaRaw c = load_chroma(ud, vd, U, V, p, uvs, cb0, uv_w, lane, true);
 #pragma unroll
       for (int k = 0; k < kGroups; ++k) {
         const int x = xl + 256 * k;
-        const int nvalid = W - x;
-        if (nvalid <= 0) continue;
+        if (!live(k)) continue;
         // pixels 0,1 take chroma column cb, pixels 2,3 column cb+1
         const uint32_t cp = c.p[k];
         const u16x2 u0 = bytes2(cp, 0, 0), u1 = bytes2(cp, 1, 1), v0 = bytes2(cp, 2, 2), v1 = bytes2(cp, 3, 3);
@@ -289,9 +338,9 @@ __device__ __forceinline__ void convert_strip(const FrameDesc& F, int tx, int ba
           const int yr = 2 * p + r;
           if (yr >= H) break;
           const uint32_t yw = r ? yB[k] : yA[k];
-          const uint2 a = yuv_to_rgba2(bytes2(yw, 0, 1), u0, v0), b = yuv_to_rgba2(bytes2(yw, 2, 3), u1, v1);
+          const uint2 a = yuv_to_rgba2(luma_lanes(yw, 0, 1), u0, v0), b = yuv_to_rgba2(luma_lanes(yw, 2, 3), u1, v1);
           const u32x4 px{a.x, a.y, b.x, b.y};
-          store_group<kAux>(out, (uint32_t)(yr * os + 4 * x), px, nvalid, aligned);
+          store_group<kAux>(out, (uint32_t)(yr * os + 4 * x), px, W - x, full(k));
         }
       }
     }

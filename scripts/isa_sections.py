@@ -40,6 +40,30 @@ def valu_units(op):
     return 1.0 if FULL_RATE.match(op) else 2.0
 
 
+def enc_bytes(op, line):
+    """Encoded size of one instruction (GCN/CDNA formats): SOP*/VOP1/VOP2/VOPC 4 bytes, VOP3(P),
+    SDWA, DPP, SMEM, DS and memory 8, plus 4 for a literal constant (a hex operand outside the
+    inline range).  For code-size (instruction-cache footprint) comparisons."""
+    if op.startswith("s_"):
+        n = 8 if op.startswith(("s_load", "s_buffer", "s_store", "s_memtime", "s_memrealtime", "s_dcache",
+                                "s_atomic")) else 4
+    elif op.startswith("v_"):
+        n = 4 if op.endswith("_e32") or (op.startswith(("v_mov_b32", "v_readfirstlane")) and "_e64" not in op) else 8
+        if op.endswith(("_sdwa", "_dpp")) or op.startswith("v_pk_"):
+            n = 8
+    else:
+        n = 8
+    for m in re.findall(r"(?<![\w:])(-?0x[0-9a-fA-F]+|-?\d+)(?![\w.\]])", line.split(";")[0][len(op) + 1:]):
+        try:
+            v = int(m, 0)
+        except ValueError:
+            continue
+        if not -16 <= v <= 64:
+            n += 4
+            break
+    return n
+
+
 def main():
     src = sys.argv[1] if len(sys.argv) > 1 else SRC
     d = os.path.dirname(os.path.abspath(src))
@@ -77,15 +101,17 @@ def main():
             cls = ("valu" if op.startswith("v_") else "salu" if op.startswith("s_") else "lds" if op.startswith("ds_")
                    else "vmem" if op.startswith(("global_", "buffer_", "flat_")) else "other")
             cnt.setdefault(cur, collections.Counter())[cls] += 1
+            cnt[cur]["bytes"] += enc_bytes(op, line)
             if cls == "valu":
                 cnt[cur]["units"] += valu_units(op)
                 if op.startswith(("v_readlane", "v_writelane")):
                     cnt[cur]["spill"] += 1  # SGPR spills through VGPR lanes
     tot = collections.Counter()
     for k, v in cnt.items():
-        print(f"{k:10s} " + " ".join(f"{c}={v[c]:g}" for c in ("valu", "units", "salu", "lds", "vmem", "spill")))
+        print(f"{k:10s} " + " ".join(f"{c}={v[c]:g}" for c in ("valu", "units", "salu", "lds", "vmem", "spill", "bytes")))
         tot += v
-    print("total      " + " ".join(f"{c}={tot[c]:g}" for c in ("valu", "units", "salu", "lds", "vmem", "spill")), meta)
+    print("total      " + " ".join(f"{c}={tot[c]:g}" for c in ("valu", "units", "salu", "lds", "vmem", "spill", "bytes")),
+          meta)
 
 
 if __name__ == "__main__":

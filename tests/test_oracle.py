@@ -159,9 +159,9 @@ def test_upsampler_closed_form():
 
 
 def test_packed_yuv_formulas():
-    """K2's packed 16-bit VP8YuvToRgba (yuv_to_rgba.hip::yuv_to_rgba2) == conversion.go:28-49
+    """K2's packed 16-bit VP8YuvToRgba (yuv_rgba_strip.h::yuv_to_rgba2) == conversion.go:28-49
     for every (y, u, v): MultHi split at the multiplier's high byte, saturating subtract
-    before the >> 6, every intermediate within 16 bits unsigned.  And the packed vertical
+    before the >> 6, every intermediate within 16 bits unsigned (or wrapping by design).  And the packed vertical
     blend + horizontal taps (upsample4) stay within 16 bits."""
     y, u, v = (a.ravel().astype(np.int64) for a in np.meshgrid(*(np.arange(256),) * 3, indexing="ij"))
 
@@ -180,17 +180,29 @@ def test_packed_yuv_formulas():
 
     def sat(a, b):
         return np.maximum(a - b, 0)
-    y1 = u16(74 * y + (u16(133 * y) >> 8))
-    r = np.minimum(sat(u16(y1 + u16(102 * v + (u16(37 * v) >> 8))), 14234) >> 6, 255)
+    # y1g = MultHi(y, 19077) + 8708 (G's constant, folded into R's and B's subtrahends), from the
+    # luma lane y + 32000 (high byte 0x7d from v_perm's constant source) by two wrapping
+    # v_pk_mad_u16: (133 yl + 4864) mod 2^16 = 133 y + 1024, and 74 yl mod 2^16 = 74 y + 8704
+    yl = y + 32000
+    t4 = ((133 * yl + 4864) % 65536) >> 8
+    assert ((133 * yl + 4864) % 65536 == 133 * y + 1024).all()
+    y1g = u16((74 * yl + t4) % 65536)
+    np.testing.assert_array_equal(y1g, mh(y, 19077) + 8708)
+    r = np.minimum(sat(u16(y1g + u16(102 * v + (u16(37 * v) >> 8))), 14234 + 8708) >> 6, 255)
     gu = u16(25 * u + (u16(19 * u) >> 8))
     gv = u16(52 * v + (v >> 5))
-    g = np.minimum(sat(sat(u16(y1 + 8708), gu), gv) >> 6, 255)
-    b = np.minimum(sat(u16(y1 + u16(129 * u + (u16(26 * u) >> 8))), 17685) >> 6, 255)
+    g = np.minimum(sat(sat(y1g, gu), gv) >> 6, 255)
+    b = np.minimum(sat(u16(y1g + u16(129 * u + (u16(26 * u) >> 8))), 17685 + 8708) >> 6, 255)
     np.testing.assert_array_equal(r, R)
     np.testing.assert_array_equal(g, G)
     np.testing.assert_array_equal(b, B)
-    a = 3 * 255 + 255
-    assert 3 * a + a + 8 < 65536
+    # upsample4: a = 3 * near + (far + 2) per chroma column, then (3 a[near col] + a[far col]) >> 4
+    # = (9a + 3b + 3c + d + 8) >> 4 (the rounding 8 = 3 * 2 + 2); every value within 16 bits
+    n, f, n2, f2 = (np.random.default_rng(9).integers(0, 256, 1 << 16) for _ in range(4))
+    a_near, a_far = 3 * n + (f + 2), 3 * n2 + (f2 + 2)
+    np.testing.assert_array_equal((3 * a_near + a_far) >> 4, (9 * n + 3 * f + 3 * n2 + f2 + 8) >> 4)
+    a = 3 * 255 + 255 + 2
+    assert 3 * a + a < 65536
     # the final `>> 6` + Clip8 as the high byte of a saturating x4 (v_pk_mad_u16 ... clamp)
     x = np.arange(65536)
     np.testing.assert_array_equal(np.minimum(4 * x, 65535) >> 8, np.minimum(x >> 6, 255))
