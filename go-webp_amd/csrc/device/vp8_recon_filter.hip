@@ -826,8 +826,13 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
           const int b0 = (m + 16 * s) >> 2, lbx = b0 & 3, lby = b0 >> 2;
           const int row_a = 4 * lby + q, row_b = row_a + 8;
           const uint32_t top = ld32(ws + Y_OFF - BPS + 4 * lbx);
-          st32(ws + Y_OFF + row_a * BPS + 4 * lbx, add_res(pred_row(oh, top, left[row_a], tl, dc), ry0[s]));
-          st32(ws + Y_OFF + row_b * BPS + 4 * lbx, add_res(pred_row(oh, top, left[row_b], tl, dc), ry1[s]));
+          const uint32_t va = add_res(pred_row(oh, top, left[row_a], tl, dc), ry0[s]);
+          const uint32_t vb = add_res(pred_row(oh, top, left[row_b], tl, dc), ry1[s]);
+          st32(ws + Y_OFF + row_a * BPS + 4 * lbx, va);
+          st32(ws + Y_OFF + row_b * BPS + 4 * lbx, vb);
+          // (and straight into the filter window: no copy section)
+          st32(fw + kFwY + (row_a + 4) * FWY + 4 + 4 * lbx, va);
+          st32(fw + kFwY + (row_b + 4) * FWY + 4 + 4 * lbx, vb);
         }
       }
       if (act && i4) {  // stage residuals for the pixel-per-lane block walk
@@ -862,7 +867,9 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
           }
           const uint32_t pred =
               pred_row(oh, ld32(base - BPS + 4 * cbx), cleft[row], base[-BPS - 1], dc_value(oh, st, sl, 3));
-          st32(ws + coff + row * BPS + 4 * cbx, add_res(pred, rcr[s]));
+          const uint32_t v = add_res(pred, rcr[s]);
+          st32(ws + coff + row * BPS + 4 * cbx, v);
+          st32(fw + (s ? kFwV : kFwU) + (row + 4) * FWC + 4 + 4 * cbx, v);
         }
       }
 #endif
@@ -908,7 +915,9 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
               const int tm = clamp255(a + b - c);
               v = (int)ew < 0 ? tm : avg3;
             }
-            org[ppy * BPS + ppx] = (uint8_t)clamp255(v + rs[j]);
+            const uint8_t px = (uint8_t)clamp255(v + rs[j]);
+            org[ppy * BPS + ppx] = px;
+            fw[kFwY + (4 * by + ppy + 4) * FWY + 4 + 4 * bx + ppx] = px;  // (the filter window too)
           }
           if (j == 15 || kI4Step[j + 1] != kI4Step[j]) lds_sync();
         }
@@ -925,16 +934,8 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
           const int so = m < 4 ? Y_OFF + 15 * BPS + 4 * m : (m < 6 ? U_OFF - 16 : V_OFF - 24) + 7 * BPS + 4 * m;
           st32(col + 4 * m, ld32(ws + so));
         }
-        // ---- filter window: MB body from the workspace, rows above from fbot
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          const int l = m + 16 * s, b0 = l >> 2;
-          st32(fw + kFwY + (b0 + 4) * FWY + 4 + 4 * q, ld32(ws + Y_OFF + b0 * BPS + 4 * q));
-          st32(fw + kFwY + (b0 + 12) * FWY + 4 + 4 * q, ld32(ws + Y_OFF + (b0 + 8) * BPS + 4 * q));
-          const int rr = (l >> 1) & 7, dd = l & 1;
-          st32(fw + (s ? kFwV : kFwU) + (rr + 4) * FWC + 4 + 4 * dd,
-               ld32(ws + (s ? V_OFF : U_OFF) + rr * BPS + 4 * dd));
-        }
+        // ---- filter window: rows above from fbot (the MB body was written into it by the
+        //      prediction sections, next to the workspace)
         if (y > 0) {
           st32(fw + kFwY + (m >> 2) * FWY + 4 + 4 * (m & 3), ld32(col + 32 + 4 * m));
           const int p = m >> 3, rr = (m >> 1) & 3, dd = m & 1;
