@@ -388,7 +388,11 @@ __device__ __forceinline__ void filter_line(Line& l, int t2, int it, int hev_t) 
   } else {
     if (on) {
       asm volatile("");
-      const int a = __mul24(d0, 3) + (hv ? sp : 0);
+      int a = __mul24(d0, 3);
+      if (hv) {  // (the hev term added under the lane mask: no select)
+        asm volatile("");
+        a += sp;
+      }
       const int a1 = sclip2((a + 4) >> 3), a2 = sclip2((a + 3) >> 3), a3 = (a1 + 1) >> 1;
       l.p0 = clamp255(l.p0 + a2);
       l.q0 = clamp255(l.q0 - a1);

@@ -607,17 +607,13 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
       __syncthreads();  // every lookup has read the slot table; the masks are complete
       const bool go_serial = slow[b & 1] != 0;
       // ---- 3. each key's last updater writes its slot and clears the key's masks
+      // the window's updaters packed 64 to a wave by rank (uval is complete after the barrier):
+      // C5's ~143 per block take three waves' single pass instead of a sparse pass in each of
+      // sixteen.  A pending copy that never resolved (the window goes serial) never registered,
+      // so its rank is no key's last: its stale uval entry changes nothing.
       if (in_win && nkeys) {
-        if (!wave_pc) {
-          for (int i = lane; i < my_wc; i += 64) {
-            const int r = woff - rb + i;
-            table_update(r, uval[r], go_serial);
-          }
-        } else {
-#pragma unroll
-          for (int j = 0; j < kPer; ++j)
-            if (is_upd(ps, j) && pk(ps, j) == kPK) table_update(R(j) - rb, v[j], go_serial);
-        }
+        const int wtot = prefix(q * wpw + wpw) - rb, wi = wave - q * wpw;
+        for (int i = wi * 64 + lane; i < wtot; i += wpw * 64) table_update(i, uval[i], go_serial);
       }
       if (tid == 0) first_pend[0] = first_pend[1] = kBlock;
       if (go_serial) {
