@@ -19,5 +19,5 @@ if [ -z "$SKIP_TESTS" ]; then
 fi
 step bench_c3 400 python bench.py --steps 10 --warmup 3
 step bench_c3s 400 python bench.py --workload c3s --steps 10 --warmup 3
-grep -h '^{' $OUT/bench_c3.log > $OUT/bench_c3.json
-grep -h '^{' $OUT/bench_c3s.log > $OUT/bench_c3s.json
+step bench_c5 400 python bench.py --workload c5 --steps 10 --warmup 3
+for w in c3 c3s c5; do grep -h '^{' $OUT/bench_$w.log > $OUT/bench_$w.json; done
