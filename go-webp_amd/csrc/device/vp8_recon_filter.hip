@@ -682,6 +682,7 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
 
     K1_SECT_START();
     K1_QUAD_MARK(k, 0);
+    uint32_t seen = 0;  // progress of quad k - 1 last read (wave-uniform)
 
     for (int i = 0; i < mb_w + 2 * (kRows - 1); ++i) {
       // Lane roles, recomputed every iteration from an opaque lane id: hoisted out of the
@@ -717,11 +718,14 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
         auto cur = [&] {
           return __builtin_amdgcn_readfirstlane(__hip_atomic_load(pr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
         };
-        if (!aborted && cur() < need) {
+        // (the last value read, kept in an SGPR: while the previous quad is further ahead than this
+        // step needs, no LDS read and no wait for it -- the acquire that returned it already
+        // ordered the data of every column it covers)
+        if (!aborted && seen < need && (seen = cur()) < need) {
           const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
           for (;;) {
             __builtin_amdgcn_s_sleep(4);
-            if (cur() >= need) break;
+            if ((seen = cur()) >= need) break;
             if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s: give up, flag
               // no exit from the loop here (an exit path skipping the stores would reach the
               // latch too): the wave runs on without waiting and the batch reports the error
