@@ -89,17 +89,18 @@ __device__ __forceinline__ int count_below(uint64_t m) {
 // 7 end of block
 __device__ unsigned long long g_k7_stats[16];
 __device__ unsigned long long g_k7_wave[kWaves][16];  // per wave (lane 0): the same phase cycles
+// The accumulators live in LDS (k7_lds[wave][i], counts in wave 0's row) and the clock in a
+// scalar pair: per-lane register accumulators spilled 29 VGPRs in the 128-VGPR kernel, and the
+// scratch traffic skewed the phase split (the timing build ran 65 % slower than the product).
 #define K7_T(i)                                                      \
   do {                                                               \
-    if ((tid & 63) == 0) {                                           \
-      const uint64_t t_ = __builtin_amdgcn_s_memtime();              \
-      k7_acc[i] += t_ - k7_t;                                        \
-      k7_t = t_;                                                     \
-    }                                                                \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime();                \
+    if (lane == 0) atomicAdd(&k7_lds[wave][i], (unsigned long long)(t_ - k7_t)); \
+    k7_t = t_;                                                       \
   } while (0)
 #define K7_COUNT(i, v)                                               \
   do {                                                               \
-    if (tid == 0) k7_cnt[i] += (v);                                  \
+    if (tid == 0) atomicAdd(&k7_lds[0][i], (unsigned long long)(v)); \
   } while (0)
 #else
 #define K7_T(i) (void)0
@@ -199,8 +200,10 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
   load_lits(tkA, lvA);
   __syncthreads();
 #ifdef WG_K7_STATS
-  uint64_t k7_acc[16] = {}, k7_t = __builtin_amdgcn_s_memtime();
-  unsigned long long k7_cnt[16] = {};
+  __shared__ unsigned long long k7_lds[kWaves][16];
+  if ((tid & 63) < 16) k7_lds[wave][tid & 63] = 0;
+  __syncthreads();
+  uint64_t k7_t = __builtin_amdgcn_s_memtime();
 #endif
 
   // Per-pixel state of a thread's four pixels, packed in one register: bits 2j..2j+1 the
@@ -677,12 +680,12 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
   if (nblocks > 0) store_block(nblocks - 1, val[(nblocks - 1) & 1]);
 #ifdef WG_K7_STATS
   if (tid == 0) {
-    k7_cnt[0] = (unsigned long long)nblocks;
-    for (int i : {0, 1, 2, 3, 9, 10}) atomicAdd(&g_k7_stats[i], k7_cnt[i]);
-    for (int i : {4, 5, 6, 7, 8, 11, 12, 13, 14, 15}) atomicAdd(&g_k7_stats[i], k7_acc[i]);
+    k7_lds[0][0] = (unsigned long long)nblocks;
+    for (int i : {0, 1, 2, 3, 9, 10}) atomicAdd(&g_k7_stats[i], k7_lds[0][i]);
+    for (int i : {4, 5, 6, 7, 8, 11, 12, 13, 14, 15}) atomicAdd(&g_k7_stats[i], k7_lds[0][i]);
   }
-  if ((tid & 63) == 0)
-    for (int i : {4, 5, 6, 7, 8, 11, 12, 13, 14, 15}) atomicAdd(&g_k7_wave[wave][i], k7_acc[i]);
+  if (lane == 0)
+    for (int i : {4, 5, 6, 7, 8, 11, 12, 13, 14, 15}) atomicAdd(&g_k7_wave[wave][i], k7_lds[wave][i]);
 #endif
 }
 
