@@ -122,7 +122,11 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
   __shared__ uint32_t slot_set[kSlots / 32];     // slot written at least once
   __shared__ __attribute__((aligned(16))) uint32_t uval[kBlock];    // window updater values by rank
                                                                      // (serial path: the block's tokens)
-  __shared__ __attribute__((aligned(16))) uint32_t val[2][kBlock];  // this / the previous block's values
+  // this / the previous block's values (two objects, not one array: the literal values of block b + 1
+  // are loaded straight into the previous block's array, and the waitcnt pass must see that this
+  // block's array is not the loads' target)
+  __shared__ __attribute__((aligned(16))) uint32_t val0[kBlock];
+  __shared__ __attribute__((aligned(16))) uint32_t val1[kBlock];
   __shared__ int16_t ref[kBlock];                // pending copy: source pointer (pointer jumping)
   __shared__ uint8_t st[kBlock];                 // kKnown / kPendCopy / kPendLookup
   __shared__ __attribute__((aligned(16))) uint32_t wsum[kWaves];  // updaters per wave of the block
@@ -163,11 +167,16 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
   // A barrier that also returns whether any thread's p was set: one s_barrier (HIP's
   // __syncthreads_or costs three).  Flag word k & 3 is set before barrier k and read after it;
   // word (k + 2) & 3, last read before barrier k - 1, is cleared after barrier k for call k + 2.
+  // A workgroup barrier for LDS hand-offs only: __syncthreads() also waits vmcnt(0) while an
+  // LDS-destination load is in flight, which would drain the literal prefetch at every barrier.
+  // (Global memory needs no fence here: a block's stores are complete before the wait for the
+  // next block's staged literals, ahead of that block's rank barrier; see store_block.)
+  auto bar = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
   int orseq = 0;
   auto sync_or = [&](bool p) -> bool {
     const int slot = orseq & 3;
     if (p) orflag[slot] = 1;
-    __syncthreads();
+    bar();
     const bool r = orflag[slot] != 0;
     if (tid == 0) orflag[(slot + 2) & 3] = 0;
     ++orseq;
@@ -183,21 +192,25 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
     const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(tok_rs, b < nblocks ? 4u * p : kDropOff, 0, 0);
     tk[0] = q.x, tk[1] = q.y, tk[2] = q.z, tk[3] = q.w;
   };
-  auto load_lits = [&](const uint32_t* tk, uint32_t* lv) {
+  // literal values straight into LDS: slot j of the wave's 64 threads at stage[wave * 256 + 64 j +
+  // lane] of the block's value array (lane-linear, as an LDS-destination load writes); each
+  // thread reads its four back in step 1 before its own values overwrite the wave's range
+  auto load_lits = [&](const uint32_t* tk, uint32_t* stage) {
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
       const bool is_lit = (tk[j] & ~kTokPayload) == kTokLiteral;
-      lv[j] = __builtin_amdgcn_raw_buffer_load_b32(lit_rs, is_lit ? 4u * (tk[j] & kTokPayload) : kDropOff, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(lit_rs, stage + wave * kWavePx + 64 * j,
+                                               4, is_lit ? 4u * (tk[j] & kTokPayload) : kDropOff, 0, 0, 0);
     }
   };
   // Software pipeline: tokens two blocks ahead, literal values one block ahead.  Two register
   // sets (A for even blocks, B for odd), the block body inlined once per set: rotating one set
   // through copies at the loop latch would make every copy wait for its load (a register with
   // a load in flight cannot be read), collapsing the prefetch distance to nothing.
-  uint32_t tkA[kPer], lvA[kPer], tkB[kPer], lvB[kPer];
+  uint32_t tkA[kPer], tkB[kPer];
   load_tokens(0, tkA);
   load_tokens(1, tkB);
-  load_lits(tkA, lvA);
+  load_lits(tkA, val0);
   __syncthreads();
 #ifdef WG_K7_STATS
   __shared__ unsigned long long k7_lds[kWaves][16];
@@ -233,12 +246,21 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
         __builtin_amdgcn_raw_buffer_store_b32(ov[j], out_rs, pos0 + j < n ? 4u * (uint32_t)(pos0 + j) : kDropOff, 0, 0);
     }
   };
+  // LDS atomics without return as inline asm: the waitcnt pass makes every LDS atomic wait
+  // vmcnt(0) while an LDS-destination load is in flight (it cannot tell the target apart), which
+  // would drain the literal prefetch in every registration.  No result, so nothing waits on them;
+  // bar() orders them (lgkmcnt(0)), and a wave's LDS operations execute in order.
+  auto lds_addr = [](const void* p) { return (uint32_t)(size_t)p; };
+  auto ds_or_b64 = [&](uint64_t* p, uint64_t v) { asm volatile("ds_or_b64 %0, %1" ::"v"(lds_addr(p)), "v"(v) : "memory"); };
+  auto ds_or_b32 = [&](uint32_t* p, uint32_t v) { asm volatile("ds_or_b32 %0, %1" ::"v"(lds_addr(p)), "v"(v) : "memory"); };
+  auto ds_max_u32 = [&](uint32_t* p, uint32_t v) { asm volatile("ds_max_u32 %0, %1" ::"v"(lds_addr(p)), "v"(v) : "memory"); };
+  auto ds_min_i32 = [&](int* p, int v) { asm volatile("ds_min_i32 %0, %1" ::"v"(lds_addr(p)), "v"(v) : "memory"); };
   // mask bit, summary, last rank of an updater whose value is in uval[r]
   auto reg_hash = [&](int r, uint32_t x) {
     const uint32_t h = hash_px(x, shift);
-    atomicOr(reinterpret_cast<unsigned long long*>(&mask[h * W + (r >> 6)]), 1ull << (r & 63));
-    atomicOr(&summ[h], 1u << (r >> 6));
-    atomicMax(&slotrec[h].x, (uint32_t)r + 1u);
+    ds_or_b64(&mask[h * W + (r >> 6)], 1ull << (r & 63));
+    ds_or_b32(&summ[h], 1u << (r >> 6));
+    ds_max_u32(&slotrec[h].x, (uint32_t)r + 1u);
   };
   // step 3 for one registered updater: if it is its key's last in the window, write the slot
   // (unless the window goes serial) and clear the key's masks.  The other updaters of the key
@@ -251,7 +273,7 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
       summ[h] = 0;
       if (!go_serial) {
         slotrec[h] = make_uint2(0u, x);
-        atomicOr(&slot_set[h >> 5], 1u << (h & 31));
+        ds_or_b32(&slot_set[h >> 5], 1u << (h & 31));
       } else {
         slotrec[h].x = 0u;
       }
@@ -294,12 +316,9 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
   // (selects; a wave walks every side of a lane branch), the rare cases sit behind wave-uniform
   // branches, and the per-updater work (3.5 % of C5's pixels) runs one updater per lane over
   // the wave's compacted updaters instead of once per pixel slot.
-  auto block = [&](const int b, uint32_t* tk_in, uint32_t* lv_in, uint32_t* tk_nxt,
-                   uint32_t* lv_nxt) __attribute__((always_inline)) {
+  auto block = [&](const int b, uint32_t* tk_in, uint32_t* tk_nxt, uint32_t* vcur,
+                   uint32_t* vprv) __attribute__((always_inline)) {
     const int base = b * kBlock;
-    const int cur = b & 1, prv = cur ^ 1;
-    uint32_t* vcur = val[cur];
-    const uint32_t* vprv = val[prv];
 
     // ---- 1. tokens: literals, copies from before the block, unset pixels are known; in-block
     //         copies and lookups are pending.  Literals and copies are updaters (ranked).  A
@@ -330,7 +349,7 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
       const uint32_t code = inb ? kPC : farc ? kPF : is_cache ? kPL : kPK;
       ps |= code << (2 * j) | (~kind & 1u) << (8 + j);  // updaters: kinds 0 (literal) and 2 (copy)
       nearm |= (uint32_t)(is_copy & !inb & !farc) << j;
-      v[j] = lv_in[j];
+      v[j] = vcur[wave * kWavePx + 64 * j + lane];
       aux[j] = is_cache ? pl & (kSlots - 1) : pl;
     }
     K7_T(8);
@@ -345,9 +364,8 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
     *reinterpret_cast<uint4*>(&vcur[li0]) = make_uint4(v[0], v[1], v[2], v[3]);
     if (b > 0) store_block(b - 1, vprv);
     K7_T(15);
-    // the next blocks' inputs go out now (tk_in and lv_in are consumed)
+    // the tokens two blocks on go out now (tk_in is consumed)
     load_tokens(b + 2, tk_in);
-    load_lits(tk_nxt, lv_nxt);
     K7_T(14);
     if (bad) {
       if (err) atomicOr(err, 4);
@@ -366,7 +384,7 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
     if (lane == 0)
       wsum[wave] = (uint32_t)(__builtin_popcountll(b0) + 2 * __builtin_popcountll(b1) + 4 * __builtin_popcountll(b2)) |
                    (wave_far ? 0x10000u : 0u) | (wave_pc ? 0x20000u : 0u);
-    __syncthreads();
+    bar();
     K7_T(4);
     // the sixteen wave counts in lanes 0..15 (one DPP row): inclusive scan, then read lanes
     const uint32_t wraw = wsum[lane & 15];
@@ -412,6 +430,9 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
         }
       }
     }
+    // the next block's literal values, into the previous block's array (every wave is past its
+    // step 1, the last reader of vprv, since the rank barrier)
+    load_lits(tk_nxt, vprv);
     // in-block copies: sources and every pixel's state for the pointer jumping (rare in C5)
     if (blk_pc) {
       uint32_t stw = 0, rfw[2] = {0u, 0u};
@@ -460,7 +481,7 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
 #pragma unroll
         for (int j = kPer - 1; j >= 0; --j)
           if (pk(ps, j) == kPC) fp = li0 + j;
-        atomicMin(&first_pend[0], fp);
+        ds_min_i32(&first_pend[0], fp);
       }
       // (a) of a round: lookups of the window before the first pending copy fp.  kRounds: the
       // window has in-block copies (fp varies, and copies read the lookups' states); instantiated
@@ -552,7 +573,7 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
       // rank barrier, and a plain barrier orders the registrations before the lookups)
       int any_pc;
       if (nwin == 1) {
-        __syncthreads();
+        bar();
         any_pc = blk_pc;
       } else {
         any_pc = sync_or(pc);
@@ -577,7 +598,7 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
         if (in_win) lookups(fp, std::true_type{});
         K7_T(12);
         if (!any_pc) break;
-        __syncthreads();
+        bar();
         // (b) pending copies: take a known source's value and register, else jump one link back
         bool still = false;  // a copy of mine still pending
         if (in_win) {
@@ -599,7 +620,7 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
               if (nkeys) reg_hash(R(j) - rb, x);
             } else {
               if (ss == kPendCopy) ref[li] = ref[src];  // (a stale or fresh link: both lie on the chain)
-              atomicMin(&first_pend[(r + 1) & 1], li);
+              ds_min_i32(&first_pend[(r + 1) & 1], li);
               still = true;
             }
           }
@@ -607,7 +628,7 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
         any_pc = sync_or(still);
         K7_T(5);
       }
-      __syncthreads();  // every lookup has read the slot table; the masks are complete
+      bar();  // every lookup has read the slot table; the masks are complete
       const bool go_serial = slow[b & 1] != 0;
       // ---- 3. each key's last updater writes its slot and clears the key's masks
       // the window's updaters packed 64 to a wave by rank (uval is complete after the barrier):
@@ -623,13 +644,13 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
         // (pending copies of the window never registered: nothing of theirs to clear; a
         // window whose rounds hit the cap leaves their registered bits, cleared above)
         serial_from = q * wpw * kWavePx;
-        __syncthreads();
+        bar();
         break;
       }
       // between windows: the next window's registration follows this one's slot table.  After
       // the last window no barrier: the next block's rank barrier orders this slot table before
       // its registration, and nothing before that barrier touches the table, the masks or uval
-      if (q + 1 < nwin) __syncthreads();
+      if (q + 1 < nwin) bar();
       K7_T(13);
     }
     K7_T(5);
@@ -644,7 +665,7 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
         const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(tok_rs, 4u * (uint32_t)(base + li0), 0, 0);
         *reinterpret_cast<uint4*>(&uval[li0]) = make_uint4(q.x, q.y, q.z, q.w);
       }
-      __syncthreads();
+      bar();
       if (tid == 0) {
         const int cnt_px = min(kBlock, n - base);
         for (int li = serial_from; li < cnt_px; ++li) {
@@ -668,16 +689,18 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
         }
         slow[b & 1] = 0;
       }
-      __syncthreads();
+      bar();
     }
     K7_T(7);
   };
 
   for (int b = 0; b < nblocks; b += 2) {
-    block(b, tkA, lvA, tkB, lvB);
-    if (b + 1 < nblocks) block(b + 1, tkB, lvB, tkA, lvA);
+    block(b, tkA, tkB, val0, val1);
+    if (b + 1 < nblocks) block(b + 1, tkB, tkA, val1, val0);
   }
-  if (nblocks > 0) store_block(nblocks - 1, val[(nblocks - 1) & 1]);
+  if (nblocks > 0) store_block(nblocks - 1, (nblocks - 1) & 1 ? val1 : val0);
+  // the last block's literal load (past the stream) must land before the workgroup's LDS is freed
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #ifdef WG_K7_STATS
   if (tid == 0) {
     k7_lds[0][0] = (unsigned long long)nblocks;
