@@ -1048,14 +1048,24 @@ const uint8_t* window_ptr(const wg_batch* b, int i) {
 }
 // Every OK frame's RGBA window to out[i] (stride strides[i]): one wait for the batch, the
 // copies queued on the context stream, one wait for them.
-int download_rgba_all(wg_batch* b, uint8_t* const* out, const int32_t* strides, int32_t* status) {
+// Bytes a row-major output of h rows of `row` bytes at `stride` needs (0 rows: nothing).
+size_t out_bytes_needed(int stride, int row, int h) {
+  return h > 0 ? (size_t)stride * (size_t)(h - 1) + (size_t)row : 0;
+}
+
+// A caller's output buffer i: present, stride >= the row, capacity >= the window.
+bool out_ok(uint8_t* const* out, const int32_t* strides, const size_t* caps, int i, int row, int h) {
+  return out[i] != nullptr && strides[i] >= row && caps[i] >= out_bytes_needed(strides[i], row, h);
+}
+
+int download_rgba_all(wg_batch* b, uint8_t* const* out, const int32_t* strides, const size_t* caps, int32_t* status) {
   int st = batch_sync(b);
   if (st != WG_STATUS_OK) return st;
   hipError_t e = hipSuccess;
   for (int i = 0; i < b->n && e == hipSuccess; ++i) {
     if (status[i] != WG_STATUS_OK) continue;
     const FrameParse& f = b->fp[(size_t)i];
-    if (out[i] == nullptr || strides[i] < 4 * f.out_w) {
+    if (!out_ok(out, strides, caps, i, 4 * f.out_w, f.out_h)) {
       status[i] = WG_STATUS_INVALID_PARAM;
       continue;
     }
@@ -1084,19 +1094,28 @@ struct PipeChunk {
   BatchPtr b;
   hipEvent_t ev[4] = {};
   bool uploaded = false, up_ok = false, ran = false;
+  bool layout_ok = true;  // batch_layout ran (false: it threw; the chunk's frames carry the status)
 };
+
+// Every frame of [a, a + n) still OK gets `st` (an early exit must not leave frames that were never
+// decoded reading OK).
+void fail_frames(int32_t* status, int a, int n, int st) {
+  for (int i = a; i < a + n; ++i)
+    if (status[i] == WG_STATUS_OK) status[i] = st;
+}
 
 // Queue the chunk's RGBA windows to the caller's buffers on its stream (asynchronous for pinned
 // memory; the runtime stages pageable memory itself).  Frames with bad arguments get
 // INVALID_PARAM; the copies' own failure USER_ABORT.
-void pipe_download(PipeChunk& c, uint8_t* const* out, const int32_t* strides, int32_t* status, double* bytes) {
+void pipe_download(PipeChunk& c, uint8_t* const* out, const int32_t* strides, const size_t* caps, int32_t* status,
+                   double* bytes) {
   wg_batch* b = c.b.get();
   hipEventRecord(c.ev[2], c.s);
   for (int j = 0; j < c.n; ++j) {
     const int i = c.a + j;
     if (status[i] != WG_STATUS_OK) continue;
     const FrameParse& f = b->fp[(size_t)j];
-    if (out[i] == nullptr || strides[i] < 4 * f.out_w) {
+    if (!out_ok(out, strides, caps, i, 4 * f.out_w, f.out_h)) {
       status[i] = WG_STATUS_INVALID_PARAM;
       continue;
     }
@@ -1141,7 +1160,7 @@ void pipe_finish(PipeChunk& c, int32_t* status, wg_pipeline_stats* ps) {
 // retires chunk k - 2, so the host stage of one chunk, the kernels of the next and the transfers
 // of a third overlap.
 int decode_pipelined(wg_ctx* ctx, const uint8_t* const* data, const size_t* sizes, int n, uint8_t* const* out,
-                     const int32_t* strides, int32_t* status, int32_t flags) {
+                     const int32_t* strides, const size_t* caps, int32_t* status, int32_t flags) {
   const double t_start = now_s();
   wg_decoder_options o{};
   o.colorspace = 1;  // MODE_RGBA
@@ -1150,7 +1169,7 @@ int decode_pipelined(wg_ctx* ctx, const uint8_t* const* data, const size_t* size
   for (int i = 0; i < n; ++i) status[i] = WG_STATUS_OK;
   std::lock_guard<std::mutex> lock(ctx->mu);
   if (!set_device(ctx->device)) {
-    for (int i = 0; i < n; ++i) status[i] = WG_STATUS_INVALID_PARAM;
+    fail_frames(status, 0, n, WG_STATUS_INVALID_PARAM);
     return WG_STATUS_INVALID_PARAM;
   }
   // chunks: a fixed frame count, or about a sixteenth of the batch's pixels (>= 32 MPix each)
@@ -1194,6 +1213,7 @@ int decode_pipelined(wg_ctx* ctx, const uint8_t* const* data, const size_t* size
       if (!w && hipStreamCreateWithFlags(&w, hipStreamNonBlocking) != hipSuccess) {
         (void)hipGetLastError();
         w = nullptr;
+        fail_frames(status, 0, n, WG_STATUS_OUT_OF_MEMORY);
         return WG_STATUS_OUT_OF_MEMORY;
       }
   }
@@ -1205,6 +1225,15 @@ int decode_pipelined(wg_ctx* ctx, const uint8_t* const* data, const size_t* size
   // one chunk: everything on the context stream; else uploads on it, the rest on a work stream
   hipStream_t streams[2] = {K > 1 ? ctx->work[0] : ctx->stream, K > 1 ? ctx->work[1] : ctx->stream};
   std::vector<PipeChunk> ch((size_t)K);
+  // the chunks' events go on every exit path, once no thread can still wait on them
+  struct EventsGuard {
+    std::vector<PipeChunk>& ch;
+    ~EventsGuard() {
+      for (PipeChunk& c : ch)
+        for (hipEvent_t& e : c.ev)
+          if (e) hipEventDestroy(e), e = nullptr;
+    }
+  } events_guard{ch};
   for (int k = 0; k < K; ++k) {
     PipeChunk& c = ch[(size_t)k];
     c.a = bounds[(size_t)k];
@@ -1214,9 +1243,8 @@ int decode_pipelined(wg_ctx* ctx, const uint8_t* const* data, const size_t* size
     for (hipEvent_t& e : c.ev)
       if (hipEventCreate(&e) != hipSuccess) {
         (void)hipGetLastError();
-        for (PipeChunk& d : ch)
-          for (hipEvent_t& x : d.ev)
-            if (x) hipEventDestroy(x), x = nullptr;
+        e = nullptr;
+        fail_frames(status, 0, n, WG_STATUS_OUT_OF_MEMORY);
         return WG_STATUS_OUT_OF_MEMORY;
       }
   }
@@ -1242,7 +1270,8 @@ int decode_pipelined(wg_ctx* ctx, const uint8_t* const* data, const size_t* size
       }
       PipeChunk& c = ch[(size_t)k];
       hipEventRecord(c.ev[0], ctx->stream);
-      int st = guarded([&] { return batch_upload(c.b.get(), *arenas[c.arena]); });
+      int st = c.layout_ok ? guarded([&] { return batch_upload(c.b.get(), *arenas[c.arena]); })
+                           : (int)WG_STATUS_OUT_OF_MEMORY;
       hipEventRecord(c.ev[1], ctx->stream);
       c.up_ok = st == WG_STATUS_OK;
       if (st == WG_STATUS_OK && c.s != ctx->stream && hipStreamWaitEvent(c.s, c.ev[1], 0) != hipSuccess) {
@@ -1260,14 +1289,28 @@ int decode_pipelined(wg_ctx* ctx, const uint8_t* const* data, const size_t* size
       if (st != WG_STATUS_OK)
         for (int j = 0; j < c.n; ++j)
           if (status[c.a + j] == WG_STATUS_OK) status[c.a + j] = st;
-      if (k >= 1 && ch[(size_t)k - 1].ran) pipe_download(ch[(size_t)k - 1], out, strides, status, &ps.d2h_bytes);
+      if (k >= 1 && ch[(size_t)k - 1].ran) pipe_download(ch[(size_t)k - 1], out, strides, caps, status, &ps.d2h_bytes);
       if (k >= 2) pipe_finish(ch[(size_t)k - 2], status, &ps);
     }
-    if (ch[(size_t)K - 1].ran) pipe_download(ch[(size_t)K - 1], out, strides, status, &ps.d2h_bytes);
+    if (ch[(size_t)K - 1].ran) pipe_download(ch[(size_t)K - 1], out, strides, caps, status, &ps.d2h_bytes);
     for (int k = std::max(0, K - 2); k < K; ++k) pipe_finish(ch[(size_t)k], status, &ps);
   };
-  std::thread dev;
-  if (K > 1) dev = std::thread(device_side);
+  // the device thread is joined on every exit path (a joinable std::thread destroyed would
+  // terminate the process)
+  struct Joiner {
+    std::thread t;
+    ~Joiner() {
+      if (t.joinable()) t.join();
+    }
+  } dev;
+  if (K > 1) {
+    try {
+      dev.t = std::thread(device_side);
+    } catch (const std::system_error&) {  // nothing started yet: fail the call cleanly
+      fail_frames(status, 0, n, WG_STATUS_OUT_OF_MEMORY);
+      return WG_STATUS_OUT_OF_MEMORY;
+    }
+  }
   // The entropy stage as ONE pool run over all frames, claimed in order: a chunk's stragglers
   // overlap the next chunk's frames (no barrier per chunk).  A chunk's first frame readies its
   // arena (chunk k - 3, on the same arena, uploaded); its last frame lays it out and hands it to
@@ -1287,7 +1330,9 @@ int decode_pipelined(wg_ctx* ctx, const uint8_t* const* data, const size_t* size
         if (k >= kRing) {
           qcv.wait(ql, [&] { return uploaded[(size_t)(k - kRing)] != 0; });
           ql.unlock();
-          if (ch[(size_t)(k - kRing)].up_ok) hipEventSynchronize(ch[(size_t)(k - kRing)].ev[1]);
+          // (ev[1] is recorded after every upload attempt: a failed upload may still have queued
+          // copies out of the arena, which must finish before it is reused)
+          hipEventSynchronize(ch[(size_t)(k - kRing)].ev[1]);
           ql.lock();
         }
         arenas[c.arena]->begin_batch();
@@ -1301,8 +1346,15 @@ int decode_pipelined(wg_ctx* ctx, const uint8_t* const* data, const size_t* size
     wg::parse_frame(data[i], sizes[i], o, arenas[c.arena], &cursors[c.arena][(size_t)worker],
                     &c.b->fp[(size_t)(i - c.a)]);
     if (left[k].fetch_sub(1) == 1) {
-      for (auto& cu : cursors[c.arena]) arenas[c.arena]->release(&cu);
-      batch_layout(c.b.get(), *arenas[c.arena], status + c.a);
+      // (on a worker thread, outside guarded(): an allocation failure marks the chunk's frames and
+      // still hands the chunk over, so the device thread never waits for it forever)
+      try {
+        for (auto& cu : cursors[c.arena]) arenas[c.arena]->release(&cu);
+        batch_layout(c.b.get(), *arenas[c.arena], status + c.a);
+      } catch (...) {
+        c.layout_ok = false;
+        for (int j = 0; j < c.n; ++j) status[c.a + j] = WG_STATUS_OUT_OF_MEMORY;
+      }
       std::lock_guard<std::mutex> ql(qmu);
       ps.h2d_bytes += (double)c.b->in_bytes;
       parsed[(size_t)k] = 1;
@@ -1311,11 +1363,8 @@ int decode_pipelined(wg_ctx* ctx, const uint8_t* const* data, const size_t* size
   });
   const double t_parsed = now_s();
   ps.parse_s = t_parsed - t_parse0;
-  if (K > 1) dev.join();
+  if (K > 1) dev.t.join();
   else device_side();
-  for (PipeChunk& c : ch)
-    for (hipEvent_t& e : c.ev)
-      if (e) hipEventDestroy(e), e = nullptr;
   const double t_end = now_s();
   ps.drain_s = t_end - t_parsed;
   ps.wall_s = t_end - t_start;
@@ -1386,9 +1435,10 @@ int wg_batch_download_yuv(wg_batch* b, int i, uint8_t* y, uint8_t* u, uint8_t* v
 }
 
 int wg_decode_rgba_batch(wg_ctx* ctx, const uint8_t* const* data, const size_t* sizes, int n,
-                         uint8_t* const* rgba, const int32_t* strides, int32_t* status, int32_t flags) {
-  if (!ctx || !data || !sizes || !rgba || !strides || !status || n <= 0) return WG_STATUS_INVALID_PARAM;
-  return guarded([&] { return decode_pipelined(ctx, data, sizes, n, rgba, strides, status, flags); });
+                         uint8_t* const* rgba, const int32_t* strides, const size_t* caps, int32_t* status,
+                         int32_t flags) {
+  if (!ctx || !data || !sizes || !rgba || !strides || !caps || !status || n <= 0) return WG_STATUS_INVALID_PARAM;
+  return guarded([&] { return decode_pipelined(ctx, data, sizes, n, rgba, strides, caps, status, flags); });
 }
 
 int wg_ctx_set_chunk_frames(wg_ctx* ctx, int frames) {
@@ -1411,8 +1461,10 @@ void wg_host_free(void* p) {
 }
 
 int wg_decode_rgba_batch_multi(wg_ctx* const* ctxs, int n_ctx, const uint8_t* const* data, const size_t* sizes,
-                               int n, uint8_t* const* rgba, const int32_t* strides, int32_t* status, int32_t flags) {
-  if (!ctxs || n_ctx <= 0 || !data || !sizes || !rgba || !strides || !status || n <= 0) return WG_STATUS_INVALID_PARAM;
+                               int n, uint8_t* const* rgba, const int32_t* strides, const size_t* caps,
+                               int32_t* status, int32_t flags) {
+  if (!ctxs || n_ctx <= 0 || !data || !sizes || !rgba || !strides || !caps || !status || n <= 0)
+    return WG_STATUS_INVALID_PARAM;
   for (int k = 0; k < n_ctx; ++k)
     if (!ctxs[k]) return WG_STATUS_INVALID_PARAM;
   const int shards = std::min(n_ctx, n);
@@ -1421,7 +1473,8 @@ int wg_decode_rgba_batch_multi(wg_ctx* const* ctxs, int n_ctx, const uint8_t* co
   auto run = [&](int k) {
     const int a = (int)((int64_t)k * n / shards), e = (int)((int64_t)(k + 1) * n / shards);
     rc[(size_t)k] = guarded([&] {
-      return wg_decode_rgba_batch(ctxs[k], data + a, sizes + a, e - a, rgba + a, strides + a, status + a, flags);
+      return wg_decode_rgba_batch(ctxs[k], data + a, sizes + a, e - a, rgba + a, strides + a, caps + a, status + a,
+                                  flags);
     });
   };
   std::vector<std::thread> th;
@@ -1440,8 +1493,9 @@ int wg_decode_rgba_batch_multi(wg_ctx* const* ctxs, int n_ctx, const uint8_t* co
 }
 
 int wg_decode_batch(wg_ctx* ctx, const uint8_t* const* data, const size_t* sizes, int n, const wg_decoder_options* opt,
-                    uint8_t* const* out, const int32_t* strides, int32_t* status) {
-  if (!ctx || !data || !sizes || !out || !strides || !status || !opt || n <= 0) return WG_STATUS_INVALID_PARAM;
+                    uint8_t* const* out, const int32_t* strides, const size_t* caps, int32_t* status) {
+  if (!ctx || !data || !sizes || !out || !strides || !caps || !status || !opt || n <= 0)
+    return WG_STATUS_INVALID_PARAM;
   wg_batch* b = wg_batch_create_ex(ctx, data, sizes, n, opt, status);
   if (!b) return WG_STATUS_OUT_OF_MEMORY;
   int st = wg_batch_run(b, nullptr);
@@ -1478,7 +1532,7 @@ int wg_decode_batch(wg_ctx* ctx, const uint8_t* const* data, const size_t* sizes
     for (int i = 0; st == WG_STATUS_OK && i < n; ++i) {
       const FrameParse& f = b->fp[i];
       if (status[i] != WG_STATUS_OK) continue;
-      if (out[i] == nullptr || strides[i] < bpp * f.out_w) {
+      if (!out_ok(out, strides, caps, i, bpp * f.out_w, f.out_h)) {
         status[i] = WG_STATUS_INVALID_PARAM;
         continue;
       }
@@ -1491,7 +1545,7 @@ int wg_decode_batch(wg_ctx* ctx, const uint8_t* const* data, const size_t* sizes
     ctx->cache.put(d_out);
     ctx->cache.put(d_ed);
   } else if (st == WG_STATUS_OK) {
-    st = download_rgba_all(b, out, strides, status);
+    st = download_rgba_all(b, out, strides, caps, status);
   }
   wg_batch_destroy(b);
   return st;
@@ -1517,8 +1571,9 @@ int wg_decode_into(const uint8_t* data, size_t size, const wg_decoder_options* o
   const size_t s[1] = {size};
   uint8_t* o[1] = {out};
   const int32_t str[1] = {stride};
+  const size_t caps[1] = {cap};
   int32_t fs[1] = {0};
-  st = wg_decode_batch(ctx.get(), d, s, 1, opt, o, str, fs);
+  st = wg_decode_batch(ctx.get(), d, s, 1, opt, o, str, caps, fs);
   return st != WG_STATUS_OK ? st : fs[0];
 }
 
@@ -1535,8 +1590,9 @@ int wg_decode_rgba_into(const uint8_t* data, size_t size, uint8_t* rgba, size_t 
   const size_t s[1] = {size};
   uint8_t* o[1] = {rgba};
   const int32_t str[1] = {stride};
+  const size_t caps[1] = {cap};
   int32_t fs[1] = {0};
-  st = wg_decode_rgba_batch(ctx.get(), d, s, 1, o, str, fs, flags);
+  st = wg_decode_rgba_batch(ctx.get(), d, s, 1, o, str, caps, fs, flags);
   return st != WG_STATUS_OK ? st : fs[0];
 }
 

@@ -331,6 +331,13 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
 #pragma unroll
       for (int j = 0; j < kPer; ++j) tk_in[j] = base + li0 + j < n ? tk_in[j] : kTokUnset;
     }
+    // The staged literal values (buffer_load ... lds, issued last in the previous block) have
+    // landed before step 1 reads them, and so have this wave's stores of block b - 2 before the
+    // rank barrier below (far copies of other waves read them).  The waitcnt pass would place the
+    // same wait only because it tells val0 from val1; this one does not depend on that analysis
+    // (tests/test_k7_isa.py checks that no path reaches these reads from an LDS-DMA load without
+    // a vmcnt(0)).
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
       const int li = li0 + j;

@@ -181,7 +181,7 @@ _SIGS = {
     "wg_decode_rgba_into": (C.c_int, [_P, C.c_size_t, _P, C.c_size_t, C.c_int, C.c_int]),
     "wg_ctx_create": (_P, [C.c_int, C.c_int]),
     "wg_ctx_destroy": (None, [_P]),
-    "wg_decode_rgba_batch": (C.c_int, [_P, _P, _P, C.c_int, _P, _P, _P, C.c_int32]),
+    "wg_decode_rgba_batch": (C.c_int, [_P, _P, _P, C.c_int, _P, _P, _P, _P, C.c_int32]),
     "wg_batch_create": (_P, [_P, _P, _P, C.c_int, C.c_int32, _P]),
     "wg_batch_destroy": (None, [_P]),
     "wg_batch_run": (C.c_int, [_P, _P]),
@@ -202,7 +202,7 @@ _SIGS = {
     "wg_anim_demux": (C.c_int, [_P, C.c_size_t, _P, _P, C.c_int]),
     "wg_output_bpp": (C.c_int, [C.c_int]),
     "wg_decode_into": (C.c_int, [_P, C.c_size_t, _P, _P, C.c_size_t, C.c_int]),
-    "wg_decode_batch": (C.c_int, [_P, _P, _P, C.c_int, _P, _P, _P, _P]),
+    "wg_decode_batch": (C.c_int, [_P, _P, _P, C.c_int, _P, _P, _P, _P, _P]),
     "wg_batch_create_ex": (_P, [_P, _P, _P, C.c_int, _P, _P]),
     "wg_batch_download": (C.c_int, [_P, C.c_int, _P, C.c_int]),
     "wg_batch_frame_status": (C.c_int, [_P, C.c_int]),
@@ -210,7 +210,7 @@ _SIGS = {
     "wg_decode_status": (C.c_int, [_P, C.c_size_t, _P]),
     "wg_set_default_device": (C.c_int, [C.c_int]),
     "wg_vp8l_resolve_device": (C.c_int, [_P, _P, C.c_int, C.c_int, C.c_int, _P, _P]),
-    "wg_decode_rgba_batch_multi": (C.c_int, [_P, C.c_int, _P, _P, C.c_int, _P, _P, _P, C.c_int32]),
+    "wg_decode_rgba_batch_multi": (C.c_int, [_P, C.c_int, _P, _P, C.c_int, _P, _P, _P, _P, C.c_int32]),
     "wg_ctx_set_chunk_frames": (C.c_int, [_P, C.c_int]),
     "wg_ctx_pipeline_stats": (C.c_int, [_P, _P]),
     "wg_host_alloc": (_P, [C.c_size_t]),
@@ -526,8 +526,9 @@ class Context:
             outs.append(np.zeros((max(h, 1), max(w, 1) * bpp), np.uint8))
         optr = (C.c_void_p * n)(*[o.ctypes.data for o in outs])
         strides = (C.c_int32 * n)(*[o.shape[1] for o in outs])
+        caps = (C.c_size_t * n)(*[o.nbytes for o in outs])
         status = np.zeros(n, np.int32)
-        st = lib().wg_decode_batch(self._h, ptrs, sizes, n, C.byref(opts), optr, strides, status.ctypes.data)
+        st = lib().wg_decode_batch(self._h, ptrs, sizes, n, C.byref(opts), optr, strides, caps, status.ctypes.data)
         if st != Status.OK:
             raise WebPError(st, "wg_decode_batch")
         return [o if s == 0 else None for o, s in zip(outs, status)], status
@@ -564,9 +565,9 @@ class Context:
         arrays are written by DMA).  Pipelined in chunks (wg_decode_rgba_batch)."""
         bufs, ptrs, sizes = _ptr_arrays(datas)
         n = len(bufs)
-        outs, optr, strides = _rgba_outs(bufs, out)
+        outs, optr, strides, caps = _rgba_outs(bufs, out)
         status = np.zeros(n, np.int32)
-        st = lib().wg_decode_rgba_batch(self._h, ptrs, sizes, n, optr, strides, status.ctypes.data, flags)
+        st = lib().wg_decode_rgba_batch(self._h, ptrs, sizes, n, optr, strides, caps, status.ctypes.data, flags)
         if st != Status.OK:
             raise WebPError(st, "wg_decode_rgba_batch")
         return [o if s == Status.OK else None for o, s in zip(outs, status)], status
@@ -587,7 +588,7 @@ class Context:
 
 def _rgba_outs(bufs, out):
     n = len(bufs)
-    outs, optr, strides = [], (C.c_void_p * n)(), (C.c_int32 * n)()
+    outs, optr, strides, caps = [], (C.c_void_p * n)(), (C.c_int32 * n)(), (C.c_size_t * n)()
     for i, b in enumerate(bufs):
         if out is not None:
             a = out[i]
@@ -602,7 +603,8 @@ def _rgba_outs(bufs, out):
         outs.append(a)
         optr[i] = a.ctypes.data
         strides[i] = a.shape[1] * 4
-    return outs, optr, strides
+        caps[i] = a.nbytes  # the C side checks every frame's window against it
+    return outs, optr, strides, caps
 
 
 class MultiContext:
@@ -617,10 +619,10 @@ class MultiContext:
         """Same contract as Context.decode_batch: (list of RGBA arrays or None, status)."""
         bufs, ptrs, sizes = _ptr_arrays(datas)
         n = len(bufs)
-        outs, optr, strides = _rgba_outs(bufs, out)
+        outs, optr, strides, caps = _rgba_outs(bufs, out)
         status = np.zeros(n, np.int32)
         hs = (C.c_void_p * len(self.contexts))(*[c._h for c in self.contexts])
-        st = lib().wg_decode_rgba_batch_multi(hs, len(self.contexts), ptrs, sizes, n, optr, strides,
+        st = lib().wg_decode_rgba_batch_multi(hs, len(self.contexts), ptrs, sizes, n, optr, strides, caps,
                                               status.ctypes.data, flags)
         if st != Status.OK:
             raise WebPError(st, "wg_decode_rgba_batch_multi")

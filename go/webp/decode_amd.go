@@ -141,7 +141,7 @@ func (d *Decoder) Close() {
 type batchArgs struct {
 	n               int
 	dataP, outP     []*C.uint8_t
-	sizes           []C.size_t
+	sizes, caps     []C.size_t
 	strides, status []C.int32_t
 	raw             []unsafe.Pointer
 	pinner          runtime.Pinner
@@ -162,6 +162,7 @@ func newBatchArgs(frames [][]byte) *batchArgs {
 	a.dataP = cAlloc[*C.uint8_t](a, n)
 	a.outP = cAlloc[*C.uint8_t](a, n)
 	a.sizes = cAlloc[C.size_t](a, n)
+	a.caps = cAlloc[C.size_t](a, n)
 	a.strides = cAlloc[C.int32_t](a, n)
 	a.status = cAlloc[C.int32_t](a, n)
 	for i, f := range frames {
@@ -178,6 +179,7 @@ func newBatchArgs(frames [][]byte) *batchArgs {
 		a.dataP[i], a.sizes[i] = cBytes(f)
 		a.outP[i] = (*C.uint8_t)(unsafe.Pointer(&a.imgs[i].Pix[0]))
 		a.strides[i] = C.int32_t(a.imgs[i].Stride)
+		a.caps[i] = C.size_t(len(a.imgs[i].Pix))
 	}
 	return a
 }
@@ -218,7 +220,7 @@ func (d *Decoder) DecodeBatch(frames [][]byte) ([]*image.NRGBA, []error) {
 	}
 	a := newBatchArgs(frames)
 	st := C.wg_decode_rgba_batch(d.ctx, &a.dataP[0], &a.sizes[0], C.int(a.n), &a.outP[0], &a.strides[0],
-		&a.status[0], 0)
+		&a.caps[0], &a.status[0], 0)
 	return a.finish(st, "DecodeBatch")
 }
 
@@ -238,7 +240,8 @@ func (d *Decoder) Stats() (C.wg_pipeline_stats, error) {
 // device writes it by DMA.  Being C memory it needs no runtime.Pinner; release it with Free.
 type PinnedNRGBA struct {
 	*image.NRGBA
-	p unsafe.Pointer
+	p     unsafe.Pointer
+	bytes int // size of the C block at p (the capacity the library checks every frame against)
 }
 
 func NewPinnedNRGBA(w, h int) (*PinnedNRGBA, error) {
@@ -247,18 +250,22 @@ func NewPinnedNRGBA(w, h int) (*PinnedNRGBA, error) {
 		return nil, &StatusError{Code: int(C.WG_STATUS_OUT_OF_MEMORY), What: "NewPinnedNRGBA"}
 	}
 	pix := unsafe.Slice((*byte)(p), 4*w*h)
-	return &PinnedNRGBA{NRGBA: &image.NRGBA{Pix: pix, Stride: 4 * w, Rect: image.Rect(0, 0, w, h)}, p: p}, nil
+	return &PinnedNRGBA{NRGBA: &image.NRGBA{Pix: pix, Stride: 4 * w, Rect: image.Rect(0, 0, w, h)}, p: p,
+		bytes: 4 * w * h}, nil
 }
 
 func (m *PinnedNRGBA) Free() {
 	if m.p != nil {
 		C.wg_host_free(m.p)
-		m.p, m.NRGBA = nil, nil
+		m.p, m.NRGBA, m.bytes = nil, nil, 0
 	}
 }
 
 // DecodeBatchInto decodes frames[i] into dst[i] (reused across calls, e.g. PinnedNRGBA
-// buffers of a serving loop); dst[i] must match frame i's size.  Per-frame errors.
+// buffers of a serving loop); dst[i] must hold frame i (Stride >= 4 * width, enough rows).
+// Per-frame errors: a nil or freed dst[i] is INVALID_PARAM here, and the library checks every
+// frame's window against dst[i]'s allocation (INVALID_PARAM, nothing written) -- a frame larger
+// than the buffer reused for it never writes past the buffer.
 func (d *Decoder) DecodeBatchInto(frames [][]byte, dst []*PinnedNRGBA) []error {
 	n := len(frames)
 	errs := make([]error, n)
@@ -270,6 +277,7 @@ func (d *Decoder) DecodeBatchInto(frames [][]byte, dst []*PinnedNRGBA) []error {
 	a.dataP = cAlloc[*C.uint8_t](a, n)
 	a.outP = cAlloc[*C.uint8_t](a, n)
 	a.sizes = cAlloc[C.size_t](a, n)
+	a.caps = cAlloc[C.size_t](a, n)
 	a.strides = cAlloc[C.int32_t](a, n)
 	a.status = cAlloc[C.int32_t](a, n)
 	for i, f := range frames {
@@ -277,12 +285,21 @@ func (d *Decoder) DecodeBatchInto(frames [][]byte, dst []*PinnedNRGBA) []error {
 			a.pinner.Pin(&f[0])
 		}
 		a.dataP[i], a.sizes[i] = cBytes(f)
+		if dst[i] == nil || dst[i].p == nil || dst[i].NRGBA == nil {
+			// NULL output: the library reports INVALID_PARAM for the frame
+			errs[i] = &StatusError{Code: int(C.WG_STATUS_INVALID_PARAM), What: fmt.Sprintf("frame %d: no buffer", i)}
+			continue
+		}
 		a.outP[i] = (*C.uint8_t)(dst[i].p) // C memory: no pinning needed
 		a.strides[i] = C.int32_t(dst[i].Stride)
+		a.caps[i] = C.size_t(dst[i].bytes)
 	}
 	st := C.wg_decode_rgba_batch(d.ctx, &a.dataP[0], &a.sizes[0], C.int(n), &a.outP[0], &a.strides[0],
-		&a.status[0], 0)
+		&a.caps[0], &a.status[0], 0)
 	for i := range errs {
+		if errs[i] != nil {
+			continue
+		}
 		if err := statusErr(st, "DecodeBatchInto"); err != nil {
 			errs[i] = err
 		} else {
@@ -326,7 +343,7 @@ func (m *MultiDecoder) DecodeBatch(frames [][]byte) ([]*image.NRGBA, []error) {
 	ctxs := cAlloc[*C.wg_ctx](a, len(m.ctxs))
 	copy(ctxs, m.ctxs)
 	st := C.wg_decode_rgba_batch_multi(&ctxs[0], C.int(len(ctxs)), &a.dataP[0], &a.sizes[0], C.int(a.n), &a.outP[0],
-		&a.strides[0], &a.status[0], 0)
+		&a.strides[0], &a.caps[0], &a.status[0], 0)
 	return a.finish(st, "MultiDecoder.DecodeBatch")
 }
 

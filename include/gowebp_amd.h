@@ -128,10 +128,13 @@ void wg_ctx_destroy(wg_ctx* ctx);
  * chunk k's kernels and download (two staging arenas, two streams) -- the parse / finish
  * overlap of libwebp's threaded decode (frame_dec.c.go:505-534, 611-667) at batch scale.  Each
  * frame's result is that of a one-batch decode.  Output memory from wg_host_alloc (pinned) is
- * written by DMA; any other memory through the HIP runtime's staged copies. */
+ * written by DMA; any other memory through the HIP runtime's staged copies.  caps[i] is the
+ * size in bytes of the buffer at rgba[i]: a frame whose output (strides[i] * (h - 1) + 4 * w
+ * bytes) does not fit, or whose rgba[i] is NULL or strides[i] < 4 * w, is INVALID_PARAM and
+ * nothing is written to it (WebPDecodeRGBAInto's output_buffer_size check, webp.go:592-594). */
 int wg_decode_rgba_batch(wg_ctx* ctx, const uint8_t* const* data, const size_t* sizes, int n,
-                         uint8_t* const* rgba, const int32_t* strides, int32_t* status,
-                         int32_t flags);
+                         uint8_t* const* rgba, const int32_t* strides, const size_t* caps,
+                         int32_t* status, int32_t flags);
 
 /* Frames per pipeline chunk of wg_decode_rgba_batch (0 = automatic: about a sixteenth of the
  * batch's pixels, at least 32 MPix per chunk, the last chunks halving; n >= the batch = no
@@ -165,12 +168,14 @@ void wg_host_free(void* p);
  * Returns OK if every shard ran (check status[]), else the first failing shard's code. */
 int wg_decode_rgba_batch_multi(wg_ctx* const* ctxs, int n_ctx, const uint8_t* const* data,
                                const size_t* sizes, int n, uint8_t* const* rgba,
-                               const int32_t* strides, int32_t* status, int32_t flags);
+                               const int32_t* strides, const size_t* caps, int32_t* status,
+                               int32_t flags);
 
-/* As wg_decode_rgba_batch with full output options (colorspace, cropping, flip). */
+/* As wg_decode_rgba_batch with full output options (colorspace, cropping, flip); caps[i] is
+ * checked against strides[i] * (h - 1) + bpp * w of the output window. */
 int wg_decode_batch(wg_ctx* ctx, const uint8_t* const* data, const size_t* sizes, int n,
                     const wg_decoder_options* opt, uint8_t* const* out, const int32_t* strides,
-                    int32_t* status);
+                    const size_t* caps, int32_t* status);
 
 /* ---- device-resident batch (benchmarks, tests) -------------------------------------- */
 typedef struct wg_batch wg_batch;

@@ -110,3 +110,31 @@ def test_alpha_and_wide_frames_across_chunks():
             assert _sha(got[2]) == want_c2[0] and _sha(got[7]) == want_c2[1]
     finally:
         ctx.close()
+
+
+def test_undersized_outputs_rejected_not_overrun():
+    """A reused output buffer smaller than the frame (fewer rows, or a narrower stride) is the
+    frame's INVALID_PARAM and nothing is written past it (WebPDecodeRGBAInto's size check,
+    webp.go:592-594): the capacity array of wg_decode_rgba_batch / wg_decode_batch is checked
+    per frame.  The other frames of the batch decode normally."""
+    frames, want = _c2_frames(3)
+    ctx = webp_amd.Context(0, host_threads=2)
+    try:
+        for chunk in (0, 1):
+            ctx.set_chunk_frames(chunk)
+            backing = np.full((1080 + 16, 1920, 4), 0xA5, np.uint8)
+            short = backing[:1000]  # 80 rows short of the frame; the sentinel rows follow it
+            narrow = np.zeros((1080, 1900, 4), np.uint8)  # stride 4 * 1900 < 4 * 1920
+            good = np.zeros((1080, 1920, 4), np.uint8)
+            got, st = ctx.decode_batch(frames, out=[short, good, narrow])
+            assert list(st) == [webp_amd.Status.INVALID_PARAM, 0, webp_amd.Status.INVALID_PARAM], st
+            assert got[0] is None and got[2] is None
+            assert _sha(got[1]) == want[1]
+            assert (backing[1000:] == 0xA5).all(), "rows past the short buffer were written"
+        # the options path (wg_decode_batch) checks the same against bpp * width
+        opts = webp_amd.DecoderOptions()
+        opts.colorspace = 0  # MODE_RGB, 3 bytes per pixel
+        outs, st = ctx.decode_batch_opts(frames[:1], opts)
+        assert st[0] == 0 and outs[0].shape == (1080, 1920 * 3)
+    finally:
+        ctx.close()
