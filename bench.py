@@ -252,6 +252,78 @@ def cpu_baseline_parallel(datas, seconds, threads):
                        f"(entropy stage + oracle/ CPU restatement), {el:.1f}s")
 
 
+def _libwebp():
+    """libwebp 1.6.0 as Pillow bundles it (the upstream the reference translates,
+    pkg/vp8/constants.go:18-20), loaded by ctypes: a real-world CPU decoder to set beside the
+    restatement.  Returns (lib, cpuinfo pointer cell, its SIMD value) or raises."""
+    import ctypes as C
+    import glob
+    import PIL
+    libs = os.path.join(os.path.dirname(os.path.dirname(PIL.__file__)), "pillow.libs")
+    C.CDLL(glob.glob(os.path.join(libs, "libsharpyuv-*.so*"))[0], mode=C.RTLD_GLOBAL)
+    lib = C.CDLL(glob.glob(os.path.join(libs, "libwebp-*.so*"))[0])
+    ver = lib.WebPGetDecoderVersion()
+    if ver != 0x010600:
+        raise RuntimeError(f"libwebp version {ver:#x}, not 1.6.0")
+    lib.WebPDecodeRGBAInto.restype = C.c_void_p
+    lib.WebPDecodeRGBAInto.argtypes = [C.c_char_p, C.c_size_t, C.c_void_p, C.c_size_t, C.c_int]
+    cpu = C.c_void_p.in_dll(lib, "VP8GetCPUInfo")
+    return lib, cpu, cpu.value
+
+
+def cpu_baseline_libwebp(datas, seconds, threads=1, simd=True):
+    """libwebp 1.6.0's WebPDecodeRGBAInto (the C library the reference is a translation of) on
+    `threads` host threads, with its SIMD kernels or, simd=False, its plain-C ones
+    (VP8GetCPUInfo = NULL, the code the reference's Go translates).  Frames decoded until
+    `seconds` elapse; ctypes releases the GIL inside the call."""
+    import threading
+    import webp_amd
+    lib, cpu, simd_ptr = _libwebp()
+    cpu.value = simd_ptr if simd else None
+    dims = [(webp_amd.features(d).width, webp_amd.features(d).height) for d in datas]
+    outs = [np.empty(max(w * h * 4 for w, h in dims), np.uint8) for _ in range(threads)]
+    # warm-up: runs libwebp's DSP init for this cpuinfo setting before the threads start
+    w0, h0 = dims[0]
+    if not lib.WebPDecodeRGBAInto(datas[0], len(datas[0]), outs[0].ctypes.data, outs[0].nbytes, 4 * w0):
+        raise RuntimeError("WebPDecodeRGBAInto failed")
+    pix, cnt = [0] * threads, [0] * threads
+    t0 = time.perf_counter()
+    stop = t0 + seconds
+
+    def work(t):
+        n = t
+        o = outs[t]
+        while time.perf_counter() < stop:
+            d = datas[n % len(datas)]
+            w, h = dims[n % len(datas)]
+            lib.WebPDecodeRGBAInto(d, len(d), o.ctypes.data, o.nbytes, 4 * w)
+            pix[t] += w * h
+            cnt[t] += 1
+            n += threads
+
+    ths = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    el = time.perf_counter() - t0
+    cpu.value = simd_ptr
+    return dict(value=round(sum(pix) / el / 1e6, 2), unit="MPix/s", cores=threads, kind="libwebp-1.6.0",
+                simd=simd, sample=f"{sum(cnt)} frames of the same workload through libwebp 1.6.0 WebPDecodeRGBAInto "
+                                  f"({'SIMD' if simd else 'plain-C'} DSP, Pillow's bundled build) on {threads} "
+                                  f"host thread(s), {el:.1f}s")
+
+
+def cpu_baselines_libwebp(datas, seconds, threads):
+    """1-core SIMD, 1-core plain-C and all-cores SIMD libwebp figures, or the reason there are none."""
+    try:
+        return {"simd_1_core": cpu_baseline_libwebp(datas, seconds, 1, True),
+                "plain_c_1_core": cpu_baseline_libwebp(datas, seconds, 1, False),
+                "simd_all_cores": cpu_baseline_libwebp(datas, seconds, threads, True)}
+    except Exception as e:  # noqa: BLE001 -- recorded in the line, never fatal
+        return {"unavailable": f"{type(e).__name__}: {e}"}
+
+
 # ------------------------------------------------------------------------------- host cores
 def host_cpus():
     """CPUs this job may use: the affinity mask, bounded by the cgroup's CPU quota (a GPU box
@@ -559,6 +631,15 @@ def main():
             if "end_to_end" in out:
                 out["end_to_end"]["vs_cpu_all_cores"] = round(out["end_to_end"]["value"] / cba["value"], 2)
                 out["end_to_end"]["vs_cpu_1_core"] = round(out["end_to_end"]["value"] / cb["value"], 1)
+            # a real-world CPU decoder beside the restatement (not the contract's cpu_baseline)
+            lw = cpu_baselines_libwebp(datas, max(2.0, args.cpu_seconds / 4), threads)
+            out["cpu_baseline_libwebp"] = lw
+            if "simd_1_core" in lw:
+                out["speedup_vs_libwebp_simd_1_core"] = round(value / lw["simd_1_core"]["value"], 1)
+                out["speedup_vs_libwebp_simd_all_cores"] = round(value / lw["simd_all_cores"]["value"], 1)
+                if "end_to_end" in out:
+                    out["end_to_end"]["vs_libwebp_simd_all_cores"] = round(
+                        out["end_to_end"]["value"] / lw["simd_all_cores"]["value"], 2)
         print(json.dumps(out), flush=True)
     barrier()
     b.close()
