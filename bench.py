@@ -43,9 +43,9 @@ WORKLOADS = {
     "c5": dict(prefix="c5_ll2048", name="c5_ll2048_x256",
                desc="2048x2048 VP8L lossless (predictor + cross-color + subtract-green + color cache), batch 256"),
 }
-# the order of Batch.kernel_ms() / kernel_bytes(): K1, K2, K3, K4, K7
+# the order of Batch.kernel_ms() / kernel_bytes(): K1, K2, K3, K4, K7, K6, K5
 KERNELS = ("vp8_recon_filter_kernel", "yuv_to_rgba_kernel", "vp8l_transforms_kernel", "alpha_kernel",
-           "vp8l_resolve_kernel")
+           "vp8l_resolve_kernel", "emit_kernel", "anim_compose_kernel")
 
 
 def _load_frames(prefix):

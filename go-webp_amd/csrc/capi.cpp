@@ -29,6 +29,7 @@
 
 using wg::AlphaDesc;
 using wg::AnimFrameDesc;
+using wg::EmitDesc;
 using wg::FrameDesc;
 using wg::FrameParse;
 using wg::LLDesc;
@@ -184,10 +185,10 @@ constexpr size_t kAlign = 256;
 inline size_t align_up(size_t v) { return (v + kAlign - 1) & ~(kAlign - 1); }
 
 // Kernels in launch order (stage) and in the public order of wg_batch_kernel_ms (K1, K2, K3,
-// K4, K7): stage s runs between events ev[s] and ev[s + 1].
-constexpr int kStages = 5;
-constexpr int kStageK1 = 0, kStageK2 = 1, kStageK7 = 2, kStageK3 = 3, kStageK4 = 4;
-constexpr int kPublicOfStage[kStages] = {0, 1, 4, 2, 3};
+// K4, K7, K6, K5): stage s runs between events ev[s] and ev[s + 1].
+constexpr int kStages = 7;
+constexpr int kStageK1 = 0, kStageK2 = 1, kStageK7 = 2, kStageK3 = 3, kStageK4 = 4, kStageK6 = 5, kStageK5 = 6;
+constexpr int kPublicOfStage[kStages] = {0, 1, 4, 2, 3, 5, 6};
 struct Timing {
   hipEvent_t ev[kStages + 1] = {};
   bool ran[kStages] = {};
@@ -225,7 +226,7 @@ struct wg_batch {
   int n_wide = 0;                          // lossy frames wider than that (global column store)
   int n_valid = 0;
   int64_t pixels = 0;
-  double kbytes[kStages] = {};  // public order: K1, K2, K3, K4, K7
+  double kbytes[kStages] = {};  // public order: K1, K2, K3, K4, K7, K6, K5
   double k1_fused_bytes = 0;  // K1 with its RGBA tail: inputs + RGBA (planes are an intermediate)
   std::vector<Timing> timings;  // one per run since the last query
   size_t n_runs_pending = 0;
@@ -234,6 +235,22 @@ struct wg_batch {
   // batch_wait waits for all of them, so runs on several user streams are all complete before
   // the buffers go back to the cache
   std::vector<std::pair<hipStream_t, hipEvent_t>> done;
+  // K6 (f4): a non-RGBA colorspace or a flipped output is a stage of wg_batch_run, from the
+  // frames' RGBA windows into d_out (frame i at off_out[i], rows of bpp * out_w bytes)
+  bool k6 = false;
+  int out_bpp = 4, k6_maxpx = 1;
+  std::vector<EmitDesc> edesc;
+  EmitDesc* d_edesc = nullptr;
+  uint8_t* d_out = nullptr;
+  size_t out_bytes = 0;
+  std::vector<size_t> off_out;
+  // K5 (f3): an animation batch (wg_anim_batch_create) composites its canvases in wg_batch_run
+  bool anim = false;
+  int canvas_w = 0, canvas_h = 0;
+  std::vector<AnimFrameDesc> fdesc;
+  AnimFrameDesc* d_fdesc = nullptr;
+  uint8_t* d_canvases = nullptr;
+  std::vector<int32_t> timestamps;
 };
 
 namespace {
@@ -484,6 +501,10 @@ void wg_batch_destroy(wg_batch* b) {
   c.put(b->d_in);
   c.put(b->d_planes);
   c.put(b->d_rgba);
+  c.put(b->d_edesc);
+  c.put(b->d_out);
+  c.put(b->d_fdesc);
+  c.put(b->d_canvases);
   delete b;
 }
 
@@ -706,11 +727,30 @@ void batch_layout(wg_batch* b, wg::StagingArena& arena, int32_t* status) {
       k4 += 8.0 * px;
     }
   }
+  // K6: non-RGBA colorspace or flip -> one output window per frame in d_out (reads the RGBA
+  // window, writes bpp bytes per pixel)
+  double k6 = 0;
+  b->k6 = !(b->opt.colorspace == 1 && !b->opt.flip);
+  if (b->k6) {
+    b->out_bpp = wg::output_bpp(b->opt.colorspace);
+    b->off_out.assign((size_t)n, 0);
+    size_t ob = 0;
+    for (int i = 0; i < n; ++i) {
+      const FrameParse& f = b->fp[(size_t)i];
+      if (f.status != WG_STATUS_OK) continue;
+      b->off_out[(size_t)i] = ob;
+      ob = align_up(ob + (size_t)b->out_bpp * f.out_w * f.out_h);
+      b->k6_maxpx = std::max(b->k6_maxpx, f.out_w * f.out_h);
+      k6 += (4.0 + b->out_bpp) * f.out_w * (double)f.out_h;
+    }
+    b->out_bytes = std::max<size_t>(ob, kAlign);
+  }
   b->kbytes[0] = k1;
   b->kbytes[1] = k2;
   b->kbytes[2] = k3;
   b->kbytes[3] = k4;
   b->kbytes[4] = k7;
+  b->kbytes[5] = k6;
   b->plane_bytes = std::max<size_t>(pl_b, kAlign);
   b->rgba_bytes = std::max<size_t>(rg_b, kAlign);
 }
@@ -812,6 +852,22 @@ int batch_upload(wg_batch* b, const wg::StagingArena& arena) {
       d2.height = f.out_h;
     }
   }
+  // K6's descriptors: every valid frame's RGBA window -> its slot of d_out
+  if (b->k6) {
+    b->d_out = static_cast<uint8_t*>(cache.get(b->out_bytes));
+    b->d_edesc = static_cast<EmitDesc*>(cache.get(sizeof(EmitDesc) * (size_t)n));
+    if (!b->d_out || !b->d_edesc) return WG_STATUS_OUT_OF_MEMORY;
+    b->edesc.assign((size_t)n, EmitDesc{});
+    for (int i = 0; i < n; ++i) {
+      const FrameParse& f = b->fp[(size_t)i];
+      if (f.status != WG_STATUS_OK) continue;
+      const FrameDesc& d = b->desc[(size_t)i];
+      // the output window inside the RGBA (window_ptr: lossless crops are sub-rectangles)
+      const uint8_t* src = d.rgba + (size_t)f.win_y * d.rgba_stride + 4 * (size_t)f.win_x;
+      b->edesc[(size_t)i] = EmitDesc{src, b->d_out + b->off_out[(size_t)i], d.rgba_stride, b->out_bpp * f.out_w,
+                                     f.out_w, f.out_h, b->opt.colorspace, b->opt.flip ? 1 : 0, 1, 0};
+    }
+  }
   // the staged inputs: one copy per arena chunk, from pinned memory
   hipError_t e = hipSuccess;
   for (size_t c = 0; c < arena.n_chunks() && e == hipSuccess; ++c) {
@@ -840,6 +896,8 @@ int batch_upload(wg_batch* b, const wg::StagingArena& arena) {
   if (e == hipSuccess && !b->adesc.empty())
     e = hipMemcpyAsync(b->d_adesc, b->adesc.data(), sizeof(AlphaDesc) * b->adesc.size(), hipMemcpyHostToDevice,
                        home);
+  if (e == hipSuccess && b->k6)
+    e = hipMemcpyAsync(b->d_edesc, b->edesc.data(), sizeof(EmitDesc) * (size_t)n, hipMemcpyHostToDevice, home);
   if (e != hipSuccess) {
     (void)hipGetLastError();
     return WG_STATUS_OUT_OF_MEMORY;
@@ -892,6 +950,8 @@ int wg_batch_run(wg_batch* b, void* stream) {
   t.ran[kStageK2] = b->n_lossy > 0 && !b->fused;
   t.ran[kStageK7] = t.ran[kStageK3] = b->n_k3 > 0;
   t.ran[kStageK4] = b->n_alpha > 0;
+  t.ran[kStageK6] = b->k6 && b->n_valid > 0;
+  t.ran[kStageK5] = b->anim;
   hipEventRecord(t.ev[kStageK1], s);
   if (b->n_lossy > 0) {
     hipError_t e = wg::launch_vp8_recon_filter(b->d_desc, b->n, b->max_mb_w, b->n_lossy > b->n_wide,
@@ -938,6 +998,16 @@ int wg_batch_run(wg_batch* b, void* stream) {
   hipEventRecord(t.ev[kStageK4], s);
   if (b->n_alpha > 0) {  // after K2 (A = 255) and K3 (alpha streams)
     hipError_t e = wg::launch_alpha(b->d_adesc, b->n_alpha, s);
+    if (e != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
+  }
+  hipEventRecord(t.ev[kStageK6], s);
+  if (t.ran[kStageK6]) {  // the output colorspace / flip over every frame's final RGBA
+    hipError_t e = wg::launch_emit(b->d_edesc, b->n, b->k6_maxpx, s);
+    if (e != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
+  }
+  hipEventRecord(t.ev[kStageK5], s);
+  if (b->anim) {  // an animation's canvases from its decoded frames
+    hipError_t e = wg::launch_anim_compose(b->d_fdesc, b->n, b->d_canvases, b->canvas_w, b->canvas_h, s);
     if (e != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
   }
   hipEventRecord(t.ev[kStages], s);
@@ -1046,8 +1116,6 @@ const uint8_t* window_ptr(const wg_batch* b, int i) {
   const FrameDesc& d = b->desc[i];
   return d.rgba + (size_t)f.win_y * d.rgba_stride + 4 * (size_t)f.win_x;
 }
-// Every OK frame's RGBA window to out[i] (stride strides[i]): one wait for the batch, the
-// copies queued on the context stream, one wait for them.
 // Bytes a row-major output of h rows of `row` bytes at `stride` needs (0 rows: nothing).
 size_t out_bytes_needed(int stride, int row, int h) {
   return h > 0 ? (size_t)stride * (size_t)(h - 1) + (size_t)row : 0;
@@ -1058,6 +1126,8 @@ bool out_ok(uint8_t* const* out, const int32_t* strides, const size_t* caps, int
   return out[i] != nullptr && strides[i] >= row && caps[i] >= out_bytes_needed(strides[i], row, h);
 }
 
+// Every OK frame's RGBA window to out[i] (stride strides[i]): one wait for the batch, the
+// copies queued on the context stream, one wait for them.
 int download_rgba_all(wg_batch* b, uint8_t* const* out, const int32_t* strides, const size_t* caps, int32_t* status) {
   int st = batch_sync(b);
   if (st != WG_STATUS_OK) return st;
@@ -1394,29 +1464,13 @@ int wg_batch_download(wg_batch* b, int i, uint8_t* out, int stride) {
   const FrameParse& f = b->fp[i];
   const int bpp = wg::output_bpp(b->opt.colorspace);
   if (stride < bpp * f.out_w) return WG_STATUS_INVALID_PARAM;
-  if (b->opt.colorspace == 1 && !b->opt.flip) return wg_batch_download_rgba(b, i, out, stride);
+  if (!b->k6) return wg_batch_download_rgba(b, i, out, stride);
   int st = batch_sync(b);
   if (st != WG_STATUS_OK) return st;
-  // K6 into a device staging buffer, then one 2D copy
+  // K6 ran in wg_batch_run: one 2D copy of the frame's slot of d_out
   const size_t row = (size_t)bpp * f.out_w;
-  uint8_t* d_out = nullptr;
-  wg::EmitDesc* d_ed = nullptr;
-  wg::EmitDesc ed{window_ptr(b, i), nullptr, b->desc[i].rgba_stride, (int32_t)row, f.out_w, f.out_h,
-                  b->opt.colorspace, b->opt.flip ? 1 : 0, 1, 0};
-  DeviceCache& cache = b->ctx->cache;
-  d_out = static_cast<uint8_t*>(cache.get(row * f.out_h));
-  d_ed = static_cast<wg::EmitDesc*>(cache.get(sizeof(ed)));
-  hipError_t e = d_out && d_ed ? hipSuccess : hipErrorOutOfMemory;
-  if (e == hipSuccess) {
-    ed.dst = d_out;
-    e = hipMemcpyAsync(d_ed, &ed, sizeof(ed), hipMemcpyHostToDevice, b->home);
-  }
-  if (e == hipSuccess) e = wg::launch_emit(d_ed, 1, f.out_w * f.out_h, b->home);
-  if (e == hipSuccess) e = hipMemcpy2DAsync(out, stride, d_out, row, row, f.out_h, hipMemcpyDeviceToHost, b->home);
-  const hipError_t se = hipStreamSynchronize(b->home);  // before the buffers go back
-  if (e == hipSuccess) e = se;
-  cache.put(d_out);
-  cache.put(d_ed);
+  const hipError_t e =
+      hipMemcpy2D(out, stride, b->d_out + b->off_out[(size_t)i], row, row, f.out_h, hipMemcpyDefault);
   return e == hipSuccess ? WG_STATUS_OK : WG_STATUS_USER_ABORT;
 }
 
@@ -1500,35 +1554,8 @@ int wg_decode_batch(wg_ctx* ctx, const uint8_t* const* data, const size_t* sizes
   if (!b) return WG_STATUS_OUT_OF_MEMORY;
   int st = wg_batch_run(b, nullptr);
   const int bpp = wg::output_bpp(opt->colorspace);
-  if (st == WG_STATUS_OK && !(opt->colorspace == 1 && !opt->flip)) {
-    // K6 over every frame in one launch into one staging buffer
-    std::vector<wg::EmitDesc> ed((size_t)n, wg::EmitDesc{});
-    std::vector<size_t> offs((size_t)n, 0);
-    size_t total = 0;
-    int maxpx = 1;
-    for (int i = 0; i < n; ++i) {
-      const FrameParse& f = b->fp[i];
-      if (f.status != WG_STATUS_OK) continue;
-      offs[(size_t)i] = total;
-      total = align_up(total + (size_t)bpp * f.out_w * f.out_h);
-      maxpx = std::max(maxpx, f.out_w * f.out_h);
-    }
-    uint8_t* d_out = nullptr;
-    wg::EmitDesc* d_ed = nullptr;
-    d_out = static_cast<uint8_t*>(ctx->cache.get(std::max<size_t>(total, kAlign)));
-    d_ed = static_cast<wg::EmitDesc*>(ctx->cache.get(sizeof(wg::EmitDesc) * (size_t)n));
-    hipError_t e = d_out && d_ed ? hipSuccess : hipErrorOutOfMemory;
-    for (int i = 0; e == hipSuccess && i < n; ++i) {
-      const FrameParse& f = b->fp[i];
-      if (f.status != WG_STATUS_OK) continue;
-      ed[(size_t)i] = wg::EmitDesc{window_ptr(b, i), d_out + offs[(size_t)i], b->desc[i].rgba_stride,
-                                   bpp * f.out_w, f.out_w, f.out_h, opt->colorspace, opt->flip ? 1 : 0, 1, 0};
-    }
-    if (e == hipSuccess)
-      e = hipMemcpyAsync(d_ed, ed.data(), sizeof(wg::EmitDesc) * (size_t)n, hipMemcpyHostToDevice, ctx->stream);
-    if (e == hipSuccess) e = wg::launch_emit(d_ed, n, maxpx, ctx->stream);
-    if (e == hipSuccess) st = batch_sync(b);
-    else st = WG_STATUS_USER_ABORT;
+  if (st == WG_STATUS_OK && b->k6) {  // K6 ran as the batch's last stage: copy each frame's slot out
+    st = batch_sync(b);
     for (int i = 0; st == WG_STATUS_OK && i < n; ++i) {
       const FrameParse& f = b->fp[i];
       if (status[i] != WG_STATUS_OK) continue;
@@ -1537,13 +1564,10 @@ int wg_decode_batch(wg_ctx* ctx, const uint8_t* const* data, const size_t* sizes
         continue;
       }
       const size_t row = (size_t)bpp * f.out_w;
-      if (hipMemcpy2D(out[i], strides[i], d_out + offs[(size_t)i], row, row, f.out_h, hipMemcpyDeviceToHost) !=
+      if (hipMemcpy2D(out[i], strides[i], b->d_out + b->off_out[(size_t)i], row, row, f.out_h, hipMemcpyDefault) !=
           hipSuccess)
         status[i] = WG_STATUS_USER_ABORT;
     }
-    hipStreamSynchronize(ctx->stream);  // (an error path may have left K6 queued)
-    ctx->cache.put(d_out);
-    ctx->cache.put(d_ed);
   } else if (st == WG_STATUS_OK) {
     st = download_rgba_all(b, out, strides, caps, status);
   }
@@ -1625,43 +1649,55 @@ int wg_anim_demux(const uint8_t* data, size_t size, wg_anim_info* info, wg_anim_
   return WG_STATUS_OK;
 }
 
-int wg_anim_decode(wg_ctx* ctx, const uint8_t* data, size_t size, uint8_t* canvases, int32_t* timestamps,
-                   int32_t flags) {
-  if (!ctx || !data || !canvases || !timestamps) return WG_STATUS_INVALID_PARAM;
+wg_batch* wg_anim_batch_create(wg_ctx* ctx, const uint8_t* data, size_t size, int32_t flags, int32_t* status) {
+  int32_t st_local = WG_STATUS_OK;
+  int32_t& st_out = status ? *status : st_local;
+  st_out = WG_STATUS_OK;
+  if (!ctx || !data) {
+    st_out = WG_STATUS_INVALID_PARAM;
+    return nullptr;
+  }
   wg::AnimInfo ai;
   std::vector<wg::AnimFrame> fr;
-  int st = wg::anim_demux(data, size, &ai, &fr);
-  if (st != WG_STATUS_OK) return st;
+  int st = guarded([&] { return wg::anim_demux(data, size, &ai, &fr); });
+  if (st == WG_STATUS_OK && ai.frame_count <= 0) st = WG_STATUS_BITSTREAM_ERROR;
+  if (st != WG_STATUS_OK) {
+    st_out = st;
+    return nullptr;
+  }
   const int n = ai.frame_count;
   // every frame's fragment decodes as one batch (K1..K4)
   std::vector<const uint8_t*> ptrs((size_t)n);
   std::vector<size_t> sizes((size_t)n);
-  std::vector<int32_t> status((size_t)n, 0);
+  std::vector<int32_t> fst((size_t)n, 0);
   for (int i = 0; i < n; ++i) {
     ptrs[(size_t)i] = data + fr[(size_t)i].off;
     sizes[(size_t)i] = fr[(size_t)i].size;
   }
-  wg_batch* b = wg_batch_create(ctx, ptrs.data(), sizes.data(), n, flags, status.data());
+  wg_batch* b = wg_batch_create(ctx, ptrs.data(), sizes.data(), n, flags, fst.data());
   if (!b) {
-    for (int i = 0; i < n; ++i)
-      if (status[(size_t)i] != WG_STATUS_OK) return status[(size_t)i];
-    return WG_STATUS_OUT_OF_MEMORY;
+    st_out = WG_STATUS_OUT_OF_MEMORY;
+    for (int i = n - 1; i >= 0; --i)
+      if (fst[(size_t)i] != WG_STATUS_OK) st_out = fst[(size_t)i];
+    return nullptr;
   }
   for (int i = 0; i < n; ++i) {
-    if (status[(size_t)i] != WG_STATUS_OK) {
+    st = fst[(size_t)i];
+    if (st == WG_STATUS_OK &&
+        (b->desc[(size_t)i].width != fr[(size_t)i].width || b->desc[(size_t)i].height != fr[(size_t)i].height))
+      st = WG_STATUS_BITSTREAM_ERROR;
+    if (st != WG_STATUS_OK) {  // WebPAnimDecoder stops at the first frame that fails
       wg_batch_destroy(b);
-      return status[(size_t)i];
-    }
-    if (b->desc[(size_t)i].width != fr[(size_t)i].width || b->desc[(size_t)i].height != fr[(size_t)i].height) {
-      wg_batch_destroy(b);
-      return WG_STATUS_BITSTREAM_ERROR;
+      st_out = st;
+      return nullptr;
     }
   }
-  st = wg_batch_run(b, nullptr);
   // frame descriptors: IsKeyFrame (anim_decode.go:183-197) and the blend / dispose flags
-  std::vector<AnimFrameDesc> fd((size_t)n);
+  b->fdesc.assign((size_t)n, AnimFrameDesc{});
+  b->timestamps.assign((size_t)n, 0);
   int32_t t = 0;
   bool prev_key = false;
+  double k5 = 0;
   auto full = [&](const wg::AnimFrame& f) { return f.width == ai.canvas_width && f.height == ai.canvas_height; };
   for (int i = 0; i < n; ++i) {
     const wg::AnimFrame& f = fr[(size_t)i];
@@ -1669,7 +1705,7 @@ int wg_anim_decode(wg_ctx* ctx, const uint8_t* data, size_t size, uint8_t* canva
     if (i == 0) key = true;
     else if ((!f.has_alpha || f.no_blend) && full(f)) key = true;
     else key = fr[(size_t)i - 1].dispose_bg && (full(fr[(size_t)i - 1]) || prev_key);
-    AnimFrameDesc& d = fd[(size_t)i];
+    AnimFrameDesc& d = b->fdesc[(size_t)i];
     d.rgba = b->desc[(size_t)i].rgba;
     d.x = f.x_offset;
     d.y = f.y_offset;
@@ -1688,34 +1724,68 @@ int wg_anim_decode(wg_ctx* ctx, const uint8_t* data, size_t size, uint8_t* canva
     }
     prev_key = key;
     t += f.duration;
-    timestamps[i] = t;
+    b->timestamps[(size_t)i] = t;
+    // K5's algorithmic bytes: the canvas written + the frame's rectangle read
+    k5 += 4.0 * ai.canvas_width * (double)ai.canvas_height + 4.0 * f.width * (double)f.height;
   }
+  b->canvas_w = ai.canvas_width;
+  b->canvas_h = ai.canvas_height;
+  b->kbytes[6] = k5;
   const size_t canvas_bytes = (size_t)ai.canvas_width * ai.canvas_height * 4;
-  AnimFrameDesc* d_fd = nullptr;
-  uint8_t* d_canvases = nullptr;
   {
     std::lock_guard<std::mutex> lock(ctx->mu);
-    if (st == WG_STATUS_OK && !set_device(ctx->device)) st = WG_STATUS_INVALID_PARAM;
-    hipError_t e = st == WG_STATUS_OK ? hipSuccess : hipErrorUnknown;
+    hipError_t e = set_device(ctx->device) ? hipSuccess : hipErrorInvalidDevice;
     if (e == hipSuccess) {
-      d_fd = static_cast<AnimFrameDesc*>(ctx->cache.get(sizeof(AnimFrameDesc) * (size_t)n));
-      d_canvases = static_cast<uint8_t*>(ctx->cache.get(canvas_bytes * (size_t)n));
-      if (!d_fd || !d_canvases) e = hipErrorOutOfMemory;
+      b->d_fdesc = static_cast<AnimFrameDesc*>(ctx->cache.get(sizeof(AnimFrameDesc) * (size_t)n));
+      b->d_canvases = static_cast<uint8_t*>(ctx->cache.get(canvas_bytes * (size_t)n));
+      if (!b->d_fdesc || !b->d_canvases) e = hipErrorOutOfMemory;
     }
     if (e == hipSuccess)
-      e = hipMemcpyAsync(d_fd, fd.data(), sizeof(AnimFrameDesc) * (size_t)n, hipMemcpyHostToDevice, ctx->stream);
-    if (e == hipSuccess)
-      e = wg::launch_anim_compose(d_fd, n, d_canvases, ai.canvas_width, ai.canvas_height, ctx->stream);
-    if (e == hipSuccess)
-      e = hipMemcpyAsync(canvases, d_canvases, canvas_bytes * (size_t)n, hipMemcpyDeviceToHost, ctx->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
-    int err = 0;
-    if (e == hipSuccess) e = hipMemcpy(&err, b->d_err, sizeof(int), hipMemcpyDeviceToHost);
-    if (st == WG_STATUS_OK && (e != hipSuccess || err)) st = WG_STATUS_USER_ABORT;
-    hipStreamSynchronize(ctx->stream);
-    ctx->cache.put(d_fd);
-    ctx->cache.put(d_canvases);
+      e = hipMemcpyAsync(b->d_fdesc, b->fdesc.data(), sizeof(AnimFrameDesc) * (size_t)n, hipMemcpyHostToDevice,
+                         b->home);
+    if (e == hipSuccess) e = hipStreamSynchronize(b->home);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      wg_batch_destroy(b);
+      st_out = e == hipErrorInvalidDevice ? WG_STATUS_INVALID_PARAM : WG_STATUS_OUT_OF_MEMORY;
+      return nullptr;
+    }
   }
+  b->anim = true;
+  return b;
+}
+
+int wg_anim_batch_info(const wg_batch* b, int32_t* canvas_width, int32_t* canvas_height, int32_t* frames) {
+  if (!b || !b->anim) return WG_STATUS_INVALID_PARAM;
+  if (canvas_width) *canvas_width = b->canvas_w;
+  if (canvas_height) *canvas_height = b->canvas_h;
+  if (frames) *frames = b->n;
+  return WG_STATUS_OK;
+}
+
+int wg_anim_batch_download(wg_batch* b, uint8_t* canvases, size_t cap, int32_t* timestamps) {
+  if (!b || !b->anim || !canvases) return WG_STATUS_INVALID_PARAM;
+  const size_t bytes = (size_t)b->canvas_w * b->canvas_h * 4 * (size_t)b->n;
+  if (cap < bytes) return WG_STATUS_INVALID_PARAM;
+  const int st = batch_sync(b);
+  if (st != WG_STATUS_OK) return st;
+  if (hipMemcpy(canvases, b->d_canvases, bytes, hipMemcpyDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    return WG_STATUS_USER_ABORT;
+  }
+  if (timestamps) std::memcpy(timestamps, b->timestamps.data(), sizeof(int32_t) * (size_t)b->n);
+  return WG_STATUS_OK;
+}
+
+int wg_anim_decode(wg_ctx* ctx, const uint8_t* data, size_t size, uint8_t* canvases, int32_t* timestamps,
+                   int32_t flags) {
+  if (!ctx || !data || !canvases || !timestamps) return WG_STATUS_INVALID_PARAM;
+  int32_t st = WG_STATUS_OK;
+  wg_batch* b = wg_anim_batch_create(ctx, data, size, flags, &st);
+  if (!b) return st;
+  st = wg_batch_run(b, nullptr);
+  if (st == WG_STATUS_OK)
+    st = wg_anim_batch_download(b, canvases, (size_t)b->canvas_w * b->canvas_h * 4 * (size_t)b->n, timestamps);
   wg_batch_destroy(b);
   return st;
 }

@@ -215,6 +215,9 @@ _SIGS = {
     "wg_ctx_pipeline_stats": (C.c_int, [_P, _P]),
     "wg_host_alloc": (_P, [C.c_size_t]),
     "wg_host_free": (None, [_P]),
+    "wg_anim_batch_create": (_P, [_P, _P, C.c_size_t, C.c_int32, _P]),
+    "wg_anim_batch_info": (C.c_int, [_P, _P, _P, _P]),
+    "wg_anim_batch_download": (C.c_int, [_P, _P, C.c_size_t, _P]),
 }
 EXPORTED = tuple(_SIGS)
 
@@ -411,13 +414,19 @@ def _ptr_arrays(datas):
 class Batch:
     """Device-resident batch: host parse + H2D once, then run() the device path many times."""
 
-    def __init__(self, ctx, datas, flags=0):
+    def __init__(self, ctx, datas, flags=0, opts=None):
+        """opts: DecoderOptions (wg_batch_create_ex: colorspace, crop, flip; a non-RGBA colorspace or
+        flip adds K6 to every run) instead of flags."""
         self._ctx = ctx  # keep the context alive while the batch exists
         self._h = None
         self._bufs, ptrs, sizes = _ptr_arrays(datas)
         n = len(self._bufs)
         self.status = np.zeros(n, np.int32)
-        self._h = lib().wg_batch_create(ctx._h, ptrs, sizes, n, flags, self.status.ctypes.data)
+        self.opts = opts
+        if opts is not None:
+            self._h = lib().wg_batch_create_ex(ctx._h, ptrs, sizes, n, C.byref(opts), self.status.ctypes.data)
+        else:
+            self._h = lib().wg_batch_create(ctx._h, ptrs, sizes, n, flags, self.status.ctypes.data)
         if not self._h:
             raise WebPError(int(self.status.max() or Status.OUT_OF_MEMORY), "wg_batch_create")
         self.n = n
@@ -443,17 +452,17 @@ class Batch:
             raise WebPError(st, "wg_batch_run_emit")
 
     def kernel_ms(self):
-        """(K1, K2, K3, K4, K7) per-launch ms averaged over the runs since the last call."""
-        ms = (C.c_float * 5)()
-        st = lib().wg_batch_kernel_ms(self._h, ms, 5)
+        """(K1, K2, K3, K4, K7, K6, K5) per-launch ms averaged over the runs since the last call."""
+        ms = (C.c_float * 7)()
+        st = lib().wg_batch_kernel_ms(self._h, ms, 7)
         if st != Status.OK:
             raise WebPError(st, "wg_batch_kernel_ms")
         return tuple(float(v) for v in ms)
 
     def kernel_bytes(self):
-        """Algorithmic HBM bytes per launch of (K1, K2, K3, K4, K7)."""
-        b = (C.c_double * 5)()
-        lib().wg_batch_kernel_bytes(self._h, b, 5)
+        """Algorithmic HBM bytes per launch of (K1, K2, K3, K4, K7, K6, K5)."""
+        b = (C.c_double * 7)()
+        lib().wg_batch_kernel_bytes(self._h, b, 7)
         return tuple(float(v) for v in b)
 
     @property
@@ -473,6 +482,16 @@ class Batch:
         st = lib().wg_batch_download_rgba(self._h, i, out.ctypes.data, 4 * w)
         if st != Status.OK:
             raise WebPError(st, "wg_batch_download_rgba")
+        return out
+
+    def download(self, i):
+        """Frame i in the batch's output colorspace: (h, w * bpp) uint8 rows (wg_batch_download)."""
+        w, h = self.dims(i)
+        bpp = output_bpp(self.opts.colorspace) if self.opts is not None else 4
+        out = np.empty((h, w * bpp), np.uint8)
+        st = lib().wg_batch_download(self._h, i, out.ctypes.data, w * bpp)
+        if st != Status.OK:
+            raise WebPError(st, "wg_batch_download")
         return out
 
     def yuv(self, i):
@@ -498,6 +517,36 @@ class Batch:
             pass
 
 
+class AnimBatch(Batch):
+    """An animation resident in HBM (wg_anim_batch_create): run() decodes every frame (K1..K4) and
+    composites every canvas (K5); canvases() downloads them with the end timestamps."""
+
+    def __init__(self, ctx, data, flags=0):
+        self._ctx = ctx
+        self._h = None
+        self._bufs = [_buf(data)]
+        st = C.c_int32(0)
+        self._h = lib().wg_anim_batch_create(ctx._h, self._bufs[0], len(self._bufs[0]), flags, C.byref(st))
+        if not self._h:
+            raise WebPError(st.value or Status.OUT_OF_MEMORY, "wg_anim_batch_create")
+        w, h, n = C.c_int32(), C.c_int32(), C.c_int32()
+        lib().wg_anim_batch_info(self._h, C.byref(w), C.byref(h), C.byref(n))
+        self.canvas_width, self.canvas_height, self.n = w.value, h.value, n.value
+        self.status = np.zeros(self.n, np.int32)
+        self.opts = None
+        self.flags = flags
+        ctx._batches.add(self)
+
+    def canvases(self):
+        """((frames, H, W, 4) uint8 canvases of the last run, (frames,) int32 end timestamps in ms)."""
+        canv = np.empty((self.n, self.canvas_height, self.canvas_width, 4), np.uint8)
+        ts = np.empty(self.n, np.int32)
+        st = lib().wg_anim_batch_download(self._h, canv.ctypes.data, canv.nbytes, ts.ctypes.data)
+        if st != Status.OK:
+            raise WebPError(st, "wg_anim_batch_download")
+        return canv, ts
+
+
 class Context:
     """One decode context per HIP device (wg_ctx)."""
 
@@ -508,8 +557,11 @@ class Context:
             raise WebPError(Status.UNSUPPORTED_FEATURE, f"wg_ctx_create(device={device}) (no GPU?)")
         self.device = device
 
-    def batch(self, datas, flags=0):
-        return Batch(self, datas, flags)
+    def batch(self, datas, flags=0, opts=None):
+        return Batch(self, datas, flags, opts)
+
+    def anim_batch(self, data, flags=0):
+        return AnimBatch(self, data, flags)
 
     def decode_batch_opts(self, datas, opts):
         """wg_decode_batch: frames -> ([(h, w * bpp) uint8 rows or None], status)."""

@@ -192,7 +192,8 @@ void wg_batch_destroy(wg_batch* b);
 
 /* Run the device DSP path for the whole batch on `stream` (NULL = ctx stream):
  * lossy frames: K1 reconstruct+deblock wavefront (+ YUV420->RGBA in its tail, or K2), K4 ALPH plane -> A;
- * lossless frames (and lossless ALPH streams): K3 inverse transforms + RGBA.  Kernel durations of the last run
+ * lossless frames (and lossless ALPH streams): K3 inverse transforms + RGBA; then K6 (non-RGBA
+ * colorspace or flip) and K5 (animation batches).  Kernel durations of the last run
  * (HIP events on that stream) are available from wg_batch_kernel_ms(). */
 int wg_batch_run(wg_batch* b, void* stream);
 
@@ -212,12 +213,14 @@ int wg_batch_run_emit(wg_batch* b, void* stream);
 /* Per-launch kernel durations averaged over the runs since the last query:
  * ms[0] = VP8 reconstruct+filter (K1, with its RGBA tail by default), ms[1] = YUV->RGBA (K2), ms[2] = VP8L inverse
  * transforms (K3, lossless frames and lossless ALPH streams), ms[3] = ALPH unfilter + A
- * channel (K4), ms[4] = VP8L color cache + back-references (K7, before K3); a kernel with no
- * frames in the batch reports 0.  n_ms >= 1 (entries beyond n_ms are not written). */
+ * channel (K4), ms[4] = VP8L color cache + back-references (K7, before K3), ms[5] = output
+ * colorspace / flip (K6, batches created with a non-RGBA colorspace or flip), ms[6] = animation
+ * canvases (K5, wg_anim_batch_create); a kernel with no frames in the batch reports 0.
+ * n_ms >= 1 (entries beyond n_ms are not written). */
 int wg_batch_kernel_ms(const wg_batch* b, float* ms, int n_ms);
 
-/* Algorithmic HBM bytes per launch of K1, K2, K3, K4, K7; K1 with
- * its RGBA tail: records + coefficients in, RGBA out (the planes are an intermediate). */
+/* Algorithmic HBM bytes per launch of K1, K2, K3, K4, K7, K6, K5;
+ * K1 with its RGBA tail: records + coefficients in, RGBA out (the planes are an intermediate). */
 int wg_batch_kernel_bytes(const wg_batch* b, double* bytes, int n_bytes);
 
 int wg_batch_size(const wg_batch* b);
@@ -366,6 +369,17 @@ int wg_anim_demux(const uint8_t* data, size_t size, wg_anim_info* info, wg_anim_
  * as one batch (K1..K4), then K5 composites.  Returns the first failing frame's status. */
 int wg_anim_decode(wg_ctx* ctx, const uint8_t* data, size_t size, uint8_t* canvases, int32_t* timestamps,
                    int32_t flags);
+
+/* The same animation decode kept resident in HBM (benchmarks, tests): the frames' inputs
+ * parsed and uploaded once, then every wg_batch_run() runs K1..K4 over the frames and K5 over
+ * the canvases (its time is wg_batch_kernel_ms' seventh entry).  NULL on failure, *status says
+ * why (the first failing frame's status, as WebPAnimDecoderGetNext stops there). */
+wg_batch* wg_anim_batch_create(wg_ctx* ctx, const uint8_t* data, size_t size, int32_t flags, int32_t* status);
+/* canvas size and frame count of an animation batch */
+int wg_anim_batch_info(const wg_batch* b, int32_t* canvas_width, int32_t* canvas_height, int32_t* frames);
+/* every canvas of the last run (frames * canvas_height * canvas_width * 4 bytes; cap checked)
+ * and the frames' end timestamps (ms) */
+int wg_anim_batch_download(wg_batch* b, uint8_t* canvases, size_t cap, int32_t* timestamps);
 
 #ifdef __cplusplus
 }  /* extern "C" */

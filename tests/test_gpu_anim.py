@@ -42,3 +42,23 @@ def test_animated_file_through_still_api_is_unsupported(ctx):
     assert status[0] == webp_amd.Status.UNSUPPORTED_FEATURE
     w, h, _ = webp_amd.decode_config(data)
     assert (w, h) == (96, 80)
+
+
+@pytest.mark.parametrize("name", anim_names())
+def test_resident_anim_batch(ctx, name):
+    """wg_anim_batch_create: the animation resident in HBM, every run decoding the frames and
+    compositing the canvases (K5 as the batch's last stage, its own kernel_ms entry): the
+    canvases of repeated runs equal WebPAnimDecoder's."""
+    data, gold = load_anim(name)
+    b = ctx.anim_batch(data)
+    try:
+        assert (b.n, b.canvas_height, b.canvas_width) == gold["canvases"].shape[:3]
+        for _ in range(2):
+            b.run()
+            canv, ts = b.canvases()
+            np.testing.assert_array_equal(canv, gold["canvases"])
+            np.testing.assert_array_equal(ts, gold["timestamps"])
+        assert b.kernel_ms()[6] > 0
+        assert b.kernel_bytes()[6] >= 4.0 * canv.size // 4
+    finally:
+        b.close()

@@ -78,3 +78,28 @@ def test_cropped_batch_keeps_separate_emit(ctx):
     finally:
         L.wg_batch_destroy(h)
     assert L.wg_batch_set_emit(None, 0) == webp_amd.Status.INVALID_PARAM
+
+
+@pytest.mark.parametrize("key", ["m0_none_f1_nf0", "m7_none_f0_nf0", "m4_none_f0_nf1", "m1_none_f1_nf0"])
+def test_resident_batch_runs_k6_as_a_stage(ctx, key):
+    """A batch created with an output colorspace (or flip) runs K6 as the last stage of every
+    wg_batch_run (its own kernel_ms entry); downloads copy its output: equal to WebPDecode's
+    bytes after repeated runs (RGB flipped, rgbA premultiplied, RGB565 point-sampled, RGBA
+    flipped)."""
+    mode, cname, flip, nf = parse_mode_key(key)
+    srcs = [load_modes(s) for s in mode_sources()]
+    sub = [(d, g) for d, g, e in srcs if e["status"].get(key) == 0 and key in g]
+    assert len(sub) >= 3
+    b = ctx.batch([d for d, _ in sub], opts=webp_amd.options(mode, None, flip, nf))
+    try:
+        for _ in range(2):
+            b.run()
+        ms = b.kernel_ms()
+        assert ms[5] > 0, ms
+        by = b.kernel_bytes()
+        bpp = webp_amd.output_bpp(mode)
+        assert by[5] == sum((4 + bpp) * g[key].shape[0] * g[key].shape[1] // bpp for _, g in sub)
+        for i, (_, g) in enumerate(sub):
+            np.testing.assert_array_equal(b.download(i), g[key], err_msg=f"{key} frame {i}")
+    finally:
+        b.close()
