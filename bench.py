@@ -42,6 +42,15 @@ WORKLOADS = {
                      "batch 256"),
     "c5": dict(prefix="c5_ll2048", name="c5_ll2048_x256",
                desc="2048x2048 VP8L lossless (predictor + cross-color + subtract-green + color cache), batch 256"),
+    # SURVEY §8's "next" rows, each measured with its kernel's roofline (`roofline_target`)
+    "c3a": dict(prefix="c3a_4k", name="c3a_4k_alpha_x256", target="alpha_kernel",
+                desc="3840x2160 VP8-lossy + ALPH (lossless-compressed feathered cut-out alpha), deblock on, batch 256: "
+                     "K1 + the alpha streams' K7 / K3 + K4 (SURVEY 8 f2)"),
+    "c3rgb565": dict(prefix="c3_4k", name="c3_4k_rgb565_x256", target="emit_kernel", colorspace=4,
+                     desc="C3's frames decoded to MODE_RGB_565 (fancy upsampling), batch 256: K1 + K6 (SURVEY 8 f4)"),
+    "anim": dict(prefix="anim_1080p_x64", name="anim_1080p_x64", target="anim_compose_kernel", kind="anim",
+                 desc="one 64-frame 1920x1080 lossy animation per GPU (WebPAnimEncoder: blended sub-rectangles), "
+                      "resident: frames K1..K4, 64 canvases K5; value = canvas pixels / s (SURVEY 8 f3)"),
 }
 # the order of Batch.kernel_ms() / kernel_bytes(): K1, K2, K3, K4, K7, K6, K5
 KERNELS = ("vp8_recon_filter_kernel", "yuv_to_rgba_kernel", "vp8l_transforms_kernel", "alpha_kernel",
@@ -49,7 +58,12 @@ KERNELS = ("vp8_recon_filter_kernel", "yuv_to_rgba_kernel", "vp8l_transforms_ker
 
 
 def _load_frames(prefix):
-    from oracle_lib import bench_files, manifest
+    from oracle_lib import GOLDEN, bench_files, manifest
+    ent = manifest().get("bench_anim", {}).get(prefix)
+    if ent is not None:  # one animation file: bits per canvas pixel
+        data = open(os.path.join(GOLDEN, "bench", prefix + ".webp"), "rb").read()
+        inf = ent["info"]
+        return [data], 8.0 * len(data) / (inf["canvas_width"] * inf["canvas_height"] * inf["frame_count"])
     paths = bench_files(prefix)
     datas = [open(p, "rb").read() for p in paths]
     m = manifest()["bench"]
@@ -162,10 +176,23 @@ def spawn_ranks(n, argv, timeout=None):
 
 
 # ------------------------------------------------------------------------------- CPU legs
-def _cpu_decode_one(d):
-    """One frame through the CPU path (host entropy stage + oracle); returns its pixels."""
+def _cpu_decode_one(d, wl=None):
+    """One frame (an animation: all its canvases) through the CPU path (host entropy stage +
+    oracle) as the workload `wl` needs it; returns its pixels."""
     import webp_amd
-    from oracle_lib import oracle_decode, oracle_vp8l_decode
+    from oracle_lib import oracle_anim, oracle_decode, oracle_output, oracle_still_rgba, oracle_vp8l_decode
+    wl = wl or {}
+    if wl.get("kind") == "anim":
+        canv, _ = oracle_anim(d)
+        return canv.shape[0] * canv.shape[1] * canv.shape[2]
+    if wl.get("colorspace") is not None:
+        out = oracle_output(d, mode=wl["colorspace"])
+        f = webp_amd.features(d)
+        assert out is not None
+        return f.width * f.height
+    if wl.get("target") == "alpha_kernel":
+        rgba = oracle_still_rgba(d)
+        return rgba.shape[0] * rgba.shape[1]
     if webp_amd.features(d).format == 2:
         info, coded, tdata = webp_amd.vp8l_parse(d)
         oracle_vp8l_decode(info, coded, tdata)
@@ -175,13 +202,14 @@ def _cpu_decode_one(d):
     return info.width * info.height
 
 
-def cpu_baseline(datas, seconds):
+def cpu_baseline(datas, seconds, wl=None):
     """CPU oracle (C restatement, 1 thread): host entropy stage + reconstruct + filter +
-    fancy RGBA, frames decoded serially until `seconds` elapse."""
+    fancy RGBA (+ the workload's alpha / colorspace / compositing), frames decoded serially
+    until `seconds` elapse."""
     pix, n, t0 = 0, 0, time.perf_counter()
     while True:
         d = datas[n % len(datas)]
-        pix += _cpu_decode_one(d)
+        pix += _cpu_decode_one(d, wl)
         n += 1
         el = time.perf_counter() - t0
         if el >= seconds:
@@ -220,7 +248,7 @@ def cpu_baseline_dsp(datas, seconds):
                        f"(reconstruct + filter + RGBA, or the VP8L inverse transforms) on 1 host core, {el:.1f}s")
 
 
-def cpu_baseline_parallel(datas, seconds, threads):
+def cpu_baseline_parallel(datas, seconds, threads, wl=None):
     """The same CPU path on `threads` host threads, frames decoded concurrently (ctypes
     releases the GIL inside the entropy stage and the oracle)."""
     import threading
@@ -228,7 +256,7 @@ def cpu_baseline_parallel(datas, seconds, threads):
     from oracle_lib import oracle
     oracle()
     webp_amd.lib()
-    _cpu_decode_one(datas[0])
+    _cpu_decode_one(datas[0], wl)
     pix = [0] * threads
     cnt = [0] * threads
     t0 = time.perf_counter()
@@ -237,7 +265,7 @@ def cpu_baseline_parallel(datas, seconds, threads):
     def work(t):
         n = t
         while time.perf_counter() < stop:
-            pix[t] += _cpu_decode_one(datas[n % len(datas)])
+            pix[t] += _cpu_decode_one(datas[n % len(datas)], wl)
             cnt[t] += 1
             n += threads
 
@@ -501,16 +529,22 @@ def main():
         oversubscribed = world > ndev
         torch.cuda.set_device(device)
         datas, bpp = _load_frames(wl["prefix"])
-        frames = shard_frames(datas, rank, args.batch)
         ctx_threads = rank_host_threads(args.host_threads, world)
         ctx = webp_amd.Context(device, host_threads=ctx_threads)
         t_prep = time.perf_counter()
-        b = ctx.batch(frames)
+        if wl.get("kind") == "anim":  # one animation per rank, resident (frames + canvases)
+            frames = None
+            b = ctx.anim_batch(datas[rank % len(datas)])
+        else:
+            frames = shard_frames(datas, rank, args.batch)
+            opts = webp_amd.options(wl["colorspace"]) if wl.get("colorspace") is not None else None
+            b = ctx.batch(frames, opts=opts)
         t_prep = time.perf_counter() - t_prep
         if not (b.status == 0).all():
             raise SystemExit(f"rank {rank}: frames failed to parse: {b.status}")
         stream = torch.cuda.current_stream().cuda_stream
-        b.set_emit(args.emit == "separate")
+        if wl.get("kind") != "anim":
+            b.set_emit(args.emit == "separate")
         sync = torch.cuda.synchronize
 
     for _ in range(args.warmup):
@@ -539,10 +573,12 @@ def main():
         for _ in range(args.steps):
             b.run_emit(stream)
         stage_ms = b.kernel_ms()[1]
-    px_rank = b.pixels
+    # pixels per step: decoded frame pixels (an animation: every canvas it composites)
+    px_rank = b.pixels if wl.get("kind") != "anim" or args.mock else b.n * b.canvas_width * b.canvas_height
     dt, total_px = reduce_job(dist, "cpu", dt, px_rank * args.steps)
     e2e = None
-    if not args.no_e2e:
+    # the end-to-end leg (host in, host out through wg_decode_rgba_batch) exists for RGBA stills
+    if not args.no_e2e and wl.get("kind") != "anim" and wl.get("colorspace") is None:
         e2e = end_to_end(args, ctx, b, frames if not args.mock else None, dist, barrier, px_rank, ctx_threads)
     value = total_px / dt / 1e6
     ranks = [(rank, local, os.getpid())]
@@ -551,6 +587,7 @@ def main():
         dist.all_gather_object(gathered, (rank, local, os.getpid()))
         ranks = gathered
 
+    frames_per_gpu = b.n if wl.get("kind") == "anim" and not args.mock else args.batch
     if rank == 0:
         def roof(bytes_, ms, kernel):
             ach = bytes_ / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
@@ -568,6 +605,7 @@ def main():
                 # the ceiling the kernel is closest to (the contract's `bound` names the HBM roofline)
                 roofs[KERNELS[k]]["binding"] = "valu" if vr["frac"] > roofs[KERNELS[k]]["frac"] else "hbm"
         dominant = roofs[KERNELS[max(ran, key=lambda k: kms[k])]] if ran else None
+        target = roofs.get(wl.get("target")) if wl.get("target") else None
         if dominant and dominant["kernel"] == "vp8_recon_filter_kernel":
             # measured limiter: instruction issue / latency on the frame's CU, not HBM
             dominant["limiter"] = "VALU instruction issue on the frame's CU (roofline.valu; DESIGN.md §4)"
@@ -593,14 +631,15 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (SURVEY App. B frames encoded by libwebp 1.6.0, committed bitstreams)",
-            "config": {"workload": wl["name"], "description": wl["desc"], "frames_per_gpu": args.batch,
-                       "frames_total": args.batch * world,
+            "config": {"workload": wl["name"], "description": wl["desc"], "frames_per_gpu": frames_per_gpu,
+                       "frames_total": frames_per_gpu * world,
                        "distinct_bitstreams": len(datas), "input_bpp": round(bpp, 3),
                        "parallelism": f"frame-sharded over {world} GPU(s), one process each, no collectives "
                                       f"(gloo barrier + timing reduction only)",
                        "inputs": "resident in HBM (host entropy stage + H2D outside the timed region)"},
             "roofline": dominant,
             "kernel_ms": {KERNELS[k]: round(kms[k], 4) for k in ran},
+            "roofline_all": roofs,
             "lossy_emit": args.emit if kms[0] > 0 else None,
             "host_prepare_s": round(t_prep, 3),
             "ranks": [{"rank": r, "local_rank": lr, "pid": pid} for r, lr, pid in sorted(ranks)],
@@ -612,27 +651,33 @@ def main():
                                      "multi-rank path, not a scaling figure")
         if "yuv_to_rgba_kernel" in roofs:
             out["roofline_yuv_to_rgba"] = roofs["yuv_to_rgba_kernel"]
+        if target is not None:  # the kernel this "next"-row workload exists for
+            out["roofline_target"] = target
         if e2e is not None:
             out["end_to_end"] = e2e["pinned"]
             out["end_to_end_pageable"] = e2e["pageable"]
         out["host"] = host_info(world, ctx_threads)
         if not args.no_cpu_baseline:
             # rank 0 only, on the host cores of this job; the other ranks wait at the final barrier
-            cb = cpu_baseline(datas, args.cpu_seconds)
+            cb = cpu_baseline(datas, args.cpu_seconds, wl)
             out["cpu_baseline"] = cb
             out["speedup_vs_cpu_baseline"] = round(value / cb["value"], 1)
-            cbd = cpu_baseline_dsp(datas, max(2.0, args.cpu_seconds / 2))
-            out["cpu_baseline_dsp"] = cbd
-            out["speedup_vs_cpu_dsp"] = round(value / cbd["value"], 1)
+            if not wl.get("target"):  # (the pre-parsed leg restates the (a) rows only)
+                cbd = cpu_baseline_dsp(datas, max(2.0, args.cpu_seconds / 2))
+                out["cpu_baseline_dsp"] = cbd
+                out["speedup_vs_cpu_dsp"] = round(value / cbd["value"], 1)
             threads = max(1, min(64, host_cpus()))  # every CPU of the job
-            cba = cpu_baseline_parallel(datas, max(2.0, args.cpu_seconds / 2), threads)
+            cba = cpu_baseline_parallel(datas, max(2.0, args.cpu_seconds / 2), threads, wl)
             out["cpu_baseline_all_cores"] = cba
             out["speedup_vs_cpu_all_cores"] = round(value / cba["value"], 1)
             if "end_to_end" in out:
                 out["end_to_end"]["vs_cpu_all_cores"] = round(out["end_to_end"]["value"] / cba["value"], 2)
                 out["end_to_end"]["vs_cpu_1_core"] = round(out["end_to_end"]["value"] / cb["value"], 1)
             # a real-world CPU decoder beside the restatement (not the contract's cpu_baseline)
-            lw = cpu_baselines_libwebp(datas, max(2.0, args.cpu_seconds / 4), threads)
+            if wl.get("kind") == "anim" or wl.get("colorspace") is not None:
+                lw = {"unavailable": "libwebp leg times WebPDecodeRGBAInto on stills only"}
+            else:
+                lw = cpu_baselines_libwebp(datas, max(2.0, args.cpu_seconds / 4), threads)
             out["cpu_baseline_libwebp"] = lw
             if "simd_1_core" in lw:
                 out["speedup_vs_libwebp_simd_1_core"] = round(value / lw["simd_1_core"]["value"], 1)

@@ -267,6 +267,40 @@ def with_alpha(img, seed):
     return np.concatenate([img, a.astype(np.uint8)[..., None]], -1)
 
 
+def cutout_alpha(H, W, seed):
+    """The alpha of a cut-out (a product shot, a sticker): an off-centre ellipse with a 24-px
+    feathered edge, a half-transparent band below it, transparent elsewhere."""
+    rng = np.random.default_rng(1000 + seed)
+    yy, xx = np.mgrid[0:H, 0:W].astype(np.float32)
+    cy, cx = H * (0.4 + 0.1 * rng.random()), W * (0.4 + 0.2 * rng.random())
+    ry, rx = H * 0.38, W * 0.33
+    d = np.sqrt(((yy - cy) / ry) ** 2 + ((xx - cx) / rx) ** 2)
+    a = np.clip((1.0 - d) * min(ry, rx) / 24.0, 0.0, 1.0) * 255.0
+    band = (yy > H * 0.82) & (yy < H * 0.9)
+    a[band] = np.maximum(a[band], 128.0)
+    return a.astype(np.uint8)
+
+
+def anim_scene(H, W, n, seed):
+    """n full-canvas RGBA frames: an opaque textured background, a semi-transparent sprite a
+    quarter of the canvas wide sliding across it and a small opaque box changing colour:
+    WebPAnimEncoder emits blended sub-rectangles, as sticker / screen-capture animations do."""
+    rng = np.random.default_rng(seed)
+    base = np.concatenate([synth(H, W, seed, 4), np.full((H, W, 1), 255, np.uint8)], -1)
+    sh, sw = H // 3, W // 4
+    spr = np.concatenate([synth(sh, sw, seed + 1, 10), np.full((sh, sw, 1), 170, np.uint8)], -1)
+    out = []
+    for i in range(n):
+        img = base.copy()
+        y0, x0 = (H - sh) // 2 + int(40 * np.sin(i / 5.0)), (i * (W - sw)) // max(1, n - 1)
+        region = img[y0:y0 + sh, x0:x0 + sw].astype(np.int32)
+        a = spr[..., 3:4].astype(np.int32)
+        img[y0:y0 + sh, x0:x0 + sw, :3] = ((spr[..., :3] * a + region[..., :3] * (255 - a)) // 255).astype(np.uint8)
+        img[32:96, 32:160, :3] = rng.integers(0, 256, 3, dtype=np.uint8)
+        out.append(img)
+    return out
+
+
 def alpha_pattern(H, W, seed, kind):
     """RGB content plus an alpha plane shaped so one unfilter wins: 'h' rows of ramps with
     random row offsets, 'v' the transpose, 'g' a plane plus a mild texture, 'lv' four levels."""
@@ -715,6 +749,15 @@ BENCH_C5X = [("c5_ll2048", 2048, 2048, list(range(1, 8)), {"lossless": 1}, "corr
 # section bench_c3s: SURVEY §8(d)'s entropy-stress variant of C3 (sigma = 18, ~2 bpp: dense
 # coefficients, i4-heavy), 8 seeds, the C3 encoder settings
 BENCH_C3S = [("c3s_4k", 2160, 3840, list(range(8)), {"filter_type": 1, "filter_strength": 60}, "synth18")]
+# section bench_c3a: the "next" row f2 (ALPH, K4) at C3's size: C3's frames (same encoder
+# settings) with a feathered cut-out alpha plane, lossless-compressed ALPH, 8 seeds
+BENCH_C3A = [("c3a_4k", 2160, 3840, list(range(8)), {"filter_type": 1, "filter_strength": 60}, "synth6a")]
+# section bench_anim: the "next" row f3 (animation, K5): 64 frames of a 1920x1080 canvas through
+# WebPAnimEncoder (lossy, blended sub-rectangles); per-canvas SHA-256 of WebPAnimDecoder's output
+BENCH_ANIM = [("anim_1080p_x64", 1080, 1920, 64, 70)]
+# section bench_modes: the "next" row f4 (output colorspace, K6) on C3's frames: SHA-256 of
+# WebPDecode's MODE_RGB_565 bytes (fancy upsampling) added to the C3 entries
+BENCH_MODES = [("c3_4k", 4, "rgb565")]
 
 
 def sha(a):
@@ -725,14 +768,14 @@ def main(argv):
     """argv: sections to (re)generate among lossy, lossy_extra, lossless, alpha, modes, anim, bench (default: all);
     the manifest entries of the other sections are kept."""
     sections = set(argv) or {"lossy", "lossy_extra", "lossless", "alpha", "modes", "anim", "bench", "bench_c5x",
-                             "bench_c3s", "fuzz"}
+                             "bench_c3s", "bench_c3a", "bench_anim", "bench_modes", "fuzz"}
     os.makedirs(os.path.join(HERE, "lossy"), exist_ok=True)
     os.makedirs(os.path.join(HERE, "lossless"), exist_ok=True)
     os.makedirs(os.path.join(HERE, "bench"), exist_ok=True)
     mpath = os.path.join(HERE, "manifest.json")
     manifest = json.load(open(mpath)) if os.path.exists(mpath) else {}
     manifest["libwebp"] = "1.6.0 (Pillow 12.2.0 bundle, plain-C DSP)"
-    for sec in sections - {"bench_c5x", "bench_c3s"}:  # (bench_c5x / bench_c3s add to "bench")
+    for sec in sections - {"bench_c5x", "bench_c3s", "bench_c3a", "bench_modes"}:  # (these add to "bench")
         manifest[sec] = {}
     manifest.setdefault("bench", {})
     if "alpha" in sections:
@@ -827,10 +870,11 @@ def main(argv):
             print(name, len(data), info, [(f["x"], f["y"], f["w"], f["h"], f["dispose_bg"], f["no_blend"])
                                           for f in flags], flush=True)
     bench = ((BENCH_CASES if "bench" in sections else []) + (BENCH_C5X if "bench_c5x" in sections else []) +
-             (BENCH_C3S if "bench_c3s" in sections else []))
+             (BENCH_C3S if "bench_c3s" in sections else []) + (BENCH_C3A if "bench_c3a" in sections else []))
     for name, H, W, seeds, kw, gen in bench:
         for s in seeds:
             img = (synth(H, W, s, 6) if gen == "synth6" else synth(H, W, s, 18) if gen == "synth18"
+                   else np.concatenate([synth(H, W, s, 6), cutout_alpha(H, W, s)[..., None]], -1) if gen == "synth6a"
                    else corr_luma(H, W, s))
             lossless = kw.get("lossless", 0)
             data = encode(img, **kw)
@@ -842,8 +886,40 @@ def main(argv):
                        sha256={k: sha(v) for k, v in r.items()})
             if not lossless:
                 ent["header"] = vp8_header(data)
+            if gen == "synth6a":
+                ent["alph"] = alpha_header(data)
             manifest["bench"][fn] = ent
             print(fn, len(data), flush=True)
+    for name, mode, key in BENCH_MODES if "bench_modes" in sections else []:
+        for fn in sorted(k for k in manifest["bench"] if k.startswith(name + "_s")):
+            data = open(os.path.join(HERE, "bench", fn), "rb").read()
+            st, out = decode_mode(data, mode)
+            _plain_c(False)
+            st2, out2 = decode_mode(data, mode)
+            _plain_c(True)
+            assert st == 0 and st2 == 0 and np.array_equal(out, out2), fn
+            manifest["bench"][fn]["sha256"][key] = sha(out)
+            print(fn, key, flush=True)
+    if "bench_anim" in sections:
+        manifest["bench_anim"] = {}
+        for name, H, W, n, seed in BENCH_ANIM:
+            data = anim_encode(anim_scene(H, W, n, seed), [40] * n, [0] * n, allow_mixed=0)
+            info, canv, ts = anim_decode(data)
+            _plain_c(False)
+            _, canv_simd, ts_simd = anim_decode(data)
+            _plain_c(True)
+            assert np.array_equal(canv, canv_simd) and np.array_equal(ts, ts_simd), name
+            with open(os.path.join(HERE, "bench", name + ".webp"), "wb") as f:
+                f.write(data)
+            frames = []
+            for t, pl in riff_chunks(data):
+                if t == b"ANMF":
+                    frames.append([2 * int.from_bytes(pl[0:3], "little"), 2 * int.from_bytes(pl[3:6], "little"),
+                                   1 + int.from_bytes(pl[6:9], "little"), 1 + int.from_bytes(pl[9:12], "little"),
+                                   pl[15] & 1, (pl[15] >> 1) & 1])
+            manifest["bench_anim"][name] = dict(bytes=len(data), info=info, timestamps=ts.tolist(),
+                                                canvas_sha256=[sha(c) for c in canv], frames=frames)
+            print(name, len(data), info, "frame rects", frames[:4], flush=True)
     if "fuzz" in sections:
         # libwebp's WebPDecode status and RGBA digest of every mutant of the fuzz corpora
         # (oracle_lib.fuzz_mutants), so the GPU fuzz tests compare against libwebp too
