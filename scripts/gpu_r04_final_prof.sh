@@ -12,7 +12,8 @@ for w in ${WLS:-c3 c3s c5}; do
 done
 args=""
 for w in ${WLS:-c3 c3s c5}; do
-  case $w in c3) n=c3_4k_deblock_x256;; c3s) n=c3s_4k_deblock_x256;; c5) n=c5_ll2048_x256;; c2) n=c2_1080p_x256;; esac
+  case $w in c3) n=c3_4k_deblock_x256;; c3s) n=c3s_4k_deblock_x256;; c5) n=c5_ll2048_x256;; c2) n=c2_1080p_x256;;
+    c3a) n=c3a_4k_alpha_x256;; c3rgb565) n=c3_4k_rgb565_x256;; anim) n=anim_1080p_x64;; esac
   args="$args $n gpurun_out/prof_${T}_$w"
 done
 python3 scripts/make_pmc_traffic.py $args > gpurun_out/pmc_traffic_${T}.log 2>&1 || { tail gpurun_out/pmc_traffic_${T}.log; exit 1; }

@@ -17,7 +17,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNELS = {k: k for k in ("vp8_recon_filter_kernel", "yuv_to_rgba_kernel", "vp8l_transforms_kernel", "alpha_kernel",
-                           "vp8l_resolve_kernel")}
+                           "vp8l_resolve_kernel", "emit_kernel", "anim_compose_kernel")}
 
 
 def per_kernel(d):
