@@ -12,6 +12,7 @@
 #include <atomic>
 #include <chrono>
 #include <climits>
+#include <cstdlib>
 #include <condition_variable>
 #include <cstring>
 #include <memory>
@@ -224,6 +225,10 @@ struct wg_batch {
   size_t in_bytes = 0, plane_bytes = 0, rgba_bytes = 0;
   int max_mb_w = 1, max_w = 1, max_h = 1;  // max_mb_w over the frames whose K1 column store is in LDS
   int n_wide = 0;                          // lossy frames wider than that (global column store)
+  // K1's split kernel (several workgroups per frame, batches of fewer frames than CUs): parts per
+  // frame (1 = the one-workgroup kernels), and the lossy frames' progress flags (one region)
+  int split_parts = 1;
+  size_t off_gprog = 0, gprog_bytes = 0;
   int n_valid = 0;
   int64_t pixels = 0;
   double kbytes[kStages] = {};  // public order: K1, K2, K3, K4, K7, K6, K5
@@ -677,13 +682,14 @@ void batch_layout(wg_batch* b, wg::StagingArena& arena, int32_t* status) {
     f.off_v = pl_b;
     pl_b = align_up(pl_b + nmb * 64);
     f.wide = inf.mb_w > wg::vp8_recon_max_mb_w();
-    if (f.wide) {
-      b->n_wide++;
-      f.off_cols = pl_b;
-      pl_b = align_up(pl_b + (size_t)inf.mb_w * 160);
-    } else {
-      b->max_mb_w = std::max(b->max_mb_w, inf.mb_w);
-    }
+    if (f.wide) b->n_wide++;
+    else b->max_mb_w = std::max(b->max_mb_w, inf.mb_w);
+    // a global column store for every lossy frame: wide frames need it, and the split kernel
+    // runs every frame from it (mb_w * 160 B: 38 KB at 4K)
+    f.off_cols = pl_b;
+    pl_b = align_up(pl_b + (size_t)inf.mb_w * 160);
+    f.off_gprog = b->gprog_bytes;
+    b->gprog_bytes += wg::kGProgBytes;
     if (f.cropped) {  // K2 reads the crop window from compact planes (copied after K1)
       b->any_crop = true;
       f.yc_stride = (f.out_w + 15) & ~15;
@@ -751,6 +757,9 @@ void batch_layout(wg_batch* b, wg::StagingArena& arena, int32_t* status) {
   b->kbytes[3] = k4;
   b->kbytes[4] = k7;
   b->kbytes[5] = k6;
+  // the split kernel's progress flags, one region (zeroed at upload)
+  b->off_gprog = pl_b;
+  pl_b = align_up(pl_b + b->gprog_bytes);
   b->plane_bytes = std::max<size_t>(pl_b, kAlign);
   b->rgba_bytes = std::max<size_t>(rg_b, kAlign);
 }
@@ -759,6 +768,39 @@ void batch_layout(wg_batch* b, wg::StagingArena& arena, int32_t* status) {
 // inputs, all queued on the batch's home stream; the arena may be reused once they complete.
 // OUT_OF_MEMORY if a buffer or a copy could not be had (the batch then holds what it got: its
 // deleter hands it back).
+// Workgroups per frame for K1 (1 = one per frame, the kernels with the RGBA tail).  A batch of
+// fewer frames than CUs leaves CUs idle while each frame's wavefront runs on one of them, so
+// with room for two or more workgroups per frame the split kernel spreads each frame's MB-row
+// quads over up to three CUs -- if some frame has more quads than one workgroup reconstructs at
+// once (a 4K frame: 34 quads, 12 per workgroup).  WG_K1_SPLIT=0 disables it, =N forces N parts
+// (measurement).
+int split_k1_parts(const wg_batch* b) {
+  static const int forced = [] {
+    const char* e = getenv("WG_K1_SPLIT");
+    return e ? atoi(e) : -1;
+  }();
+  if (b->n_lossy == 0 || forced == 0 || forced == 1) return 1;
+  constexpr int kCUs = 256, kRecon = 12, kQuadRows = 4;
+  if (forced >= 2) return std::min(forced, wg::kMaxSplitParts);
+  int max_quads = 0;
+  for (const FrameParse& f : b->fp)
+    if (f.status == WG_STATUS_OK && !f.lossless) max_quads = std::max(max_quads, (f.info.mb_h + kQuadRows - 1) / kQuadRows);
+  const int cap = kCUs / std::max(1, (b->n + 7) / 8 * 8);  // (the grid rounds the frames up to whole XCD groups)
+  const int want = (max_quads + kRecon - 1) / kRecon;       // slabs of 12 quads
+  const int parts = std::min({3, cap, want});
+  return parts >= 2 ? parts : 1;
+}
+
+// Tags of the split kernel's progress flags: a fresh value per launch, never 0 (the flags are
+// zeroed at upload), so a flag left by an earlier launch on the same buffers never matches.
+uint32_t next_epoch() {
+  static std::atomic<uint32_t> epoch{0};
+  uint32_t e;
+  do e = (epoch.fetch_add(1, std::memory_order_relaxed) + 1) & 0xffffu;
+  while (e == 0);
+  return e;
+}
+
 int batch_upload(wg_batch* b, const wg::StagingArena& arena) {
   wg_ctx* ctx = b->ctx;
   const int n = b->n;
@@ -797,7 +839,8 @@ int batch_upload(wg_batch* b, const wg::StagingArena& arena) {
     d.blocks = reinterpret_cast<const int16_t*>(in + f.off_blocks);
     d.blocks_bytes = (int32_t)(f.n_blocks * 32);
     d.y = b->d_planes + f.off_y;
-    d.cols = f.wide ? b->d_planes + f.off_cols : nullptr;
+    d.cols = b->d_planes + f.off_cols;
+    d.gprog = reinterpret_cast<uint32_t*>(b->d_planes + b->off_gprog + f.off_gprog);
     d.u = b->d_planes + f.off_u;
     d.v = b->d_planes + f.off_v;
     d.mb_w = inf.mb_w;
@@ -805,7 +848,7 @@ int batch_upload(wg_batch* b, const wg::StagingArena& arena) {
     d.y_stride = 16 * inf.mb_w;
     d.uv_stride = 8 * inf.mb_w;
     d.filter_type = inf.filter_type;
-    d.flags = flags;
+    d.flags = flags | (f.wide ? wg::kFrameGlobalCols : 0);
     d.valid = 1;
     if (f.alpha) {
       AlphaDesc a{};
@@ -831,9 +874,11 @@ int batch_upload(wg_batch* b, const wg::StagingArena& arena) {
       b->adesc.push_back(a);
     }
   }
+  // Fewer frames than CUs: K1's split kernel (split_k1_parts); it has no RGBA tail, K2 converts.
+  b->split_parts = split_k1_parts(b);
   // Full-frame RGBA (no crop window anywhere in the batch): K1 converts each frame in its
   // own tail instead of a separate K2 launch (wg_batch_set_emit() switches back).
-  b->fused = !b->any_crop;
+  b->fused = !b->any_crop && b->split_parts < 2;
   if (b->fused)
     for (int i = 0; i < n; ++i)
       if (b->desc[(size_t)i].valid) b->desc[(size_t)i].flags |= wg::kFrameEmitRgba;
@@ -870,6 +915,7 @@ int batch_upload(wg_batch* b, const wg::StagingArena& arena) {
   }
   // the staged inputs: one copy per arena chunk, from pinned memory
   hipError_t e = hipSuccess;
+  if (b->gprog_bytes) e = hipMemsetAsync(b->d_planes + b->off_gprog, 0, b->gprog_bytes, home);
   for (size_t c = 0; c < arena.n_chunks() && e == hipSuccess; ++c) {
     const wg::StagingArena::Chunk& ch = arena.chunk(c);
     if (ch.used) e = hipMemcpyAsync(b->d_in + ch.dev_base, ch.p, ch.used, hipMemcpyHostToDevice, home);
@@ -955,7 +1001,7 @@ int wg_batch_run(wg_batch* b, void* stream) {
   hipEventRecord(t.ev[kStageK1], s);
   if (b->n_lossy > 0) {
     hipError_t e = wg::launch_vp8_recon_filter(b->d_desc, b->n, b->max_mb_w, b->n_lossy > b->n_wide,
-                                               b->n_wide > 0, b->d_err, s);
+                                               b->n_wide > 0, b->d_err, s, b->split_parts, next_epoch());
     if (e != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
   }
   hipEventRecord(t.ev[kStageK2], s);
@@ -1052,6 +1098,7 @@ int wg_batch_kernel_bytes(const wg_batch* b, double* bytes, int n_bytes) {
 int wg_batch_set_emit(wg_batch* b, int separate) {
   if (!b) return WG_STATUS_INVALID_PARAM;
   if (!separate && b->any_crop) return WG_STATUS_INVALID_PARAM;  // crop windows need K2
+  if (!separate) b->split_parts = 1;  // K1's RGBA tail: the one-workgroup kernels
   if (b->fused == !separate) return WG_STATUS_OK;
   b->fused = !separate;
   for (FrameDesc& d : b->desc)
@@ -1061,6 +1108,17 @@ int wg_batch_set_emit(wg_batch* b, int separate) {
                                 b->home);
   if (e == hipSuccess) e = hipStreamSynchronize(b->home);
   return e == hipSuccess ? WG_STATUS_OK : WG_STATUS_USER_ABORT;
+}
+
+int wg_batch_set_k1_parts(wg_batch* b, int parts) {
+  if (!b || parts < 0 || parts > wg::kMaxSplitParts) return WG_STATUS_INVALID_PARAM;
+  const int p = parts == 0 ? split_k1_parts(b) : parts;
+  if (p >= 2 && b->fused) {  // the split kernel has no RGBA tail: K2 converts
+    const int st = wg_batch_set_emit(b, 1);
+    if (st != WG_STATUS_OK) return st;
+  }
+  b->split_parts = p;
+  return WG_STATUS_OK;
 }
 
 int wg_batch_run_emit(wg_batch* b, void* stream) {

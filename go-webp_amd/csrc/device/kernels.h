@@ -11,8 +11,12 @@ namespace wg {
 size_t vp8_recon_lds_bytes(int mb_w);
 int vp8_recon_max_mb_w();
 // d_err: device int, OR-ed with 1 if a wave gave up waiting (bounded spin).
+// split_parts >= 2: the split kernel (split_parts workgroups per frame, every frame, no RGBA
+// tail; `epoch` tags its part-boundary flags and must differ from the previous launch's on the
+// same descriptors).
 hipError_t launch_vp8_recon_filter(const FrameDesc* d_frames, int n_frames, int max_mb_w, bool lds_frames,
-                                   bool wide_frames, int* d_err, hipStream_t stream);
+                                   bool wide_frames, int* d_err, hipStream_t stream, int split_parts = 1,
+                                   uint32_t epoch = 0);
 
 // K2: YUV420 -> RGBA (fancy 9-3-3-1 upsampling or point sampling) over a batch.
 // `single` (when non-null, n_frames == 1) is passed by value instead of d_frames.

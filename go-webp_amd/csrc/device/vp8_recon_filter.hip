@@ -156,9 +156,22 @@ __device__ __forceinline__ uint32_t bcast(uint32_t v) { return __builtin_amdgcn_
 __device__ __forceinline__ int byte_of(uint32_t w, int i) { return (w >> (8 * i)) & 0xff; }
 __device__ __forceinline__ uint32_t ld32(const uint8_t* p) { return *reinterpret_cast<const uint32_t*>(p); }
 __device__ __forceinline__ void st32(uint8_t* p, uint32_t v) { *reinterpret_cast<uint32_t*>(p) = v; }
-// the column store of wide frames (global memory, see vp8_recon_filter_kernel)
-__device__ __forceinline__ uint32_t ld32(gptr<const uint8_t> p) { return *(gptr<const uint32_t>)p; }
-__device__ __forceinline__ void st32(gptr<uint8_t> p, uint32_t v) { *(gptr<uint32_t>)p = v; }
+// Column-store accesses (LDS, or global memory for wide frames and the split kernel, see
+// vp8_recon_filter_kernel).  Those of the split kernel's part-boundary quads (kSplit): global_load /
+// global_store with sc1 (relaxed agent-scope atomics lower to exactly that) -- the producer's
+// lines written through, the consumer's read past its CU's L1 and its XCD's L2 state, the
+// placement-independent hand-off of MI355X_MICROARCH.md §Workgroup dispatch (sc1 stores, vmcnt(0),
+// sc1 flag; sc1 poll, sc1 loads).  `sc1` is wave-uniform.
+__device__ __forceinline__ uint32_t col_ld(uint8_t* p, bool sc1) { return ld32(p); }
+__device__ __forceinline__ void col_st(uint8_t* p, uint32_t v, bool sc1) { st32(p, v); }
+__device__ __forceinline__ uint32_t col_ld(gptr<uint8_t> p, bool sc1) {
+  if (sc1) return __hip_atomic_load((gptr<uint32_t>)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return *(gptr<const uint32_t>)p;
+}
+__device__ __forceinline__ void col_st(gptr<uint8_t> p, uint32_t v, bool sc1) {
+  if (sc1) __hip_atomic_store((gptr<uint32_t>)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *(gptr<uint32_t>)p = v;
+}
 
 // 32-bit wrapping MUL1/MUL2 (dsp.h.go WEBP_TRANSFORM_AC3_MUL1/2).  |a| < 2^23 for any
 // int16 input, so the 24-bit multiplier gives the exact low 32 bits of a*c.
@@ -588,17 +601,41 @@ __device__ __forceinline__ void emit_tail(const FrameDesc& F, uint32_t* progress
 // 4k+g -> 4k+g+1) by the fences of lds_sync, across waves by the release/acquire progress
 // counters -- at workgroup scope the AMDGPU memory model orders global accesses of one CU
 // the same way (its L1 is shared by the workgroup), no extra s_waitcnt needed.
-template <bool kGlobalCols>
+//
+// kSplit (implies kGlobalCols): nparts workgroups per frame for batches of fewer frames than CUs.
+// Part p reconstructs the quads [pR, pR + R) -- one quad per reconstructing wave, the frame in
+// nparts horizontal slabs of 4R MB rows -- so a frame's wavefront runs on nparts CUs instead of
+// one (a lone 4K frame: 34 quads on 3 CUs).  Inside a part everything is as in the unsplit kernel;
+// across a slab boundary the part's first quad waits on a progress flag the previous part's last
+// quad publishes in global memory (FrameDesc::gprog, tagged with the launch's epoch), and both
+// quads access the column store with sc1 (col_ld / col_st).  Dependencies only run from part p - 1
+// to part p, and part p - 1's workgroup has the lower index (blocks are dispatched in order), so
+// no part waits on a part that cannot be running.  No RGBA tail: a split batch converts in K2.
+// A frame taller than nparts * R quads runs on part 0 alone.
+template <bool kGlobalCols, bool kSplit>
 __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc* __restrict__ frames, int* err,
-                                                                int lead_arg, int recon_waves_arg) {
+                                                                int lead_arg, int recon_waves_arg, int n_frames,
+                                                                int nparts, uint32_t epoch) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   // Progress counters as a typed __shared__ array + relaxed workgroup atomics, so the spin
   // is a ds_read (lgkmcnt) -- a volatile generic pointer became a flat load whose
   // vmcnt(0) drained the record/coefficient prefetch every MB.
   __shared__ uint32_t progress[kWaves];
   __shared__ uint32_t recon_done, next_unit;  // K1 tail (emit_tail): waves done, units claimed
-  const FrameDesc* F = frames + blockIdx.x;
-  if (!F->valid || (F->cols != nullptr) != kGlobalCols) return;
+  static_assert(!kSplit || kGlobalCols, "the split kernel keeps the column store in global memory");
+  int fidx = blockIdx.x, part = 0;
+  if constexpr (kSplit) {
+    // blocks b and b + 8 -- one XCD under the observed round-robin dealing, a matter of speed only
+    // (the hand-off is placement independent) -- are parts of one frame
+    const int b = blockIdx.x;
+    fidx = (b / (8 * nparts)) * 8 + (b & 7);
+    part = (b >> 3) % nparts;
+    if (fidx >= n_frames) return;
+  }
+  const FrameDesc* F = frames + fidx;
+  if (!F->valid) return;
+  if constexpr (!kSplit)
+    if (((F->flags & kFrameGlobalCols) != 0) != kGlobalCols) return;
   const int mb_w = F->mb_w, mb_h = F->mb_h;
   const int ftype = F->filter_type;
   const int ys = F->y_stride, uvs = F->uv_stride;
@@ -631,7 +668,7 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
   // per MB column c: cols + c*kColBytes: [0..15] ytop Y, [16..23] U, [24..31] V, [32..159] fbot
   if (threadIdx.x < kWaves) progress[threadIdx.x] = 0;
   if (threadIdx.x == 0) recon_done = next_unit = 0;
-  const bool emit = F->flags & kFrameEmitRgba;
+  const bool emit = !kSplit && (F->flags & kFrameEmitRgba);
   if (emit) __builtin_amdgcn_s_setprio(2);  // reconstruction is the critical path; the tail's conversion yields
   const int nquads = (mb_h + kRows - 1) / kRows;
   // Waves that reconstruct (quads k = wave, wave + R, ...); with the RGBA tail the others
@@ -639,16 +676,33 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
   // ring safe: quad k + 16 only starts on a wave that has completed a quad > k, so quad k
   // is complete whenever its slot holds a later quad's value.
   const int R = recon_waves_arg > 0 ? min(recon_waves_arg, kMaxRecon) : kMaxRecon;
+  // split: the frame in slabs (one quad per reconstructing wave) when it has at most nparts * R
+  // quads; parts without quads, and every part but 0 of a taller frame, leave (whole workgroups,
+  // before any barrier)
+  bool slabs = false;
+  if constexpr (kSplit) {
+    slabs = nquads <= nparts * R;
+    if (slabs ? part * R >= nquads : part > 0) return;
+  }
+  const gptr<uint32_t> gprog = as_global(F->gprog);
   for (int t = threadIdx.x; t < 160; t += blockDim.x) tab[t] = kPred4Table[t];
   K1_TIMELINE_START();
   __syncthreads();
 
   bool aborted = false;  // a progress wait timed out (error flagged): stop waiting
-  for (int k = wave; wave < R && k < nquads; k += R) {
+  const int k0 = slabs ? part * R + wave : wave;
+  const int kend = slabs ? min(nquads, part * R + R) : nquads;
+  for (int k = k0; wave < R && k < kend; k += R) {
     const int y = kRows * k + g;
     const bool row_ok = y < mb_h;
     const bool has_next = kRows * (k + 1) < mb_h;  // a later quad waits on this one's last row
     const bool last_row = y == mb_h - 1;
+    // split slabs: the part's first quad waits on the previous part's last, which publishes its
+    // progress to global memory; both access the column store agent-coherently (sc1)
+    const bool g_wait = kSplit && slabs && part > 0 && k == part * R;
+    const bool g_pub = kSplit && slabs && k == part * R + R - 1 && has_next;
+    const bool csc1 = g_wait || g_pub;
+    uint32_t gseen = 0;  // the previous part's published progress last read (g_wait)
     uint32_t blk = row_ok ? row_block0[y] : 0u;
     MbRec rc = load_rec(recs, mb_w, y, row_ok, -2 * g);
     MbRec rn = load_rec(recs, mb_w, y, row_ok, -2 * g + 1);
@@ -712,7 +766,29 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
       //      and the timeout does not leave the loop: any path reaching the loop latch without
       //      this iteration's plane stores makes the waitcnt pass extend the latch's prefetch
       //      wait over those stores (a vmcnt that waits for store acks every MB).
-      if (k > 0 && i < mb_w) {
+      if (g_wait && i < mb_w) {
+        // the flag: epoch << 16 | columns the previous part's last row has completed (sc1 poll;
+        // a flag of an earlier launch reads as 0)
+        const uint32_t gneed = (uint32_t)min(i + lead, mb_w);
+        const gptr<uint32_t> gf = gprog + 32 * (part - 1);
+        auto gcur = [&] {
+          const uint32_t v =
+              __builtin_amdgcn_readfirstlane(__hip_atomic_load(gf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+          return (v >> 16) == (epoch & 0xffffu) ? (v & 0xffffu) : 0u;
+        };
+        if (!aborted && gseen < gneed && (gseen = gcur()) < gneed) {
+          const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+          for (;;) {
+            __builtin_amdgcn_s_sleep(8);
+            if ((gseen = gcur()) >= gneed) break;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s: give up, flag
+              if (lane == 0) atomicOr(err, 1);
+              aborted = true;
+              break;
+            }
+          }
+        }
+      } else if (k > 0 && i < mb_w) {
         const uint32_t need = ((uint32_t)(k - 1) << 16) | (uint32_t)min(i + lead, mb_w);
         uint32_t* pr = progress + ((k - 1) & (kWaves - 1));
         auto cur = [&] {
@@ -771,14 +847,14 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
       //      previous load.
       if (act && y > 0) {
         if (m < 8) {
-          const uint32_t tv = ld32(col + 4 * m);
+          const uint32_t tv = col_ld(col + 4 * m, csc1);
           st32(ws + (m < 4 ? Y_OFF - BPS + 4 * m : m < 6 ? U_OFF - BPS + 4 * (m - 4) : V_OFF - BPS + 4 * (m - 6)), tv);
           if (x > 0 && (m == 3 || m == 5 || m == 7))
             ws[(m == 3 ? Y_OFF : m == 5 ? U_OFF : V_OFF) - BPS - 1] = (uint8_t)(top_carry >> 24);
           top_carry = tv;
         } else if (m == 8 && i4) {
           // top-right samples, replicated down to rows 3, 7, 11 by the same lane (no read-back)
-          const uint32_t tr = last_x ? bcast(col[15]) : ld32(col + kColBytes);
+          const uint32_t tr = last_x ? bcast(col_ld(col + 12, csc1) >> 24) : col_ld(col + kColBytes, csc1);
           st32(ws + Y_OFF - BPS + 16, tr);
           st32(ws + Y_OFF + 3 * BPS + 16, tr);
           st32(ws + Y_OFF + 7 * BPS + 16, tr);
@@ -940,14 +1016,14 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
         //      (lanes 0..3 luma, 4..5 U, 6..7 V: the column store's dword m either way)
         if (!last_row && m < 8) {
           const int so = m < 4 ? Y_OFF + 15 * BPS + 4 * m : (m < 6 ? U_OFF - 16 : V_OFF - 24) + 7 * BPS + 4 * m;
-          st32(col + 4 * m, ld32(ws + so));
+          col_st(col + 4 * m, ld32(ws + so), csc1);
         }
         // ---- filter window: rows above from fbot (the MB body was written into it by the
         //      prediction sections, next to the workspace)
         if (y > 0) {
-          st32(fw + kFwY + (m >> 2) * FWY + 4 + 4 * (m & 3), ld32(col + 32 + 4 * m));
+          st32(fw + kFwY + (m >> 2) * FWY + 4 + 4 * (m & 3), col_ld(col + 32 + 4 * m, csc1));
           const int p = m >> 3, rr = (m >> 1) & 3, dd = m & 1;
-          st32(fw + (p ? kFwV : kFwU) + rr * FWC + 4 + 4 * dd, ld32(col + 96 + 32 * p + 8 * rr + 4 * dd));
+          st32(fw + (p ? kFwV : kFwU) + rr * FWC + 4 + 4 * dd, col_ld(col + 96 + 32 * p + 8 * rr + 4 * dd, csc1));
         }
       }
       lds_sync();
@@ -977,10 +1053,10 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
           const int rr = m >> 2, d = m & 3;
           const uint8_t* src = fw + kFwY + (rr + 16) * FWY;
           if (d == 0) {
-            if (x > 0) st32(col - kColBytes + 32 + rr * 16 + 12, ld32(src));
-            if (last_x) st32(col + 32 + rr * 16 + 12, ld32(src + 16));
+            if (x > 0) col_st(col - kColBytes + 32 + rr * 16 + 12, ld32(src), csc1);
+            if (last_x) col_st(col + 32 + rr * 16 + 12, ld32(src + 16), csc1);
           } else {
-            st32(col + 32 + rr * 16 + 4 * (d - 1), ld32(src + 4 * d));
+            col_st(col + 32 + rr * 16 + 4 * (d - 1), ld32(src + 4 * d), csc1);
           }
         }
         {
@@ -988,10 +1064,10 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
           const uint8_t* src = fw + (p ? kFwV : kFwU) + (rr + 8) * FWC;
           const ColPtr cb0 = col + 96 + 32 * p + 8 * rr;
           if (d == 0) {
-            if (x > 0) st32(cb0 - kColBytes + 4, ld32(src));
-            if (last_x) st32(cb0 + 4, ld32(src + 8));
+            if (x > 0) col_st(cb0 - kColBytes + 4, ld32(src), csc1);
+            if (last_x) col_st(cb0 + 4, ld32(src + 8), csc1);
           } else {
-            st32(cb0, ld32(src + 4));
+            col_st(cb0, ld32(src + 4), csc1);
           }
         }
       }
@@ -1083,9 +1159,20 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
         }
       }
       lds_sync();
-      if (lane == 16 * (kRows - 1) && has_next && x >= 0)
+      if (g_pub) {
+        // the next part's first quad: every 4th column of the last row, and its last (after this
+        // wave's sc1 column-store stores have completed: vmcnt(0), then the sc1 flag store)
+        const int xl = i - 2 * (kRows - 1);
+        if (xl >= 0 && ((xl & 3) == 3 || xl + 1 == mb_w)) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          if (lane == 16 * (kRows - 1))
+            __hip_atomic_store(gprog + 32 * part, ((epoch & 0xffffu) << 16) | (uint32_t)(xl + 1), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+      } else if (lane == 16 * (kRows - 1) && has_next && x >= 0) {
         __hip_atomic_store(progress + (k & (kWaves - 1)), ((uint32_t)k << 16) | (uint32_t)(x + 1), __ATOMIC_RELEASE,
                            __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
       K1_SECT(12);
       rc = rn;
       rn = rnn;
@@ -1146,7 +1233,7 @@ size_t vp8_recon_lds_bytes(int mb_w) {
 int vp8_recon_max_mb_w() { return (int)((163840 - kHdrBytes - kMaxRecon * kRows * kSlotBytes) / kColBytes); }
 
 hipError_t launch_vp8_recon_filter(const FrameDesc* d_frames, int n_frames, int max_mb_w, bool lds_frames,
-                                   bool wide_frames, int* d_err, hipStream_t stream) {
+                                   bool wide_frames, int* d_err, hipStream_t stream, int split_parts, uint32_t epoch) {
   // WG_K1_LEAD overrides the inter-quad lead (tuning experiments only).
   static const int lead = [] {
     const char* e = getenv("WG_K1_LEAD");
@@ -1158,17 +1245,32 @@ hipError_t launch_vp8_recon_filter(const FrameDesc* d_frames, int n_frames, int 
     const char* e = getenv("WG_K1_RECON_WAVES");
     return e ? atoi(e) : 0;
   }();
+  if (split_parts >= 2) {  // every frame on split_parts workgroups, column stores in global memory
+    if (split_parts > kMaxSplitParts) return hipErrorInvalidValue;
+    const size_t lds = vp8_recon_lds_bytes(0);
+    static bool configured = false;
+    if (lds > 65536 && !configured) {
+      const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&vp8_recon_filter_kernel<true, true>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (e != hipSuccess) return e;
+      configured = true;
+    }
+    const int grid = ((n_frames + 7) / 8) * 8 * split_parts;
+    hipLaunchKernelGGL((vp8_recon_filter_kernel<true, true>), dim3(grid), dim3(1024), lds, stream, d_frames, d_err,
+                       lead, recon_waves, n_frames, split_parts, epoch);
+    return hipGetLastError();
+  }
   if (lds_frames) {
     const size_t lds = vp8_recon_lds_bytes(max_mb_w);
     static size_t configured = 0;
     if (lds > 65536 && lds > configured) {
-      const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&vp8_recon_filter_kernel<false>),
+      const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&vp8_recon_filter_kernel<false, false>),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       if (e != hipSuccess) return e;
       configured = lds;
     }
-    hipLaunchKernelGGL(vp8_recon_filter_kernel<false>, dim3(n_frames), dim3(1024), lds, stream, d_frames, d_err,
-                       lead, recon_waves);
+    hipLaunchKernelGGL((vp8_recon_filter_kernel<false, false>), dim3(n_frames), dim3(1024), lds, stream, d_frames,
+                       d_err, lead, recon_waves, n_frames, 1, 0u);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
@@ -1176,13 +1278,13 @@ hipError_t launch_vp8_recon_filter(const FrameDesc* d_frames, int n_frames, int 
     const size_t lds = vp8_recon_lds_bytes(0);
     static bool configured = false;
     if (lds > 65536 && !configured) {
-      const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&vp8_recon_filter_kernel<true>),
+      const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&vp8_recon_filter_kernel<true, false>),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       if (e != hipSuccess) return e;
       configured = true;
     }
-    hipLaunchKernelGGL(vp8_recon_filter_kernel<true>, dim3(n_frames), dim3(1024), lds, stream, d_frames, d_err,
-                       lead, recon_waves);
+    hipLaunchKernelGGL((vp8_recon_filter_kernel<true, false>), dim3(n_frames), dim3(1024), lds, stream, d_frames,
+                       d_err, lead, recon_waves, n_frames, 1, 0u);
     return hipGetLastError();
   }
   return hipSuccess;

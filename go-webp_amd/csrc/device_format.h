@@ -51,6 +51,13 @@ static_assert(sizeof(MbRec) == 16, "MbRec must be 16 bytes");
 // decode, plus kFrameEmitRgba: K1 itself converts the frame to RGBA in its tail (no K2).
 constexpr int32_t kFrameNoFancy = 2;
 constexpr int32_t kFrameEmitRgba = 1 << 8;
+// K1: the frame's column store is too wide for LDS (vp8_recon_max_mb_w): the global-column
+// instantiation runs it.
+constexpr int32_t kFrameGlobalCols = 1 << 9;
+// K1 split kernel: bytes of per-frame part-boundary progress flags (FrameDesc::gprog), one
+// flag per 128-B line, for up to kMaxSplitParts parts
+constexpr int kMaxSplitParts = 4;
+constexpr int kGProgBytes = 128 * kMaxSplitParts;
 
 struct FrameDesc {
   const MbRec* mbs;
@@ -60,11 +67,13 @@ struct FrameDesc {
   uint8_t* u;
   uint8_t* v;
   uint8_t* rgba;
-  uint8_t* cols;  // K1 column store in global memory (wide frames only, mb_w * 160 B), else null
+  uint8_t* cols;  // K1 column store in global memory (mb_w * 160 B): used by wide frames
+                  // (kFrameGlobalCols) and by the split kernel, which runs every frame from it
   int32_t width, height, mb_w, mb_h;
   int32_t y_stride, uv_stride, rgba_stride, filter_type;
   int32_t flags, valid, blocks_bytes, pad2;  // blocks_bytes: size of `blocks` (K1 bounds)
-  int32_t pad3[4];
+  uint32_t* gprog;  // split kernel: one progress flag per part boundary, 128 B apart (kGProgBytes)
+  int32_t pad3[2];
 };
 static_assert(sizeof(FrameDesc) == 128, "FrameDesc must be 128 bytes");
 

@@ -215,6 +215,7 @@ _SIGS = {
     "wg_ctx_pipeline_stats": (C.c_int, [_P, _P]),
     "wg_host_alloc": (_P, [C.c_size_t]),
     "wg_host_free": (None, [_P]),
+    "wg_batch_set_k1_parts": (C.c_int, [_P, C.c_int]),
     "wg_anim_batch_create": (_P, [_P, _P, C.c_size_t, C.c_int32, _P]),
     "wg_anim_batch_info": (C.c_int, [_P, _P, _P, _P]),
     "wg_anim_batch_download": (C.c_int, [_P, _P, C.c_size_t, _P]),
@@ -444,6 +445,13 @@ class Batch:
         st = lib().wg_batch_set_emit(self._h, 1 if separate else 0)
         if st != Status.OK:
             raise WebPError(st, "wg_batch_set_emit")
+
+    def set_k1_parts(self, parts):
+        """K1 workgroups per frame: 1 (the kernels with the RGBA tail), 2..4 (the split kernel;
+        K2 converts), 0 (automatic: split for batches of fewer frames than CUs)."""
+        st = lib().wg_batch_set_k1_parts(self._h, parts)
+        if st != Status.OK:
+            raise WebPError(st, "wg_batch_set_k1_parts")
 
     def run_emit(self, stream=None):
         """The YUV420->RGBA stage alone (K2) over the planes of the last run."""

@@ -205,6 +205,12 @@ int wg_batch_run(wg_batch* b, void* stream);
  * inside the decode loop, io_dec.c.go:65-115). */
 int wg_batch_set_emit(wg_batch* b, int separate);
 
+/* Workgroups per frame for K1 (tests, measurement): 1 = one per frame (the kernels with the
+ * RGBA tail); 2..4 = the split kernel, each frame's MB-row quads spread over that many CUs (K2
+ * converts); 0 = the automatic choice, which a batch makes at creation: split when it holds
+ * fewer frames than CUs and a frame has more quads than one workgroup runs at once. */
+int wg_batch_set_k1_parts(wg_batch* b, int parts);
+
 /* The YUV420->RGBA stage alone (K2: EmitFancyRGB / EmitSampledRGB, io_dec.c.go:53-115) over the batch's
  * reconstructed planes (after a wg_batch_run): the stage-roofline measurement of the
  * metric.  Its duration is reported as ms[1] by wg_batch_kernel_ms(). */

@@ -3,6 +3,7 @@
 Bit-exact is the bar everywhere (all arithmetic on this path is integer).
 """
 import hashlib
+import os
 
 import numpy as np
 import pytest
@@ -268,3 +269,55 @@ def test_wide_frames_global_column_store(ctx):
     outs, status = ctx.decode_batch_opts([d, load_lossy("wide_9617x40")[0]], webp_amd.options(1, crop))
     assert status[0] == 0 and status[1] != 0  # the window exceeds the 9617-px frame
     np.testing.assert_array_equal(outs[0], oracle_output(d, 1, crop))
+
+
+@pytest.mark.parametrize("parts", [2, 3, 4])
+def test_split_k1_bench_frames(ctx, parts):
+    """K1's split kernel (wg_batch_set_k1_parts): a frame's MB-row quads spread over `parts`
+    workgroups, part-boundary hand-offs through global progress flags and sc1 column-store
+    traffic.  4K (34 quads: slabs of 12; with 2 parts more quads than 2 x 12 -- part 0 alone),
+    the dense c3s frames and 1080p (17 quads), every frame's RGBA SHA-256 = libwebp's, on
+    repeated runs (a fresh flag epoch per launch)."""
+    m = manifest()["bench"]
+    for prefix in ("c3_4k", "c3s_4k", "c2_1080p"):
+        paths = bench_files(prefix)[:5]
+        b = ctx.batch([open(p, "rb").read() for p in paths])
+        try:
+            b.set_k1_parts(parts)
+            for r in range(3):
+                b.run()
+                for i, p in enumerate(paths):
+                    assert _sha(b.rgba(i)) == m[os.path.basename(p)]["sha256"]["rgba"], (prefix, parts, r, i)
+            ms = b.kernel_ms()
+            assert ms[0] > 0 and ms[1] > 0, ms  # split K1, then K2
+        finally:
+            b.close()
+
+
+@pytest.mark.parametrize("parts", [2, 3])
+def test_split_k1_fixtures(ctx, parts):
+    """Every opaque lossy fixture through the split kernel: tall narrow frames (16 quads: two
+    slabs), one-column frames, partial last quads, wide frames (global column store anyway),
+    both filter types -- planes and RGBA equal to libwebp's and the oracle's."""
+    datas, golds = zip(*[load_lossy(n) for n in OPAQUE])
+    b = ctx.batch(list(datas))
+    try:
+        b.set_k1_parts(parts)
+        b.run()
+        b.run()
+        for i, (name, g) in enumerate(zip(OPAQUE, golds)):
+            y, u, v = b.yuv(i)
+            np.testing.assert_array_equal(y, g["y"], err_msg=name)
+            np.testing.assert_array_equal(u, g["u"], err_msg=name)
+            np.testing.assert_array_equal(v, g["v"], err_msg=name)
+            np.testing.assert_array_equal(b.rgba(i), g["rgba"], err_msg=name)
+    finally:
+        b.close()
+
+
+def test_single_frame_decode_uses_split_and_matches():
+    """The single-frame drop-in (webp.Decode's path) on a 4K frame -- one frame, so the automatic
+    choice runs the split kernel: libwebp's RGBA."""
+    m = manifest()["bench"]
+    for p in bench_files("c3_4k")[:2] + bench_files("c3s_4k")[:1]:
+        assert _sha(webp_amd.decode(open(p, "rb").read())) == m[os.path.basename(p)]["sha256"]["rgba"]
