@@ -757,7 +757,7 @@ BENCH_C3A = [("c3a_4k", 2160, 3840, list(range(8)), {"filter_type": 1, "filter_s
 BENCH_ANIM = [("anim_1080p_x64", 1080, 1920, 64, 70)]
 # section bench_modes: the "next" row f4 (output colorspace, K6) on C3's frames: SHA-256 of
 # WebPDecode's MODE_RGB_565 bytes (fancy upsampling) added to the C3 entries
-BENCH_MODES = [("c3_4k", 4, "rgb565")]
+BENCH_MODES = [("c3_4k", 6, "rgb565")]  # MODE_RGB_565 = 6 (WEBP_CSP_MODE)
 
 
 def sha(a):

@@ -84,7 +84,7 @@ def test_cropped_batch_keeps_separate_emit(ctx):
 def test_resident_batch_runs_k6_as_a_stage(ctx, key):
     """A batch created with an output colorspace (or flip) runs K6 as the last stage of every
     wg_batch_run (its own kernel_ms entry); downloads copy its output: equal to WebPDecode's
-    bytes after repeated runs (RGB flipped, rgbA premultiplied, RGB565 point-sampled, RGBA
+    bytes after repeated runs (RGB flipped, rgbA premultiplied, ARGB point-sampled, RGBA
     flipped)."""
     mode, cname, flip, nf = parse_mode_key(key)
     srcs = [load_modes(s) for s in mode_sources()]

@@ -68,7 +68,7 @@ def test_c3_rgb565_resident_batch(ctx):
     paths = bench_files("c3_4k")
     m = manifest()["bench"]
     datas = [open(p, "rb").read() for p in paths]
-    b = ctx.batch([datas[i % 8] for i in range(16)], opts=webp_amd.options(4))
+    b = ctx.batch([datas[i % 8] for i in range(16)], opts=webp_amd.options(6))  # MODE_RGB_565
     try:
         for _ in range(2):
             b.run()
@@ -85,7 +85,7 @@ def test_c3_rgb565_resident_batch(ctx):
 def test_c3_rgb565_oracle_one_frame():
     p = bench_files("c3_4k")[5]
     want = manifest()["bench"][os.path.basename(p)]["sha256"]["rgb565"]
-    assert _sha(oracle_output(open(p, "rb").read(), mode=4)) == want
+    assert _sha(oracle_output(open(p, "rb").read(), mode=6)) == want
 
 
 def test_anim_1080p_resident(ctx):
