@@ -228,6 +228,7 @@ struct wg_batch {
   // K1's split kernel (several workgroups per frame, batches of fewer frames than CUs): parts per
   // frame (1 = the one-workgroup kernels), and the lossy frames' progress flags (one region)
   int split_parts = 1;
+  int split_from = 0;  // frames [split_from, n) on the split kernel, [0, split_from) on the others
   size_t off_gprog = 0, gprog_bytes = 0;
   int n_valid = 0;
   int64_t pixels = 0;
@@ -774,21 +775,30 @@ void batch_layout(wg_batch* b, wg::StagingArena& arena, int32_t* status) {
 // quads over up to three CUs -- if some frame has more quads than one workgroup reconstructs at
 // once (a 4K frame: 34 quads, 12 per workgroup).  WG_K1_SPLIT=0 disables it, =N forces N parts
 // (measurement).
-int split_k1_parts(const wg_batch* b) {
+// A batch of more than CUs frames runs the one-workgroup kernel over whole rounds of 256 frames; a
+// short last round (the 257th frame) would cost a full frame's critical path for a few frames, so
+// it runs on the split kernel instead, behind the others (*from = its first frame).
+int split_k1_parts(const wg_batch* b, int* from = nullptr) {
   static const int forced = [] {
     const char* e = getenv("WG_K1_SPLIT");
     return e ? atoi(e) : -1;
   }();
+  if (from) *from = 0;
   if (b->n_lossy == 0 || forced == 0 || forced == 1) return 1;
   constexpr int kCUs = 256, kRecon = 12, kQuadRows = 4;
   if (forced >= 2) return std::min(forced, wg::kMaxSplitParts);
+  const int head = b->n > kCUs ? b->n / kCUs * kCUs : 0;  // whole rounds of the one-workgroup kernel
   int max_quads = 0;
-  for (const FrameParse& f : b->fp)
+  for (int i = head; i < b->n; ++i) {
+    const FrameParse& f = b->fp[(size_t)i];
     if (f.status == WG_STATUS_OK && !f.lossless) max_quads = std::max(max_quads, (f.info.mb_h + kQuadRows - 1) / kQuadRows);
-  const int cap = kCUs / std::max(1, (b->n + 7) / 8 * 8);  // (the grid rounds the frames up to whole XCD groups)
-  const int want = (max_quads + kRecon - 1) / kRecon;       // slabs of 12 quads
+  }
+  const int cap = kCUs / std::max(1, (b->n - head + 7) / 8 * 8);  // (the grid rounds the frames up to XCD groups)
+  const int want = (max_quads + kRecon - 1) / kRecon;              // slabs of 12 quads
   const int parts = std::min({3, cap, want});
-  return parts >= 2 ? parts : 1;
+  if (parts < 2) return 1;
+  if (from) *from = head;
+  return parts;
 }
 
 // Tags of the split kernel's progress flags: a fresh value per launch, never 0 (the flags are
@@ -875,10 +885,12 @@ int batch_upload(wg_batch* b, const wg::StagingArena& arena) {
     }
   }
   // Fewer frames than CUs: K1's split kernel (split_k1_parts); it has no RGBA tail, K2 converts.
-  b->split_parts = split_k1_parts(b);
+  b->split_parts = split_k1_parts(b, &b->split_from);
   // Full-frame RGBA (no crop window anywhere in the batch): K1 converts each frame in its
-  // own tail instead of a separate K2 launch (wg_batch_set_emit() switches back).
-  b->fused = !b->any_crop && b->split_parts < 2;
+  // own tail instead of a separate K2 launch (wg_batch_set_emit() switches back); a split
+  // remainder behind whole rounds converts in a K2 over its frames alone.
+  if (b->split_parts >= 2 && b->split_from > 0 && b->any_crop) b->split_parts = 1, b->split_from = 0;
+  b->fused = !b->any_crop && (b->split_parts < 2 || b->split_from > 0);
   if (b->fused)
     for (int i = 0; i < n; ++i)
       if (b->desc[(size_t)i].valid) b->desc[(size_t)i].flags |= wg::kFrameEmitRgba;
@@ -993,15 +1005,22 @@ int wg_batch_run(wg_batch* b, void* stream) {
   }
   Timing& t = b->timings[b->n_runs_pending++];
   t.ran[kStageK1] = b->n_lossy > 0;
-  t.ran[kStageK2] = b->n_lossy > 0 && !b->fused;
+  // (a split remainder behind fused rounds: K2 over the remainder)
+  const int k2_from = b->fused ? b->split_from : 0;
+  t.ran[kStageK2] = b->n_lossy > 0 && (!b->fused || (b->split_parts >= 2 && b->split_from > 0));
   t.ran[kStageK7] = t.ran[kStageK3] = b->n_k3 > 0;
   t.ran[kStageK4] = b->n_alpha > 0;
   t.ran[kStageK6] = b->k6 && b->n_valid > 0;
   t.ran[kStageK5] = b->anim;
   hipEventRecord(t.ev[kStageK1], s);
   if (b->n_lossy > 0) {
-    hipError_t e = wg::launch_vp8_recon_filter(b->d_desc, b->n, b->max_mb_w, b->n_lossy > b->n_wide,
-                                               b->n_wide > 0, b->d_err, s, b->split_parts, next_epoch());
+    hipError_t e = hipSuccess;
+    const int head = b->split_parts >= 2 ? b->split_from : b->n;  // frames on the one-workgroup kernels
+    if (head > 0)
+      e = wg::launch_vp8_recon_filter(b->d_desc, head, b->max_mb_w, b->n_lossy > b->n_wide, b->n_wide > 0, b->d_err, s);
+    if (e == hipSuccess && b->split_parts >= 2)
+      e = wg::launch_vp8_recon_filter(b->d_desc + head, b->n - head, b->max_mb_w, false, false, b->d_err, s,
+                                      b->split_parts, next_epoch());
     if (e != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
   }
   hipEventRecord(t.ev[kStageK2], s);
@@ -1027,8 +1046,9 @@ int wg_batch_run(wg_batch* b, void* stream) {
         if (e != hipSuccess) return WG_STATUS_USER_ABORT;
       }
     }
-    hipError_t e = wg::launch_yuv_to_rgba(b->any_crop ? b->d_desc2 : b->d_desc, nullptr, b->n, b->max_out_w,
-                                          b->max_out_h, (b->flags & WG_FLAG_NO_FANCY_UPSAMPLING) ? 0 : 1, s);
+    hipError_t e = wg::launch_yuv_to_rgba((b->any_crop ? b->d_desc2 : b->d_desc) + k2_from, nullptr, b->n - k2_from,
+                                          b->max_out_w, b->max_out_h, (b->flags & WG_FLAG_NO_FANCY_UPSAMPLING) ? 0 : 1,
+                                          s);
     if (e != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
   }
   hipEventRecord(t.ev[kStageK7], s);
@@ -1098,7 +1118,7 @@ int wg_batch_kernel_bytes(const wg_batch* b, double* bytes, int n_bytes) {
 int wg_batch_set_emit(wg_batch* b, int separate) {
   if (!b) return WG_STATUS_INVALID_PARAM;
   if (!separate && b->any_crop) return WG_STATUS_INVALID_PARAM;  // crop windows need K2
-  if (!separate) b->split_parts = 1;  // K1's RGBA tail: the one-workgroup kernels
+  if (!separate) b->split_parts = 1, b->split_from = 0;  // K1's RGBA tail: the one-workgroup kernels
   if (b->fused == !separate) return WG_STATUS_OK;
   b->fused = !separate;
   for (FrameDesc& d : b->desc)
@@ -1112,12 +1132,15 @@ int wg_batch_set_emit(wg_batch* b, int separate) {
 
 int wg_batch_set_k1_parts(wg_batch* b, int parts) {
   if (!b || parts < 0 || parts > wg::kMaxSplitParts) return WG_STATUS_INVALID_PARAM;
-  const int p = parts == 0 ? split_k1_parts(b) : parts;
-  if (p >= 2 && b->fused) {  // the split kernel has no RGBA tail: K2 converts
+  int from = 0;
+  const int p = parts == 0 ? split_k1_parts(b, &from) : parts;
+  if (p >= 2 && from == 0 && b->fused) {  // the split kernel has no RGBA tail: K2 converts
     const int st = wg_batch_set_emit(b, 1);
     if (st != WG_STATUS_OK) return st;
   }
+  if (p >= 2 && from > 0 && b->any_crop) return WG_STATUS_OK;  // (cropped: whole rounds only)
   b->split_parts = p;
+  b->split_from = p >= 2 ? from : 0;
   return WG_STATUS_OK;
 }
 

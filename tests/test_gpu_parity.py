@@ -321,3 +321,27 @@ def test_single_frame_decode_uses_split_and_matches():
     m = manifest()["bench"]
     for p in bench_files("c3_4k")[:2] + bench_files("c3s_4k")[:1]:
         assert _sha(webp_amd.decode(open(p, "rb").read())) == m[os.path.basename(p)]["sha256"]["rgba"]
+
+
+def test_short_last_round_on_split_kernel(ctx):
+    """More frames than CUs: whole rounds of 256 on the one-workgroup kernel (RGBA in its tail),
+    the short remainder behind them on the split kernel and a K2 over the remainder alone.  258
+    1080p frames (17 quads: two slabs): every frame's RGBA = libwebp's, the head's and the
+    remainder's; then the same batch switched to separate K2 (remainder still split)."""
+    paths = bench_files("c2_1080p")
+    m = manifest()["bench"]
+    datas = [open(p, "rb").read() for p in paths]
+    n = 258
+    b = ctx.batch([datas[i % len(datas)] for i in range(n)])
+    try:
+        for sep in (False, True):
+            if sep:
+                b.set_emit(True)
+            b.run()
+            ms = b.kernel_ms()
+            assert ms[0] > 0 and ms[1] > 0, ms  # K1 (both kernels), K2 (the remainder / every frame)
+            for i in (0, 1, 100, 255, 256, 257):
+                want = m[os.path.basename(paths[i % len(paths)])]["sha256"]["rgba"]
+                assert _sha(b.rgba(i)) == want, (sep, i)
+    finally:
+        b.close()
