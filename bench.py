@@ -342,12 +342,101 @@ def cpu_baseline_libwebp(datas, seconds, threads=1, simd=True):
                                   f"host thread(s), {el:.1f}s")
 
 
-def cpu_baselines_libwebp(datas, seconds, threads):
+def _libwebp_frame_fn(wl, lib):
+    """A callable decoding one input with libwebp 1.6.0 as the workload needs it -> pixels out:
+    WebPDecode with a WebPDecoderConfig (output colorspace) for a colorspace workload, the
+    WebPAnimDecoder loop (every canvas, MODE_RGBA; libwebpdemux) for the animation one, else
+    WebPDecodeRGBAInto (see cpu_baseline_libwebp)."""
+    import ctypes as C
+    import glob
+    import PIL
+    abi = 0x0210  # WEBP_DECODER_ABI_VERSION of 1.6.0
+    if wl.get("colorspace") is not None:
+        mode = wl["colorspace"]
+
+        def dec(d):
+            cfg = (C.c_uint8 * 512)()
+            assert lib.WebPInitDecoderConfigInternal(cfg, abi)
+            ci = C.cast(cfg, C.POINTER(C.c_int32))
+            ci[40 // 4] = mode  # config.output.colorspace
+            assert lib.WebPDecode(d, C.c_size_t(len(d)), cfg) == 0
+            px = ci[44 // 4] * ci[48 // 4]
+            lib.WebPFreeDecBuffer(C.byref(cfg, 40))
+            return px
+        return dec
+    if wl.get("kind") == "anim":
+        libs = os.path.join(os.path.dirname(os.path.dirname(PIL.__file__)), "pillow.libs")
+        dmx = C.CDLL(glob.glob(os.path.join(libs, "libwebpdemux-*.so*"))[0])
+        dmx.WebPAnimDecoderNewInternal.restype = C.c_void_p
+        dmx.WebPAnimDecoderNewInternal.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+        for f in ("WebPAnimDecoderGetInfo", "WebPAnimDecoderGetNext"):
+            getattr(dmx, f).argtypes = [C.c_void_p] + [C.c_void_p] * (1 if f.endswith("Info") else 2)
+        dmx.WebPAnimDecoderHasMoreFrames.argtypes = [C.c_void_p]
+        dmx.WebPAnimDecoderDelete.argtypes = [C.c_void_p]
+
+        class _Data(C.Structure):
+            _fields_ = [("bytes", C.c_void_p), ("size", C.c_size_t)]
+
+        def dec(d):
+            opt = (C.c_int32 * 9)()
+            assert dmx.WebPAnimDecoderOptionsInitInternal(opt, 0x0107)  # WEBP_DEMUX_ABI_VERSION
+            opt[0] = 1  # MODE_RGBA
+            buf = C.c_char_p(d)
+            wd = _Data(C.cast(buf, C.c_void_p).value, len(d))
+            h = dmx.WebPAnimDecoderNewInternal(C.byref(wd), opt, 0x0107)
+            info = (C.c_uint32 * 9)()
+            dmx.WebPAnimDecoderGetInfo(h, info)
+            px = 0
+            out, ts = C.c_void_p(), C.c_int()
+            while dmx.WebPAnimDecoderHasMoreFrames(h):
+                dmx.WebPAnimDecoderGetNext(h, C.byref(out), C.byref(ts))
+                px += info[0] * info[1]
+            dmx.WebPAnimDecoderDelete(h)
+            return px
+        return dec
+    return None
+
+
+def cpu_baseline_libwebp_wl(datas, seconds, threads, simd, wl):
+    """cpu_baseline_libwebp for the colorspace / animation workloads (_libwebp_frame_fn)."""
+    import threading
+    lib, cpu, simd_ptr = _libwebp()
+    dec = _libwebp_frame_fn(wl, lib)
+    cpu.value = simd_ptr if simd else None
+    dec(datas[0])
+    pix, cnt = [0] * threads, [0] * threads
+    t0 = time.perf_counter()
+    stop = t0 + seconds
+
+    def work(t):
+        n = t
+        while time.perf_counter() < stop:
+            pix[t] += dec(datas[n % len(datas)])
+            cnt[t] += 1
+            n += threads
+
+    ths = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    el = time.perf_counter() - t0
+    cpu.value = simd_ptr
+    what = "WebPAnimDecoder, every canvas" if wl.get("kind") == "anim" else f"WebPDecode to colorspace {wl['colorspace']}"
+    return dict(value=round(sum(pix) / el / 1e6, 2), unit="MPix/s", cores=threads, kind="libwebp-1.6.0", simd=simd,
+                sample=f"{sum(cnt)} inputs of the same workload through libwebp 1.6.0 {what} "
+                       f"({'SIMD' if simd else 'plain-C'} DSP, Pillow's bundled build) on {threads} host thread(s), {el:.1f}s")
+
+
+def cpu_baselines_libwebp(datas, seconds, threads, wl=None):
     """1-core SIMD, 1-core plain-C and all-cores SIMD libwebp figures, or the reason there are none."""
+    wl = wl or {}
     try:
-        return {"simd_1_core": cpu_baseline_libwebp(datas, seconds, 1, True),
-                "plain_c_1_core": cpu_baseline_libwebp(datas, seconds, 1, False),
-                "simd_all_cores": cpu_baseline_libwebp(datas, seconds, threads, True)}
+        if wl.get("kind") == "anim" or wl.get("colorspace") is not None:
+            f = lambda th, simd: cpu_baseline_libwebp_wl(datas, seconds, th, simd, wl)  # noqa: E731
+        else:
+            f = lambda th, simd: cpu_baseline_libwebp(datas, seconds, th, simd)  # noqa: E731
+        return {"simd_1_core": f(1, True), "plain_c_1_core": f(1, False), "simd_all_cores": f(threads, True)}
     except Exception as e:  # noqa: BLE001 -- recorded in the line, never fatal
         return {"unavailable": f"{type(e).__name__}: {e}"}
 
@@ -674,10 +763,7 @@ def main():
                 out["end_to_end"]["vs_cpu_all_cores"] = round(out["end_to_end"]["value"] / cba["value"], 2)
                 out["end_to_end"]["vs_cpu_1_core"] = round(out["end_to_end"]["value"] / cb["value"], 1)
             # a real-world CPU decoder beside the restatement (not the contract's cpu_baseline)
-            if wl.get("kind") == "anim" or wl.get("colorspace") is not None:
-                lw = {"unavailable": "libwebp leg times WebPDecodeRGBAInto on stills only"}
-            else:
-                lw = cpu_baselines_libwebp(datas, max(2.0, args.cpu_seconds / 4), threads)
+            lw = cpu_baselines_libwebp(datas, max(2.0, args.cpu_seconds / 4), threads, wl)
             out["cpu_baseline_libwebp"] = lw
             if "simd_1_core" in lw:
                 out["speedup_vs_libwebp_simd_1_core"] = round(value / lw["simd_1_core"]["value"], 1)
