@@ -136,6 +136,7 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
   __shared__ int slow[2];
   __shared__ int orflag[4];                      // sync_or: a ring of flag words
   __shared__ uint2 sscr[kWaves * 64];            // a wave's straddling lookups, compacted (key, rank)
+  __shared__ int rscan[kWaves];                  // in-block copies: each wave's last run root (max-scan)
   const LLTokDesc D = kSingle ? single : descs[blockIdx.x];
   if (!D.valid) return;
   const int tid = threadIdx.x;
@@ -442,12 +443,36 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
     load_lits(tk_nxt, vprv);
     // in-block copies: sources and every pixel's state for the pointer jumping (rare in C5)
     if (blk_pc) {
+      // Runs of distance-1 copies (run-length coding, CopyBlock32b with dist 1: every pixel of the
+      // run equals the one before it) point straight at their root -- the last pixel before them
+      // that is not such a copy -- from a block-wide max-scan of root positions, so the pointer
+      // jumping below meets no chain of a run's length (log2 of it in rounds, two barriers each;
+      // alpha planes and flat lossless content are mostly runs) but only the short chains of the
+      // other distances.  Pixel 0 of a block is never an in-block copy, so a root always exists.
+      uint32_t runm = 0;
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) runm |= (uint32_t)(pk(ps, j) == kPC && aux[j] == 1u) << j;
+      const uint32_t nonrun = ~runm & 0xfu;
+      int sc = nonrun ? li0 + 31 - __builtin_clz(nonrun) : -1;  // my last root
+      sc = max(sc, __builtin_amdgcn_update_dpp(-1, sc, 0x111, 0xf, 0xf, false));  // row_shr:1
+      sc = max(sc, __builtin_amdgcn_update_dpp(-1, sc, 0x112, 0xf, 0xf, false));  // row_shr:2
+      sc = max(sc, __builtin_amdgcn_update_dpp(-1, sc, 0x114, 0xf, 0xf, false));  // row_shr:4
+      sc = max(sc, __builtin_amdgcn_update_dpp(-1, sc, 0x118, 0xf, 0xf, false));  // row_shr:8
+      sc = lane >= 16 ? max(sc, __builtin_amdgcn_readlane(sc, 15)) : sc;
+      sc = lane >= 32 ? max(sc, __builtin_amdgcn_readlane(sc, 31)) : sc;
+      sc = lane >= 48 ? max(sc, __builtin_amdgcn_readlane(sc, 47)) : sc;
+      if (lane == 63) rscan[wave] = sc;
+      int root = __builtin_amdgcn_update_dpp(-1, sc, 0x138, 0xf, 0xf, false);  // wave_shr:1: lanes before me
+      bar();
+      for (int w = 0; w < wave; ++w) root = max(root, rscan[w]);  // (wave-uniform loop)
       uint32_t stw = 0, rfw[2] = {0u, 0u};
 #pragma unroll
       for (int j = 0; j < kPer; ++j) {
         const uint32_t c = pk(ps, j);
         stw |= (uint32_t)(c == kPC ? kPendCopy : c == kPL ? kPendLookup : kKnown) << (8 * j);
-        rfw[j >> 1] |= (c == kPC ? (uint32_t)(li0 + j) - aux[j] : 0u) << (16 * (j & 1));
+        const uint32_t src = (runm >> j) & 1u ? (uint32_t)root : (uint32_t)(li0 + j) - aux[j];
+        rfw[j >> 1] |= (c == kPC ? src : 0u) << (16 * (j & 1));
+        if (!((runm >> j) & 1u)) root = li0 + j;
       }
       *reinterpret_cast<uint2*>(&ref[li0]) = make_uint2(rfw[0], rfw[1]);
       *reinterpret_cast<uint32_t*>(&st[li0]) = stw;

@@ -159,4 +159,12 @@ CASES = [
     ("three_px", 3, 4, dict()),
     ("block_edge", 4097, 10, dict(p_lit=0.2, p_copy=0.2, dist=(1, "near"), run=8)),
     ("b1", 4096 + 33, 1, dict(p_lit=0.3, palette=8)),
+    # alpha-plane shaped (ALPH streams: almost all copies, runs of distance 1 and of one row):
+    # distance-1 runs collapse to their root by the block max-scan, across blocks too
+    ("alpha_runs", 5 * 4096 + 77, 0, dict(p_lit=0.01, p_copy=0.99, dist=(1, 1, "w"), run=2500, width=1920,
+                                          palette=12)),
+    ("alpha_runs_cached", 4 * 4096 + 3, 3, dict(p_lit=0.02, p_copy=0.9, dist=(1, "w", 2), run=900, width=700,
+                                                palette=20)),
+    ("long_run", 3 * 4096 + 500, 0, dict(p_lit=0.0005, p_copy=0.9995, dist=(1,), run=20000)),
+    ("short_runs", 2 * 4096 + 11, 4, dict(p_lit=0.2, p_copy=0.6, dist=(1, 1, 1, "near"), run=3, palette=30)),
 ]

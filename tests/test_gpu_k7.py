@@ -57,6 +57,20 @@ def test_k7_c5_streams():
         assert np.array_equal(got, want), f"s{s}: {(got != want).sum()} pixels differ"
 
 
+def test_k7_c3a_alpha_streams():
+    """The alpha streams of the c3a bench frames (ALPH method 1: green-only VP8L, no cache):
+    nearly every token a distance-1 or one-row copy."""
+    import webp_amd
+    for s in (0, 5):
+        path = os.path.join(ROOT, "tests", "golden", "bench", f"c3a_4k_s{s}.webp")
+        info, (ll, coded, _) = webp_amd.alpha_parse(open(path, "rb").read())
+        toks = np.ascontiguousarray(coded.tokens, np.uint32).ravel()
+        lits = np.ascontiguousarray(coded.lits, np.uint32)
+        want = oracle_resolve(toks, lits, coded.cache_bits)
+        got = device_resolve(toks, lits, coded.cache_bits)
+        assert np.array_equal(got, want), f"s{s}: {(got != want).sum()} pixels differ"
+
+
 _STATS_CHILD = r"""
 import ctypes as C, sys, numpy as np, torch
 sys.path[:0] = [sys.argv[1], sys.argv[2]]
