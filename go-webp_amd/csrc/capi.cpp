@@ -714,23 +714,33 @@ void batch_layout(wg_batch* b, wg::StagingArena& arena, int32_t* status) {
       // rewrites the RGBA A bytes (dword read-modify-write)
       b->n_alpha++;
       if (f.ah.method == 1) {
-        b->n_k3++;
-        if (f.al.two_pass()) {
+        b->n_k3++;  // (K7 resolves every lossless stream)
+        // libwebp's 8-bit alpha streams (a color map and nothing else, or no transform) under
+        // filter none / horizontal: K4 expands the palette itself, straight from K7's output
+        f.alpha_direct = f.ah.filter <= 1 && (f.al.n_transforms == 0 ||
+                                              (f.al.n_transforms == 1 && f.al.type[0] == wg::kVP8LColorIndexing));
+        if (f.al.two_pass() && !f.alpha_direct) {
           f.off_ascratch = pl_b;
           pl_b = align_up(pl_b + (size_t)f.width * f.height * 4);
         }
         f.al.off_coded = pl_b;
         pl_b = align_up(pl_b + f.al.n_px() * 4);
-        k3 += ll_bytes(f.al);
         k7 += k7_bytes(f.al);
-        f.off_argba = pl_b;
-        pl_b = align_up(pl_b + (size_t)f.width * f.height * 4);
-        k4 += 4.0 * px;
+        if (f.alpha_direct) {
+          k4 += 4.0 * f.al.n_px() + (f.al.n_transforms ? (double)f.al.tdata[0].bytes : 0.0);
+        } else {
+          k3 += ll_bytes(f.al);
+          f.off_argba = pl_b;
+          pl_b = align_up(pl_b + (size_t)f.width * f.height * 4);
+          k4 += 4.0 * px;
+        }
       } else {
         k4 += px;
       }
-      f.off_aplane = pl_b;
-      pl_b = align_up(pl_b + (size_t)f.width * f.height);
+      if (!f.alpha_direct) {
+        f.off_aplane = pl_b;
+        pl_b = align_up(pl_b + (size_t)f.width * f.height);
+      }
       k4 += 8.0 * px;
     }
   }
@@ -865,14 +875,21 @@ int batch_upload(wg_batch* b, const wg::StagingArena& arena) {
     if (f.alpha) {
       AlphaDesc a{};
       if (f.ah.method == 1) {
-        b->lldesc.push_back(make_ll(f.al, arena, b->d_in, b->d_planes, b->d_planes + f.off_ascratch,
-                                    b->d_planes + f.off_argba, 4 * f.width));
         b->tokdesc.push_back(make_tok(f.al, arena, b->d_in, b->d_planes));
-        a.green = b->d_planes + f.off_argba;
+        if (f.alpha_direct) {
+          a.coded = reinterpret_cast<const uint32_t*>(b->d_planes + f.al.off_coded);
+          a.coded_width = f.al.coded_width;
+          a.cbits = f.al.n_transforms ? f.al.bits[0] : 0;
+          if (f.al.n_transforms) a.pal = reinterpret_cast<const uint32_t*>(b->d_in + arena.dev_offset(f.al.tdata[0]));
+        } else {
+          b->lldesc.push_back(make_ll(f.al, arena, b->d_in, b->d_planes, b->d_planes + f.off_ascratch,
+                                      b->d_planes + f.off_argba, 4 * f.width));
+          a.green = b->d_planes + f.off_argba;
+        }
       } else {
         a.raw = b->d_in + arena.dev_offset(f.araw);
       }
-      a.plane = b->d_planes + f.off_aplane;
+      a.plane = f.alpha_direct ? nullptr : b->d_planes + f.off_aplane;
       a.rgba = d.rgba;
       a.width = f.width;
       a.height = f.height;
@@ -1010,7 +1027,8 @@ int wg_batch_run(wg_batch* b, void* stream) {
   // (a split remainder behind fused rounds: K2 over the remainder)
   const int k2_from = b->fused ? b->split_from : 0;
   t.ran[kStageK2] = b->n_lossy > 0 && (!b->fused || (b->split_parts >= 2 && b->split_from > 0));
-  t.ran[kStageK7] = t.ran[kStageK3] = b->n_k3 > 0;
+  t.ran[kStageK7] = b->n_k3 > 0;
+  t.ran[kStageK3] = !b->lldesc.empty();
   t.ran[kStageK4] = b->n_alpha > 0;
   t.ran[kStageK6] = b->k6 && b->n_valid > 0;
   t.ran[kStageK5] = b->anim;
@@ -1059,7 +1077,7 @@ int wg_batch_run(wg_batch* b, void* stream) {
     if (e != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
   }
   hipEventRecord(t.ev[kStageK3], s);
-  if (b->n_k3 > 0) {
+  if (!b->lldesc.empty()) {
     hipError_t e = wg::launch_vp8l_transforms(b->d_lldesc, b->ll_groups, b->d_err, s);
     if (e != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
   }

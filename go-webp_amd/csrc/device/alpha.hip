@@ -11,11 +11,13 @@
 // decode options here keep it 0, as WebPDecode's defaults do, so pre-processed (level
 // quantized) planes are emitted as decoded.
 //
-// One 1024-thread workgroup per plane, after K2 (which wrote A = 255).  Passes:
+// After K2 / K1's tail (which wrote A = 255).  Filters none and horizontal -- what libwebp's
+// encoder picks for most planes -- go straight from the filtered bytes to the A bytes, rows in
+// parallel (alpha_rows_direct): out[y][x] = c[y-1] + sum_{i<=x} in[y][i] with c the column-0
+// prefix sums (one block scan), then a wave scan per row.  Vertical and gradient keep one
+// 1024-thread workgroup per plane and a scratch plane:
 //   1. gather the filtered bytes into `plane` (green extraction or a copy);
-//   2. unfilter in place.  The unfilters are per-byte sums mod 256 except gradient:
-//        horizontal  out[y][x] = c[y-1] + sum_{i<=x} in[y][i], c = column-0 prefix sums
-//                    -> one block scan down column 0, then a wave scan per row;
+//   2. unfilter in place:
 //        vertical    row 0 as horizontal, then out[y][x] = out[y-1][x] + in[y][x]
 //                    -> a running sum per column (threads across columns);
 //        gradient    row 0 as horizontal, then out = in + clip(L + T - TL): a wavefront
@@ -23,10 +25,11 @@
 //                    thread above via DPP / LDS, the band's top row from LDS);
 //   3. write the plane (its output window when cropping) into the A bytes (dword
 //      read-modify-write, coalesced).
-// The plane traffic is small next to K1/K2 (1 B/px vs 5.5 B/px); the gradient wavefront is
-// latency-bound (one barrier per column step) and is the slow case.
+// The gradient wavefront is latency-bound (one barrier per column step) and is the slow case.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <algorithm>
 
 #include "../device_format.h"
 #include "kernels.h"
@@ -82,13 +85,135 @@ __device__ __forceinline__ uint32_t shr1(uint32_t old, uint32_t v) {  // lane i 
   return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x138, 0xF, 0xF, false);
 }
 
+// Filtered byte x of row y: green = byte 1 of K3's pixel; raw = the ALPH payload; coded = K7's
+// coded image of an 8-bit alpha stream (ColorIndexInverseTransform, lossless.go:428-459: index
+// of pixel x in the green of coded[x >> cbits], its palette entry's green from `palg`, the
+// palette's green bytes in LDS; no palette: the coded pixel's green).
+__device__ __forceinline__ uint32_t coded_green(const AlphaDesc& F, const uint8_t* palg, uint32_t v, int x) {
+  const uint32_t g = (v >> 8) & 0xff;
+  if (!F.pal) return g;
+  const int cb = F.cbits, bpp = 8 >> cb;
+  return palg[(g >> ((x & ((1 << cb) - 1)) * bpp)) & ((1u << bpp) - 1)];
+}
+
+__device__ __forceinline__ uint32_t src_byte(const AlphaDesc& F, const uint8_t* palg, int y, int x) {
+  if (F.coded) return coded_green(F, palg, F.coded[(size_t)y * F.coded_width + (x >> F.cbits)], x);
+  const size_t i = (size_t)y * F.width + x;
+  return F.green ? (reinterpret_cast<const uint32_t*>(F.green)[i] >> 8) & 0xff : F.raw[i];
+}
+
+// Four filtered bytes x .. x+3 of row y (x % 4 == 0, x + 3 < W), packed little-endian: green as
+// one 16-byte load when the row's pixels are 16-byte aligned (`vec`); coded as one load per
+// coded pixel the four share (1, 2 or 4); raw per byte.
+__device__ __forceinline__ uint32_t src_quad(const AlphaDesc& F, const uint8_t* palg, int y, int x, bool vec) {
+  if (F.coded) {
+    const uint32_t* c = F.coded + (size_t)y * F.coded_width;
+    uint32_t v0, v1, v2, v3;
+    if (F.cbits >= 2) {
+      v0 = v1 = v2 = v3 = c[x >> F.cbits];
+    } else if (F.cbits == 1) {
+      v0 = v1 = c[x >> 1];
+      v2 = v3 = c[(x >> 1) + 1];
+    } else {
+      v0 = c[x], v1 = c[x + 1], v2 = c[x + 2], v3 = c[x + 3];
+    }
+    return coded_green(F, palg, v0, x) | coded_green(F, palg, v1, x + 1) << 8 | coded_green(F, palg, v2, x + 2) << 16 |
+           coded_green(F, palg, v3, x + 3) << 24;
+  }
+  const size_t i = (size_t)y * F.width + x;
+  if (F.green && vec) {
+    const uint4 g = *reinterpret_cast<const uint4*>(F.green + 4 * i);
+    return __builtin_amdgcn_perm(__builtin_amdgcn_perm(g.w, g.z, 0x0c0c0501u), __builtin_amdgcn_perm(g.y, g.x, 0x0c0c0501u),
+                                 0x05040100u);
+  }
+  return src_byte(F, palg, y, x) | src_byte(F, palg, y, x + 1) << 8 | src_byte(F, palg, y, x + 2) << 16 |
+         src_byte(F, palg, y, x + 3) << 24;
+}
+
+// Filters none / horizontal straight from the filtered bytes into the A bytes, one wave per
+// output row, no plane: HorizontalUnfilter_C (filters.go:130-140) is out[y][x] = out[y-1][0] +
+// sum_{i<=x} in[y][i] (mod 256), and out[y-1][0] is the column-0 prefix c[y-1], so the rows are
+// independent once c (one block scan of column 0, `rowbuf`) is known.  A lane owns 4 adjacent
+// pixels: 4 filtered bytes in, an in-lane prefix, one wave scan of the 4-sums, a running carry
+// per 256 pixels, and the RGBA window's 16 bytes read-modify-written (4 dwords where the window
+// is not 16-byte aligned).  Workgroup `part` of `parts` takes output rows part, part + parts, ...
+// (each computes c itself: H strided bytes).  12 B/px (green) at most: 4 in + 8 RMW.
+__device__ void alpha_rows_direct(const AlphaDesc& F, int part, int parts, uint8_t* rowbuf, uint8_t* palg, int* wsum,
+                                  int* total) {
+  const int W = F.width, H = F.height, tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const bool horiz = F.filter == 1;
+  if (F.coded && F.pal) {
+    if (tid < (1 << (8 >> F.cbits))) palg[tid] = (uint8_t)(F.pal[tid] >> 8);
+    __syncthreads();
+  }
+  if (horiz) {
+    const int per = (H + kThreads - 1) / kThreads, y0 = tid * per, y1 = min(H, y0 + per);
+    int s = 0;
+    for (int y = y0; y < y1; ++y) s += src_byte(F, palg, y, 0);
+    int run = block_excl_scan(s, wsum, total);
+    for (int y = y0; y < y1; ++y) {
+      run += src_byte(F, palg, y, 0);
+      rowbuf[y] = (uint8_t)run;
+    }
+    __syncthreads();
+  }
+  const bool gvec = F.green && (reinterpret_cast<uintptr_t>(F.green) & 15) == 0 && (W & 3) == 0;
+  const bool ovec = ((reinterpret_cast<uintptr_t>(F.rgba) | (uintptr_t)F.rgba_stride) & 15) == 0 && (F.win_x & 3) == 0;
+  const int xe = F.win_x + F.win_w;  // window columns [win_x, xe)
+  for (int yo = part * kWaves + wave; yo < F.win_h; yo += parts * kWaves) {
+    const int y = yo + F.win_y;
+    uint8_t* orow = F.rgba + (size_t)yo * F.rgba_stride - 4 * (size_t)F.win_x;  // (pixel x at orow + 4x)
+    uint32_t carry = horiz && y > 0 ? rowbuf[y - 1] : 0u;
+    // (horizontal: every chunk from x = 0, the prefix needs it; none: the window's chunks)
+    for (int x0 = horiz ? 0 : (F.win_x & ~255); x0 < xe; x0 += 256) {
+      const int x = x0 + 4 * lane;
+      uint32_t q = 0;
+      if (x + 3 < W) q = src_quad(F, palg, y, x, gvec);
+      else
+        for (int k = 0; k < 4 && x + k < W; ++k) q |= src_byte(F, palg, y, x + k) << (8 * k);
+      uint32_t o = q;
+      if (horiz) {  // in-lane prefix of the 4 bytes (mod 256 per byte), then the wave scan
+        const uint32_t b0 = q & 0xff, b1 = b0 + ((q >> 8) & 0xff), b2 = b1 + ((q >> 16) & 0xff), b3 = b2 + (q >> 24);
+        const uint32_t incl = (uint32_t)wave_incl_scan((int)(b3 & 0xff));
+        const uint32_t base = carry + incl - (b3 & 0xff);
+        o = ((base + b0) & 0xff) | ((base + b1) & 0xff) << 8 | ((base + b2) & 0xff) << 16 | (base + b3) << 24;
+        carry += (uint32_t)__shfl((int)incl, 63, 64);
+      }
+      if (x0 + 256 <= F.win_x) continue;
+      if (ovec && x >= F.win_x && x + 3 < xe) {
+        uint4* d = reinterpret_cast<uint4*>(orow + 4 * (size_t)x);
+        uint4 v = *d;
+        v.x = (v.x & 0x00ffffffu) | o << 24;
+        v.y = (v.y & 0x00ffffffu) | (o >> 8) << 24;
+        v.z = (v.z & 0x00ffffffu) | (o >> 16) << 24;
+        v.w = (v.w & 0x00ffffffu) | (o >> 24) << 24;
+        *d = v;
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (x + k < F.win_x || x + k >= xe) continue;
+          uint32_t* d = reinterpret_cast<uint32_t*>(orow + 4 * (size_t)(x + k));
+          *d = (*d & 0x00ffffffu) | ((o >> (8 * k)) & 0xff) << 24;
+        }
+      }
+    }
+  }
+}
+
 __global__ void __launch_bounds__(kThreads) alpha_kernel(const AlphaDesc* __restrict__ frames) {
   __shared__ uint8_t rowbuf[kMaxDim];  // horizontal: column-0 prefix; gradient: the band's top row
   __shared__ int wsum[kWaves];
   __shared__ int total;
   __shared__ uint32_t edge[2][kWaves];  // gradient: each wave's lane-63 output of the last step
+  __shared__ uint8_t palg[256];         // an 8-bit alpha stream's palette (green bytes)
   const AlphaDesc& F = frames[blockIdx.x];
   if (!F.valid) return;
+  if (F.filter <= 1) {
+    alpha_rows_direct(F, blockIdx.y, gridDim.y, rowbuf, palg, wsum, &total);
+    return;
+  }
+  if (blockIdx.y > 0) return;  // (vertical / gradient: the whole plane in one workgroup)
   const int W = F.width, H = F.height, tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const size_t n = (size_t)W * H;
@@ -213,7 +338,10 @@ __global__ void __launch_bounds__(kThreads) alpha_kernel(const AlphaDesc* __rest
 
 hipError_t launch_alpha(const AlphaDesc* d_frames, int n_frames, hipStream_t stream) {
   if (n_frames <= 0) return hipSuccess;
-  hipLaunchKernelGGL(alpha_kernel, dim3(n_frames), dim3(kThreads), 0, stream, d_frames);
+  // filters none / horizontal run rows on `parts` workgroups per plane (the chip holds two
+  // 1024-thread workgroups per CU); vertical / gradient planes use the first only
+  const int parts = std::max(1, std::min(8, 512 / n_frames));
+  hipLaunchKernelGGL(alpha_kernel, dim3(n_frames, parts), dim3(kThreads), 0, stream, d_frames);
   return hipGetLastError();
 }
 

@@ -118,17 +118,22 @@ struct LLDesc {
 };
 static_assert(sizeof(LLDesc) == 192, "LLDesc must be 192 bytes");
 
-// One ALPH plane for K4 (alpha.hip).  Exactly one of green / raw is set.
+// One ALPH plane for K4 (alpha.hip).  Exactly one of green / raw / coded is set.
 struct AlphaDesc {
   const uint8_t* green;  // K3's RGBA output of the lossless alpha stream: byte 1 of each pixel
   const uint8_t* raw;    // method 0: the filtered bytes, width*height
-  uint8_t* plane;        // width*height scratch: filtered -> unfiltered alpha
+  uint8_t* plane;        // width*height scratch: filtered -> unfiltered alpha (vertical / gradient)
   uint8_t* rgba;         // the frame's RGBA output; K4 writes its A bytes
   int32_t width, height, rgba_stride, filter;  // plane size; filter: 0 none, 1 horizontal, 2 vertical, 3 gradient
   int32_t valid, win_x, win_y, win_w;           // the output window of the plane (cropping)
-  int32_t win_h, pad0, pad1, pad2;
+  int32_t win_h, cbits, coded_width, pad0;
+  // a lossless alpha stream whose only transform is color indexing (or that has none), filter
+  // none / horizontal: K7's coded image read directly (K3 skipped) -- green of pal[index of
+  // pixel x in coded[x >> cbits]], or of the coded pixel itself when pal is null
+  const uint32_t* coded;
+  const uint32_t* pal;   // 1 << (8 >> cbits) ARGB entries (ExpandColorMap's padded map)
 };
-static_assert(sizeof(AlphaDesc) == 80, "AlphaDesc must be 80 bytes");
+static_assert(sizeof(AlphaDesc) == 96, "AlphaDesc must be 96 bytes");
 
 // One frame's output conversion for K6 (emit.hip): RGBA window -> WEBP_CSP_MODE bytes.
 struct EmitDesc {

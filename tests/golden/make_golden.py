@@ -315,6 +315,12 @@ def alpha_pattern(H, W, seed, kind):
         a = xx * 5 + yy * 7 + (rng.integers(0, 3, (H, W)))
     elif kind == "lv":
         a = ((xx // 7 + yy // 5) % 4) * 85
+    elif kind == "bin":  # two levels: a 2-colour palette, eight pixels per coded pixel
+        a = ((xx // 9 + yy // 6) % 3 == 0) * 255
+    elif kind == "rl":  # 40 random levels: a palette of more than 16 colours
+        a = rng.integers(0, 40, (H, W)) * 6
+    elif kind == "many":  # 61 levels: a palette of more than 16 colours, one pixel per coded pixel
+        a = ((xx * 2 + yy) % 61) * 4
     else:
         a = rng.integers(0, 256, (H, W))
     return np.concatenate([img, (a % 256).astype(np.uint8)[..., None]], -1)
@@ -736,6 +742,17 @@ ALPHA_CASES = [
     ("a_ll_q50_80x80", lambda: alpha_pattern(80, 80, 40, "g"), {"alpha_filtering": 1, "alpha_quality": 50}, None),
     ("a_ll_1x1", lambda: alpha_pattern(1, 1, 41, "n"), {}, None),
 ]
+# section alpha_r5 (added to "alpha"): alpha streams under filters none / horizontal -- 8-bit ones
+# (a palette, 1 or 8 pixels per coded pixel), which K4 expands straight from K7's output (no K3),
+# and predictor-coded ones (K3, then K4 from its RGBA)
+ALPHA_CASES_R5 = [
+    ("a_ll_bin_none_70x45", lambda: alpha_pattern(45, 70, 45, "bin"), {"alpha_filtering": 0}, (1, 0)),
+    ("a_ll_bin_h_133x40", lambda: alpha_pattern(40, 133, 46, "bin"), {"alpha_filtering": 0, "set_filter": 1}, (1, 1)),
+    ("a_ll_many_none_75x50", lambda: alpha_pattern(50, 75, 47, "many"), {"alpha_filtering": 0}, (1, 0)),
+    ("a_ll_many_h_66x90", lambda: alpha_pattern(90, 66, 48, "many"), {"alpha_filtering": 0, "set_filter": 1}, (1, 1)),
+    ("a_ll_rl_none_61x29", lambda: alpha_pattern(29, 61, 49, "rl"), {"alpha_filtering": 0}, (1, 0)),
+    ("a_ll_rl_h_64x33", lambda: alpha_pattern(33, 64, 50, "rl"), {"alpha_filtering": 0, "set_filter": 1}, (1, 1)),
+]
 
 BENCH_CASES = [
     # name, H, W, seeds, kwargs, generator  
@@ -768,15 +785,16 @@ def main(argv):
     """argv: sections to (re)generate among lossy, lossy_extra, lossless, alpha, modes, anim, bench (default: all);
     the manifest entries of the other sections are kept."""
     sections = set(argv) or {"lossy", "lossy_extra", "lossless", "alpha", "modes", "anim", "bench", "bench_c5x",
-                             "bench_c3s", "bench_c3a", "bench_anim", "bench_modes", "fuzz"}
+                             "bench_c3s", "bench_c3a", "bench_anim", "bench_modes", "fuzz", "alpha_r5"}
     os.makedirs(os.path.join(HERE, "lossy"), exist_ok=True)
     os.makedirs(os.path.join(HERE, "lossless"), exist_ok=True)
     os.makedirs(os.path.join(HERE, "bench"), exist_ok=True)
     mpath = os.path.join(HERE, "manifest.json")
     manifest = json.load(open(mpath)) if os.path.exists(mpath) else {}
     manifest["libwebp"] = "1.6.0 (Pillow 12.2.0 bundle, plain-C DSP)"
-    for sec in sections - {"bench_c5x", "bench_c3s", "bench_c3a", "bench_modes"}:  # (these add to "bench")
+    for sec in sections - {"bench_c5x", "bench_c3s", "bench_c3a", "bench_modes", "alpha_r5"}:  # (these add)
         manifest[sec] = {}
+    manifest.setdefault("alpha", {})
     manifest.setdefault("bench", {})
     if "alpha" in sections:
         manifest["alpha_errors"] = {}
@@ -804,7 +822,8 @@ def main(argv):
         manifest["lossless"][name] = dict(bytes=len(data), width=img.shape[1], height=img.shape[0], encoder=kw)
         print(name, len(data), flush=True)
     os.makedirs(os.path.join(HERE, "alpha"), exist_ok=True)
-    for name, fn, kw, want in ALPHA_CASES if "alpha" in sections else []:
+    for name, fn, kw, want in (ALPHA_CASES if "alpha" in sections else []) + \
+            (ALPHA_CASES_R5 if sections & {"alpha", "alpha_r5"} else []):
         img = fn()
         kw = dict(kw)
         filt = kw.pop("set_filter", None)

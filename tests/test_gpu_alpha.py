@@ -81,3 +81,34 @@ def test_alpha_single_decode_dropin():
     np.testing.assert_array_equal(webp_amd.decode(data), gold["rgba"])
     data, gold = load_lossy("alpha_64x48")
     np.testing.assert_array_equal(webp_amd.decode(data), gold["rgba"])
+
+
+@pytest.mark.parametrize("name", ["a_ll_h_130x70", "a_raw_h_71x33", "a_ll_none_33x65", "a_raw_none_40x30",
+                                  "a_ll_v_97x81", "a_raw_g_64x64", "a_ll_best_g_96x64", "a_ll_levels_90x60",
+                                  "a_ll_bin_h_133x40", "a_ll_bin_none_70x45", "a_ll_rl_h_64x33", "a_ll_many_h_66x90"])
+def test_alpha_crop_windows_every_filter(ctx, name):
+    """K4 writes the A bytes of a crop window: the direct row path (filters none / horizontal:
+    rows from the column-0 prefix, window columns at any offset, 16-byte and dword stores; from
+    raw bytes, from K3's RGBA, or -- 8-bit alpha streams: a palette of 1 / 2 / 8 pixels per
+    coded pixel, or no transform -- from K7's coded image with K3 skipped) and the plane path
+    (vertical / gradient), in batches large enough and small enough to change the
+    rows-per-workgroup split.  Against the CPU oracle's WebPDecode with the same options."""
+    from oracle_lib import oracle_output
+    data = load_alpha(name)[0]
+    f = webp_amd.features(data)
+    W, H = f.width, f.height
+    crops = [(0, 0, W, H), (2, 1, W - 2, H - 1), (4, 6, min(17, W - 4), min(9, H - 6)), (8, 0, W - 8, 3),
+             (W - 5, H - 4, 5, 4)]
+    for crop in crops:
+        want = oracle_output(data, mode=1, crop=crop)
+        opts = webp_amd.options(1, crop)
+        for n in (1, 3, 70):
+            b = ctx.batch([data] * n, opts=opts)
+            try:
+                assert (b.status == 0).all()
+                b.run()
+                for i in sorted({0, n - 1}):
+                    got = b.download(i)
+                    np.testing.assert_array_equal(got.reshape(want.shape), want, err_msg=f"{name} {crop} n={n} i={i}")
+            finally:
+                b.close()

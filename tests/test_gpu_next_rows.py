@@ -50,6 +50,7 @@ def test_c3a_alpha_frames(ctx, mode):
             b.run()
         ms = b.kernel_ms()
         assert ms[0] > 0 and ms[3] > 0 and ms[4] > 0, ms  # K1, K4 and the alpha streams' K7
+        assert ms[2] == 0, ms  # 8-bit alpha streams (a color map only): K4 expands them from K7's output, no K3
         key = "rgba_point" if mode == "point" else "rgba"
         for i in range(n):
             want = m[os.path.basename(paths[i % 8])]["sha256"][key]
