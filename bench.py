@@ -46,8 +46,9 @@ WORKLOADS = {
     "c3a": dict(prefix="c3a_4k", name="c3a_4k_alpha_x256", target="alpha_kernel",
                 desc="3840x2160 VP8-lossy + ALPH (lossless-compressed feathered cut-out alpha), deblock on, batch 256: "
                      "K1 + the alpha streams' K7 / K3 + K4 (SURVEY 8 f2)"),
-    "c3rgb565": dict(prefix="c3_4k", name="c3_4k_rgb565_x256", target="emit_kernel", colorspace=6,
-                     desc="C3's frames decoded to MODE_RGB_565 (fancy upsampling), batch 256: K1 + K6 (SURVEY 8 f4)"),
+    "c3rgb565": dict(prefix="c3_4k", name="c3_4k_rgb565_x256", target="vp8_recon_filter_kernel", colorspace=6,
+                     desc="C3's frames decoded to MODE_RGB_565 (fancy upsampling), batch 256: K1, whose tail writes "
+                          "the 565 pixels directly (no RGBA copy, no K6) (SURVEY 8 f4)"),
     "anim": dict(prefix="anim_1080p_x64", name="anim_1080p_x64", target="anim_compose_kernel", kind="anim",
                  desc="one 64-frame 1920x1080 lossy animation per GPU (WebPAnimEncoder: blended sub-rectangles), "
                       "resident: frames K1..K4, 64 canvases K5; value = canvas pixels / s (SURVEY 8 f3)"),

@@ -210,7 +210,8 @@ struct wg_batch {
   FrameDesc* d_desc = nullptr;
   LLDesc* d_lldesc = nullptr;
   AlphaDesc* d_adesc = nullptr;
-  int n_lossy = 0, n_lossless = 0, n_alpha = 0, n_k3 = 0;
+  int n_lossy = 0, n_lossless = 0, n_alpha = 0, n_k3 = 0, n_k6 = 0;  // n_k6: frames K6 converts
+  bool tail_modes = true, no_tail = false;  // no_tail: frames emitted directly in a mode K1's tail lacks
   wg_decoder_options opt{};          // output colorspace, cropping, flip (f4)
   bool any_crop = false;             // K2 reads compact cropped planes through desc2
   bool fused = false;                // lossy RGBA emitted by K1's tail (wg::kFrameEmitRgba), no K2 launch
@@ -647,12 +648,18 @@ void batch_layout(wg_batch* b, wg::StagingArena& arena, int32_t* status) {
   // layout of the planes / RGBA, and the algorithmic bytes per kernel
   size_t pl_b = 0, rg_b = 0;
   double k1 = 0, k2 = 0, k3 = 0, k4 = 0, k7 = 0;
+  // K6: a non-RGBA colorspace or flip.  Lossy frames without alpha or crop window leave the
+  // YUV -> RGB strips (K1's tail or K2) in the output colorspace, straight into their output slot:
+  // no RGBA copy for them, and K6 converts only the others.
+  b->k6 = !(b->opt.colorspace == 1 && !b->opt.flip);
+  const int obpp = wg::output_bpp(b->opt.colorspace);
   for (int i = 0; i < n; ++i) {
     FrameParse& f = b->fp[(size_t)i];
     if (status) status[i] = f.status;
     if (f.status != WG_STATUS_OK) continue;
+    f.emit_direct = b->k6 && !f.lossless && !f.alpha && !f.cropped;
     f.off_rgba = rg_b;
-    rg_b = align_up(rg_b + (size_t)f.rgba_w * f.rgba_h * 4);
+    if (!f.emit_direct) rg_b = align_up(rg_b + (size_t)f.rgba_w * f.rgba_h * 4);
     b->max_w = std::max(b->max_w, f.width);
     b->max_h = std::max(b->max_h, f.height);
     b->max_out_w = std::max(b->max_out_w, f.out_w);
@@ -706,9 +713,10 @@ void batch_layout(wg_batch* b, wg::StagingArena& arena, int32_t* status) {
     // MB-padded planes (or, with its RGBA tail, the RGBA); K2 reads cropped planes, writes RGBA.
     const double k1_in = (double)nmb * sizeof(MbRec) + inf.mb_h * 4.0 + (double)f.n_blocks * 32.0;
     k1 += k1_in + nmb * 384.0;
-    b->k1_fused_bytes += k1_in + 4.0 * inf.width * (double)inf.height;
+    const double obytes = f.emit_direct ? (double)obpp : 4.0;  // output bytes per pixel of the strips
+    b->k1_fused_bytes += k1_in + obytes * inf.width * (double)inf.height;
     const double opx = (double)f.out_w * f.out_h;
-    k2 += opx + 2.0 * ((f.out_w + 1) / 2) * (double)((f.out_h + 1) / 2) + 4.0 * opx;
+    k2 += opx + 2.0 * ((f.out_w + 1) / 2) * (double)((f.out_h + 1) / 2) + obytes * opx;
     if (f.alpha) {
       // K4 reads the filtered alpha (raw bytes, or K3's RGBA of the alpha stream) and
       // rewrites the RGBA A bytes (dword read-modify-write)
@@ -744,12 +752,11 @@ void batch_layout(wg_batch* b, wg::StagingArena& arena, int32_t* status) {
       k4 += 8.0 * px;
     }
   }
-  // K6: non-RGBA colorspace or flip -> one output window per frame in d_out (reads the RGBA
-  // window, writes bpp bytes per pixel)
+  // K6 batches: one output window per frame in d_out; K6 reads the RGBA window of the frames not
+  // emitted directly and writes bpp bytes per pixel
   double k6 = 0;
-  b->k6 = !(b->opt.colorspace == 1 && !b->opt.flip);
   if (b->k6) {
-    b->out_bpp = wg::output_bpp(b->opt.colorspace);
+    b->out_bpp = obpp;
     b->off_out.assign((size_t)n, 0);
     size_t ob = 0;
     for (int i = 0; i < n; ++i) {
@@ -757,6 +764,8 @@ void batch_layout(wg_batch* b, wg::StagingArena& arena, int32_t* status) {
       if (f.status != WG_STATUS_OK) continue;
       b->off_out[(size_t)i] = ob;
       ob = align_up(ob + (size_t)b->out_bpp * f.out_w * f.out_h);
+      if (f.emit_direct) continue;
+      b->n_k6++;
       b->k6_maxpx = std::max(b->k6_maxpx, f.out_w * f.out_h);
       k6 += (4.0 + b->out_bpp) * f.out_w * (double)f.out_h;
     }
@@ -903,13 +912,34 @@ int batch_upload(wg_batch* b, const wg::StagingArena& arena) {
       b->adesc.push_back(a);
     }
   }
+  // K6 batches: the output slots; frames emitted directly point K1's tail / K2 at theirs
+  if (b->k6) {
+    b->d_out = static_cast<uint8_t*>(cache.get(b->out_bytes));
+    b->d_edesc = static_cast<EmitDesc*>(cache.get(sizeof(EmitDesc) * (size_t)n));
+    if (!b->d_out || !b->d_edesc) return WG_STATUS_OUT_OF_MEMORY;
+    for (int i = 0; i < n; ++i) {
+      const FrameParse& f = b->fp[(size_t)i];
+      if (f.status != WG_STATUS_OK || !f.emit_direct) continue;
+      FrameDesc& d = b->desc[(size_t)i];
+      d.rgba = b->d_out + b->off_out[(size_t)i];
+      d.rgba_stride = b->out_bpp * f.out_w;
+      d.emit = b->opt.colorspace + 1;
+      d.emit_flip = b->opt.flip ? 1 : 0;
+    }
+  }
   // Fewer frames than CUs: K1's split kernel (split_k1_parts); it has no RGBA tail, K2 converts.
   b->split_parts = split_k1_parts(b, &b->split_from);
   // Full-frame RGBA (no crop window anywhere in the batch): K1 converts each frame in its
   // own tail instead of a separate K2 launch (wg_batch_set_emit() switches back); a split
   // remainder behind whole rounds converts in a K2 over its frames alone.
   if (b->split_parts >= 2 && b->split_from > 0 && b->any_crop) b->split_parts = 1, b->split_from = 0;
-  b->fused = !b->any_crop && (b->split_parts < 2 || b->split_from > 0);
+  // K1's tail writes RGBA and RGB_565 (rgbA = RGBA for the opaque frames it emits directly); the
+  // other output colorspaces of directly emitted frames convert in K2 (yuv_rgba_strip.h store_out)
+  const int cs = b->opt.colorspace;
+  b->tail_modes = cs == 1 || cs == 7 || cs == 6;
+  for (int i = 0; i < n && !b->tail_modes; ++i) b->no_tail |= b->fp[(size_t)i].emit_direct;
+  if (b->no_tail && b->split_parts >= 2 && b->split_from > 0) b->split_parts = 1, b->split_from = 0;
+  b->fused = !b->any_crop && !b->no_tail && (b->split_parts < 2 || b->split_from > 0);
   if (b->fused)
     for (int i = 0; i < n; ++i)
       if (b->desc[(size_t)i].valid) b->desc[(size_t)i].flags |= wg::kFrameEmitRgba;
@@ -928,15 +958,12 @@ int batch_upload(wg_batch* b, const wg::StagingArena& arena) {
       d2.height = f.out_h;
     }
   }
-  // K6's descriptors: every valid frame's RGBA window -> its slot of d_out
+  // K6's descriptors: the RGBA window of every frame not emitted directly -> its slot of d_out
   if (b->k6) {
-    b->d_out = static_cast<uint8_t*>(cache.get(b->out_bytes));
-    b->d_edesc = static_cast<EmitDesc*>(cache.get(sizeof(EmitDesc) * (size_t)n));
-    if (!b->d_out || !b->d_edesc) return WG_STATUS_OUT_OF_MEMORY;
     b->edesc.assign((size_t)n, EmitDesc{});
     for (int i = 0; i < n; ++i) {
       const FrameParse& f = b->fp[(size_t)i];
-      if (f.status != WG_STATUS_OK) continue;
+      if (f.status != WG_STATUS_OK || f.emit_direct) continue;
       const FrameDesc& d = b->desc[(size_t)i];
       // the output window inside the RGBA (window_ptr: lossless crops are sub-rectangles)
       const uint8_t* src = d.rgba + (size_t)f.win_y * d.rgba_stride + 4 * (size_t)f.win_x;
@@ -1030,7 +1057,7 @@ int wg_batch_run(wg_batch* b, void* stream) {
   t.ran[kStageK7] = b->n_k3 > 0;
   t.ran[kStageK3] = !b->lldesc.empty();
   t.ran[kStageK4] = b->n_alpha > 0;
-  t.ran[kStageK6] = b->k6 && b->n_valid > 0;
+  t.ran[kStageK6] = b->k6 && b->n_k6 > 0;
   t.ran[kStageK5] = b->anim;
   hipEventRecord(t.ev[kStageK1], s);
   if (b->n_lossy > 0) {
@@ -1137,7 +1164,7 @@ int wg_batch_kernel_bytes(const wg_batch* b, double* bytes, int n_bytes) {
 
 int wg_batch_set_emit(wg_batch* b, int separate) {
   if (!b) return WG_STATUS_INVALID_PARAM;
-  if (!separate && b->any_crop) return WG_STATUS_INVALID_PARAM;  // crop windows need K2
+  if (!separate && (b->any_crop || b->no_tail)) return WG_STATUS_INVALID_PARAM;  // crop windows / modes K2 emits
   if (!separate) b->split_parts = 1, b->split_from = 0;  // K1's RGBA tail: the one-workgroup kernels
   if (b->fused == !separate) return WG_STATUS_OK;
   b->fused = !separate;
@@ -1551,6 +1578,7 @@ int wg_batch_download_rgba(wg_batch* b, int i, uint8_t* rgba, int stride) {
   if (!b || i < 0 || i >= b->n || !rgba) return WG_STATUS_INVALID_PARAM;
   if (b->fp[i].status != WG_STATUS_OK) return b->fp[i].status;
   const FrameParse& f = b->fp[i];
+  if (f.emit_direct) return WG_STATUS_UNSUPPORTED_FEATURE;  // emitted in the batch's colorspace only
   if (stride < 4 * f.out_w) return WG_STATUS_INVALID_PARAM;
   int st = batch_sync(b);
   if (st != WG_STATUS_OK) return st;

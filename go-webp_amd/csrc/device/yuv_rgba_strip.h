@@ -31,6 +31,7 @@
 #include <stdint.h>
 
 #include "../device_format.h"
+#include "emit_px.h"
 
 namespace wg {
 namespace strip {
@@ -236,6 +237,60 @@ __device__ __forceinline__ void store_group(__amdgpu_buffer_rsrc_t o, uint32_t o
   }
 }
 
+// Direct emission (FrameDesc::emit = 1 + WEBP_CSP_MODE, emit_flip): a lossy frame without alpha
+// leaves the strips in its output colorspace, so no RGBA copy is written and read back (K6).  The
+// group's four pixels in the mode (emit_px.h), bpp bytes each, at byte offset roff + bpp * x: one
+// 16 / 12 / 8-byte store for a whole group, per-pixel stores (dropped past the width through the
+// buffer range) otherwise.  The frames emitted directly are opaque (a = 255), where each
+// premultiplied mode equals its plain form (emit_px: no premultiply at a = 255; the 4444 one is
+// the identity at a = 0xf).  Only the conversion is switched on the mode: the store code is shared.
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+template <int M>
+__device__ __forceinline__ u32x4 conv4(u32x4 p) {
+  return u32x4{emit_px<M>(p.x), emit_px<M>(p.y), emit_px<M>(p.z), emit_px<M>(p.w)};
+}
+
+// em = FrameDesc::emit (wave-uniform): 0 RGBA, else 1 + the mode.  kAllModes false (K1's tail,
+// whose code size is kept down: the switch sits at each of its eight unrolled store sites): RGBA,
+// rgbA and RGB_565 only -- capi.cpp sends batches in the other modes through K2.
+template <int kAux, bool kAllModes>
+__device__ __forceinline__ void store_out(__amdgpu_buffer_rsrc_t o, int em, uint32_t roff, int x, u32x4 px, int nvalid,
+                                          bool full) {
+  int bpp = 4;
+  u32x4 c = px;
+  if (kAllModes) {
+    switch (em) {
+      case 1: c = conv4<0>(px), bpp = 3; break;            // RGB
+      case 3: c = conv4<2>(px), bpp = 3; break;            // BGR
+      case 4: case 9: c = conv4<3>(px); break;             // BGRA, bgrA
+      case 5: case 10: c = conv4<4>(px); break;            // ARGB, Argb
+      case 6: case 11: c = conv4<5>(px), bpp = 2; break;   // RGBA_4444, rgbA_4444
+      case 7: c = conv4<6>(px), bpp = 2; break;            // RGB_565
+      default: break;                                      // RGBA, rgbA
+    }
+  } else if (em == 7) {
+    c = conv4<6>(px), bpp = 2;
+  }
+  if (bpp == 4) {
+    store_group<kAux>(o, roff + 4u * (uint32_t)x, c, nvalid, full);
+    return;
+  }
+  const uint32_t off = roff + (uint32_t)(bpp * x);
+  if (full) {
+    if (bpp == 2) __builtin_amdgcn_raw_buffer_store_b64(u32x2{c.x | c.y << 16, c.z | c.w << 16}, o, off, 0, kAux);
+    else __builtin_amdgcn_raw_buffer_store_b96(u32x3{c.x | c.y << 24, c.y >> 8 | c.z << 16, c.z >> 16 | c.w << 8}, o, off, 0, kAux);
+    return;
+  }
+  const uint32_t ov[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t a = nvalid > k ? off + (uint32_t)(bpp * k) : kOffDrop;
+    __builtin_amdgcn_raw_buffer_store_b16((unsigned short)ov[k], o, a, 0, 0);
+    if (bpp == 3) __builtin_amdgcn_raw_buffer_store_b8((unsigned char)(ov[k] >> 16), o, nvalid > k ? a + 2 : kOffDrop, 0, 0);
+  }
+}
+
 // Strips and bands of a frame: strip tx covers x in [1024 tx, 1024 tx + 1024), band j the
 // row pairs [kPairs j, kPairs j + kPairs) (fancy: pair p = output rows 2p-1, 2p; point:
 // rows 2p, 2p+1).
@@ -245,13 +300,17 @@ __device__ __forceinline__ int n_bands(int H, bool fancy) {
   return (npairs + kPairs - 1) / kPairs;
 }
 
-template <bool kFancy, int kAux>
+template <bool kFancy, int kAux, bool kAllModes = true>
 __device__ __forceinline__ void convert_strip(const FrameDesc& F, int tx, int band, int lane) {
   const int W = F.width, H = F.height;
   const int uv_w = (W + 1) >> 1, uv_h = (H + 1) >> 1;
   const int xl = tx * kStripPx + 4 * lane;  // group k pixel x = xl + 256k
   const int cb0 = xl >> 1;
-  const bool aligned = ((F.rgba_stride & 15) == 0) && ((reinterpret_cast<uintptr_t>(F.rgba) & 15) == 0);
+  // output: RGBA, or (emit) the frame's mode, rows bottom-up with emit_flip
+  int em = __builtin_amdgcn_readfirstlane(F.emit);
+  const bool flip = __builtin_amdgcn_readfirstlane(F.emit_flip) != 0;
+  const int bpp = em ? bpp_of(em - 1) : 4;
+  const bool aligned = ((F.rgba_stride & (bpp == 4 ? 15 : 3)) == 0) && ((reinterpret_cast<uintptr_t>(F.rgba) & 15) == 0);
   // per group k, from the wave's first pixel x0 (scalar): some lane's group lies in the frame
   // (else skipped), every lane's group is whole (one 16-byte store each)
   const int x0 = tx * kStripPx;
@@ -260,6 +319,7 @@ __device__ __forceinline__ void convert_strip(const FrameDesc& F, int tx, int ba
   const gptr<const uint8_t> U = as_global(static_cast<const uint8_t*>(F.u));
   const gptr<const uint8_t> V = as_global(static_cast<const uint8_t*>(F.v));
   const int ys = F.y_stride, uvs = F.uv_stride, os = F.rgba_stride;
+  auto roff = [&](int y) { return (uint32_t)((flip ? H - 1 - y : y) * os); };
   // (the descriptor from readfirstlane'd values: F is one frame per workgroup, but where the
   // compiler cannot prove it uniform (K2 picks `single` or frames[y]) a VGPR descriptor
   // would wrap every store in a readfirstlane waterfall loop)
@@ -294,6 +354,7 @@ __device__ __forceinline__ void convert_strip(const FrameDesc& F, int tx, int ba
     // its code grew K1 by 8 KB: not kept.)
     auto pair_step = [&](int p, const ChromaCols& prv) __attribute__((always_inline)) {
       const int ya = 2 * p - 1, yb = 2 * p;
+      asm volatile("" : "+s"(em));  // (no loop copy per output mode: only the conversion switches)
       uint32_t yA[kGroups], yB[kGroups];
       load_luma(ya, yA);
       load_luma(yb, yB);
@@ -304,8 +365,8 @@ __device__ __forceinline__ void convert_strip(const FrameDesc& F, int tx, int ba
       for (int k = 0; k < kGroups; ++k) {
         const int x = xl + 256 * k;
         if (!live(k)) continue;
-        if (ya >= 0) store_group<kAux>(out, (uint32_t)(ya * os + 4 * x), convert_group(prv, cur, k, yA[k]), W - x, full(k));
-        if (yb < H) store_group<kAux>(out, (uint32_t)(yb * os + 4 * x), convert_group(cur, prv, k, yB[k]), W - x, full(k));
+        if (ya >= 0) store_out<kAux, kAllModes>(out, em, roff(ya), x, convert_group(prv, cur, k, yA[k]), W - x, full(k));
+        if (yb < H) store_out<kAux, kAllModes>(out, em, roff(yb), x, convert_group(cur, prv, k, yB[k]), W - x, full(k));
       }
       raw_cur = raw_next;
       // K1's tail yields the SIMD for a moment after each pair: its denser packed code otherwise
@@ -322,6 +383,7 @@ __device__ __forceinline__ void convert_strip(const FrameDesc& F, int tx, int ba
     if (p0 >= npairs) return;
     const int p1 = min(p0 + kPairs, npairs);
     for (int p = p0; p < p1; ++p) {
+      asm volatile("" : "+s"(em));
       uint32_t yA[kGroups], yB[kGroups];
       load_luma(2 * p, yA);
       load_luma(2 * p + 1, yB);
@@ -340,7 +402,7 @@ __device__ __forceinline__ void convert_strip(const FrameDesc& F, int tx, int ba
           const uint32_t yw = r ? yB[k] : yA[k];
           const uint2 a = yuv_to_rgba2(luma_lanes(yw, 0, 1), u0, v0), b = yuv_to_rgba2(luma_lanes(yw, 2, 3), u1, v1);
           const u32x4 px{a.x, a.y, b.x, b.y};
-          store_group<kAux>(out, (uint32_t)(yr * os + 4 * x), px, W - x, full(k));
+          store_out<kAux, kAllModes>(out, em, roff(yr), x, px, W - x, full(k));
         }
       }
     }

@@ -73,7 +73,9 @@ struct FrameDesc {
   int32_t y_stride, uv_stride, rgba_stride, filter_type;
   int32_t flags, valid, blocks_bytes, pad2;  // blocks_bytes: size of `blocks` (K1 bounds)
   uint32_t* gprog;  // split kernel: one progress flag per part boundary, 128 B apart (kGProgBytes)
-  int32_t pad3[2];
+  // K1's tail / K2 output: 0 RGBA at `rgba`; else 1 + the WEBP_CSP_MODE written straight into
+  // `rgba` (the frame's output slot, rgba_stride = bpp * width), rows bottom-up if emit_flip
+  int32_t emit, emit_flip;
 };
 static_assert(sizeof(FrameDesc) == 128, "FrameDesc must be 128 bytes");
 

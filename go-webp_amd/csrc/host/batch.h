@@ -46,6 +46,7 @@ struct FrameParse {
   LLMeta al;
   Region araw;
   bool alpha_direct = false;  // capi.cpp: K4 reads the alpha stream's coded image itself (no K3)
+  bool emit_direct = false;   // capi.cpp: K1's tail / K2 write the output colorspace itself (no K6)
   // output (cropping, f4): out_w x out_h, taken at (win_x, win_y) of the frame's RGBA buffer
   // (rgba_w x rgba_h: the window itself for lossy frames, the whole frame for lossless)
   int out_w = 0, out_h = 0, win_x = 0, win_y = 0, rgba_w = 0, rgba_h = 0;

@@ -235,8 +235,10 @@ int wg_batch_frame_status(const wg_batch* b, int i);
 int64_t wg_batch_pixels(const wg_batch* b);
 
 /* Copy results of frame i back to host: RGBA of the output window (stride >= 4*width; no flip,
- * whatever the batch's colorspace), the batch's colorspace / flip via K6 (wg_batch_download,
- * stride >= bpp*width), and/or the full frame's Y/U/V planes (strides width, (width+1)/2).
+ * whatever the batch's colorspace -- except a lossy frame without alpha or crop window in a
+ * non-RGBA / flipped batch, which is written straight in the batch's colorspace and has no RGBA
+ * copy: UNSUPPORTED_FEATURE), the batch's colorspace / flip (wg_batch_download, stride >=
+ * bpp*width), and/or the full frame's Y/U/V planes (strides width, (width+1)/2).
  * wg_batch_download_rgba's destination may also be device memory (e.g. a torch tensor on the
  * batch's device): the copy is then device to device and the frame never crosses PCIe. */
 int wg_batch_download_rgba(wg_batch* b, int i, uint8_t* rgba, int stride);

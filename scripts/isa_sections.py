@@ -4,7 +4,8 @@
 Copies vp8_recon_filter.hip with `asm volatile(";MARK name")` inserted before the section
 comments listed below, compiles it for gfx950 and counts VALU/SALU/LDS/VMEM instructions
 between markers.  Static counts (loops and both filter variants counted once), useful for
-before/after comparisons of a change.
+before/after comparisons of a change.  KERNEL (env) picks the instantiation: default the
+product kernel of c3 / c3s (vp8_recon_filter_kernel<false, false>).
 """
 import collections
 import glob
@@ -84,16 +85,30 @@ def main():
         meta = {}
         dump = os.environ.get("DUMP_SECTION")  # write that section's ISA to /tmp/isa_<name>.s
         out = open(f"/tmp/isa_{dump}.s", "w") if dump else None
+        # one instantiation only (the c3 product kernel by default: no global columns, not split)
+        want = os.environ.get("KERNEL", "vp8_recon_filter_kernelILb0ELb0E")
+        inside = False
         for line in open(asm):
+            if re.match(r"^_Z\w+:", line):
+                inside = want in line
+                cur = "pre"
+                continue
+            if line.startswith(".Lfunc_end"):
+                inside = False
+            if not inside:
+                m = re.match(r"\s+\.(vgpr_count|sgpr_count|private_segment_fixed_size|sgpr_spill_count|vgpr_spill_count):\s+(\d+)", line)
+                if m and meta.get("_name_ok"):
+                    meta[m.group(1)] = m.group(2)
+                m = re.match(r"\s+\.name:\s+(\S+)", line)
+                if m:
+                    meta["_name_ok"] = want in m.group(1)
+                continue
             m = re.search(r";MARK (\w+)", line)
             if m:
                 cur = m.group(1)
                 continue
             if out and cur == dump:
                 out.write(line)
-            m = re.match(r"\s+\.(vgpr_count|sgpr_count|private_segment_fixed_size):\s+(\d+)", line)
-            if m:
-                meta[m.group(1)] = m.group(2)
             tok = line.strip().split()
             if not tok or tok[0].startswith((".", ";")) or tok[0].endswith(":"):
                 continue
@@ -101,6 +116,8 @@ def main():
             cls = ("valu" if op.startswith("v_") else "salu" if op.startswith("s_") else "lds" if op.startswith("ds_")
                    else "vmem" if op.startswith(("global_", "buffer_", "flat_")) else "other")
             cnt.setdefault(cur, collections.Counter())[cls] += 1
+            if op == "s_waitcnt":
+                cnt[cur]["waitcnt"] += 1
             cnt[cur]["bytes"] += enc_bytes(op, line)
             if cls == "valu":
                 cnt[cur]["units"] += valu_units(op)
@@ -108,9 +125,10 @@ def main():
                     cnt[cur]["spill"] += 1  # SGPR spills through VGPR lanes
     tot = collections.Counter()
     for k, v in cnt.items():
-        print(f"{k:10s} " + " ".join(f"{c}={v[c]:g}" for c in ("valu", "units", "salu", "lds", "vmem", "spill", "bytes")))
+        print(f"{k:10s} " + " ".join(f"{c}={v[c]:g}" for c in ("valu", "units", "salu", "lds", "vmem", "waitcnt", "spill", "bytes")))
         tot += v
-    print("total      " + " ".join(f"{c}={tot[c]:g}" for c in ("valu", "units", "salu", "lds", "vmem", "spill", "bytes")),
+    meta.pop("_name_ok", None)
+    print("total      " + " ".join(f"{c}={tot[c]:g}" for c in ("valu", "units", "salu", "lds", "vmem", "waitcnt", "spill", "bytes")),
           meta)
 
 

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """K7 (vp8l_resolve.hip) block statistics from the measurement build (make VARIANT=timing,
 WG_LIB_VARIANT=timing): blocks, blocks redone serially, rounds, and wave 0's cycles per phase
-(tokens + ranks, windows, serial path, stores) for one c5 batch."""
+(tokens + ranks, windows, serial path, stores) for one batch of a bench workload:
+k7_stats.py [frames] [workload: c5 (default) | c3a (the ALPH streams)]."""
 import ctypes as C
 import os
 import sys
@@ -15,7 +16,8 @@ def main():
     import torch  # noqa: F401
     import webp_amd
     from bench import WORKLOADS, _load_frames
-    datas, _ = _load_frames(WORKLOADS["c5"]["prefix"])
+    wl = sys.argv[2] if len(sys.argv) > 2 else "c5"
+    datas, _ = _load_frames(WORKLOADS[wl]["prefix"])
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 32
     ctx = webp_amd.Context(0, host_threads=16)
     b = ctx.batch([datas[i % len(datas)] for i in range(n)])

@@ -167,4 +167,9 @@ CASES = [
                                                 palette=20)),
     ("long_run", 3 * 4096 + 500, 0, dict(p_lit=0.0005, p_copy=0.9995, dist=(1,), run=20000)),
     ("short_runs", 2 * 4096 + 11, 4, dict(p_lit=0.2, p_copy=0.6, dist=(1, 1, 1, "near"), run=3, palette=30)),
+    # every pixel an updater (registration combined per key across a wave's lanes), with lookups
+    # straddling them: few keys (b2) and many (b10), windows of 2048 updaters
+    ("dense_b2", 3 * 4096 + 9, 2, dict(p_lit=0.1, p_copy=0.85, dist=(1, 2, "w", "near"), run=40, width=300,
+                                       palette=6)),
+    ("dense_b10", 3 * 4096 + 70, 10, dict(p_lit=0.3, p_copy=0.6, dist=(1, "near", "far"), run=12, palette=3000)),
 ]

@@ -83,9 +83,10 @@ def test_cropped_batch_keeps_separate_emit(ctx):
 @pytest.mark.parametrize("key", ["m0_none_f1_nf0", "m7_none_f0_nf0", "m4_none_f0_nf1", "m1_none_f1_nf0"])
 def test_resident_batch_runs_k6_as_a_stage(ctx, key):
     """A batch created with an output colorspace (or flip) runs K6 as the last stage of every
-    wg_batch_run (its own kernel_ms entry); downloads copy its output: equal to WebPDecode's
-    bytes after repeated runs (RGB flipped, rgbA premultiplied, ARGB point-sampled, RGBA
-    flipped)."""
+    wg_batch_run (its own kernel_ms entry) over the frames the YUV -> RGB strips do not emit
+    directly (lossless frames and frames with alpha); downloads copy its output: equal to
+    WebPDecode's bytes after repeated runs (RGB flipped, rgbA premultiplied, ARGB point-sampled,
+    RGBA flipped).  The directly emitted frames have no RGBA copy (UNSUPPORTED_FEATURE)."""
     mode, cname, flip, nf = parse_mode_key(key)
     srcs = [load_modes(s) for s in mode_sources()]
     sub = [(d, g) for d, g, e in srcs if e["status"].get(key) == 0 and key in g]
@@ -98,8 +99,82 @@ def test_resident_batch_runs_k6_as_a_stage(ctx, key):
         assert ms[5] > 0, ms
         by = b.kernel_bytes()
         bpp = webp_amd.output_bpp(mode)
-        assert by[5] == sum((4 + bpp) * g[key].shape[0] * g[key].shape[1] // bpp for _, g in sub)
+        direct = [webp_amd.features(d).format != 2 and not webp_amd.features(d).has_alpha for d, _ in sub]
+        assert any(direct) and not all(direct)
+        assert by[5] == sum((4 + bpp) * g[key].shape[0] * g[key].shape[1] // bpp
+                            for (_, g), dr in zip(sub, direct) if not dr)
         for i, (_, g) in enumerate(sub):
             np.testing.assert_array_equal(b.download(i), g[key], err_msg=f"{key} frame {i}")
+            if direct[i]:
+                with pytest.raises(webp_amd.WebPError):
+                    b.rgba(i)
     finally:
         b.close()
+
+
+def _modes_from_rgba(rgba, mode, flip):
+    """WebPDecode's bytes of an opaque frame in `mode` from its RGBA (emit_px.h's packings; the
+    premultiplied modes equal the plain ones at a = 255)."""
+    r, g, b, a = (rgba[..., c].astype(np.uint32) for c in range(4))
+    m = {7: 1, 8: 3, 9: 4, 10: 5}.get(mode, mode)
+    if m == 0:
+        out = np.stack([r, g, b], -1)
+    elif m == 1:
+        out = np.stack([r, g, b, a], -1)
+    elif m == 2:
+        out = np.stack([b, g, r], -1)
+    elif m == 3:
+        out = np.stack([b, g, r, a], -1)
+    elif m == 4:
+        out = np.stack([a, r, g, b], -1)
+    elif m == 5:
+        out = np.stack([(r & 0xf0) | (g >> 4), (b & 0xf0) | (a >> 4)], -1)
+    else:
+        out = np.stack([(r & 0xf8) | (g >> 5), ((g << 3) & 0xe0) | (b >> 3)], -1)
+    out = out.astype(np.uint8).reshape(rgba.shape[0], -1)
+    return out[::-1] if flip else out
+
+
+@pytest.mark.parametrize("emit", ["auto", "tail"])
+def test_direct_emission_every_mode_4k(ctx, emit):
+    """Lossy 4K frames without alpha emitted straight into every output colorspace, flipped or
+    not: by K2 (a 3-frame batch runs the split K1, K2 converts) or by K1's tail (set_emit(False):
+    RGBA / rgbA / RGB_565; the other modes refuse the tail and keep K2).  No K6; the bytes equal
+    the packing of the frames' RGBA, itself checked against libwebp's SHA-256."""
+    import hashlib
+    import os
+    from oracle_lib import bench_files, manifest
+    paths = bench_files("c3_4k")
+    want = manifest()["bench"]
+    n = 3
+    datas = [open(paths[i], "rb").read() for i in range(n)]
+    ref = ctx.batch(datas)
+    try:
+        ref.run()
+        rgbas = [ref.rgba(i) for i in range(n)]
+    finally:
+        ref.close()
+    for i, im in enumerate(rgbas):
+        assert hashlib.sha256(im.tobytes()).hexdigest() == want[os.path.basename(paths[i])]["sha256"]["rgba"]
+    for mode in range(11):
+        for flip in (0, 1):
+            if mode == 1 and not flip:
+                continue  # (plain RGBA: no K6 batch)
+            b = ctx.batch(datas, opts=webp_amd.options(mode, None, flip))
+            try:
+                tail = emit == "tail" and mode in (1, 6, 7)
+                if emit == "tail":
+                    if tail:
+                        b.set_emit(False)
+                    else:
+                        with pytest.raises(webp_amd.WebPError):
+                            b.set_emit(False)
+                b.run()
+                ms = b.kernel_ms()
+                assert ms[5] == 0, (mode, flip, ms)  # no K6: every frame emitted directly
+                assert (ms[1] > 0) == (not tail), (mode, flip, ms)  # K2, or K1's tail
+                for i, im in enumerate(rgbas):
+                    np.testing.assert_array_equal(b.download(i), _modes_from_rgba(im, mode, flip),
+                                                  err_msg=f"mode {mode} flip {flip} frame {i}")
+            finally:
+                b.close()

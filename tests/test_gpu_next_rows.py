@@ -3,8 +3,8 @@
 
 * c3a (f2, K4): 8 x 4K lossy + lossless-compressed ALPH frames, the bench's 256-frame layout
   (frames cycled), RGBA SHA-256 with K1's tail and with a separate K2, and point sampling;
-* c3rgb565 (f4, K6): C3's frames decoded to MODE_RGB_565 as a resident batch, K6 a stage of
-  every run, SHA-256 of WebPDecode's bytes;
+* c3rgb565 (f4): C3's frames decoded to MODE_RGB_565 as a resident batch -- K1's tail emits the
+  565 pixels itself (no RGBA copy, no K6) -- SHA-256 of WebPDecode's bytes;
 * anim (f3, K5): the 64-frame 1920x1080 animation as a resident animation batch, every
   canvas's SHA-256 against WebPAnimDecoder and its timestamps, on repeated runs.
 
@@ -74,7 +74,7 @@ def test_c3_rgb565_resident_batch(ctx):
         for _ in range(2):
             b.run()
         ms = b.kernel_ms()
-        assert ms[0] > 0 and ms[5] > 0, ms  # K1 (its RGBA tail) then K6
+        assert ms[0] > 0 and ms[5] == 0, ms  # K1's tail writes RGB_565 itself: no RGBA copy, no K6
         for i in range(16):
             out = b.download(i)
             assert out.shape == (2160, 3840 * 2)
