@@ -212,6 +212,7 @@ struct wg_batch {
   AlphaDesc* d_adesc = nullptr;
   int n_lossy = 0, n_lossless = 0, n_alpha = 0, n_k3 = 0, n_k6 = 0;  // n_k6: frames K6 converts
   bool tail_modes = true, no_tail = false;  // no_tail: frames emitted directly in a mode K1's tail lacks
+  int n_tok_w64 = 0;                         // K7 streams on its 64-mask-word instantiation (first in tokdesc)
   wg_decoder_options opt{};          // output colorspace, cropping, flip (f4)
   bool any_crop = false;             // K2 reads compact cropped planes through desc2
   bool fused = false;                // lossy RGBA emitted by K1's tail (wg::kFrameEmitRgba), no K2 launch
@@ -994,6 +995,11 @@ int batch_upload(wg_batch* b, const wg::StagingArena& arena) {
   if (e == hipSuccess && !b->lldesc.empty())
     e = hipMemcpyAsync(b->d_lldesc, b->lldesc.data(), sizeof(LLDesc) * b->lldesc.size(), hipMemcpyHostToDevice,
                        home);
+  // K7 launches the streams of its 64-mask-word instantiation first (one kernel each)
+  std::stable_partition(b->tokdesc.begin(), b->tokdesc.end(),
+                        [](const wg::LLTokDesc& t) { return wg::vp8l_resolve_w64(t.cache_bits); });
+  b->n_tok_w64 = (int)std::count_if(b->tokdesc.begin(), b->tokdesc.end(),
+                                    [](const wg::LLTokDesc& t) { return wg::vp8l_resolve_w64(t.cache_bits); });
   if (e == hipSuccess && !b->tokdesc.empty())
     e = hipMemcpyAsync(b->d_tokdesc, b->tokdesc.data(), sizeof(wg::LLTokDesc) * b->tokdesc.size(),
                        hipMemcpyHostToDevice, home);
@@ -1100,7 +1106,7 @@ int wg_batch_run(wg_batch* b, void* stream) {
   }
   hipEventRecord(t.ev[kStageK7], s);
   if (b->n_k3 > 0) {  // K7: the lossless streams' color cache and back-references
-    hipError_t e = wg::launch_vp8l_resolve(b->d_tokdesc, nullptr, (int)b->tokdesc.size(), b->d_err, s);
+    hipError_t e = wg::launch_vp8l_resolve(b->d_tokdesc, nullptr, (int)b->tokdesc.size(), b->d_err, s, b->n_tok_w64);
     if (e != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
   }
   hipEventRecord(t.ev[kStageK3], s);

@@ -34,9 +34,12 @@ hipError_t launch_vp8l_transforms(const LLDesc* d_frames, const int* group_count
 
 // K7: VP8L color cache + back-references (tokens -> coded ARGB), one 1024-thread workgroup per
 // lossless stream; runs before K3.  d_err: OR-ed with 4 on an invalid token.
-// d_descs null: the single stream `single` (stage entry)
+// d_descs null: the single stream `single` (stage entry).  The first n_w64 of d_descs take the
+// 64-mask-word instantiation (vp8l_resolve_w64(cache_bits): one window per block), the rest the
+// 32-word one.
+bool vp8l_resolve_w64(int cache_bits);
 hipError_t launch_vp8l_resolve(const LLTokDesc* d_descs, const LLTokDesc* single, int n, int* d_err,
-                               hipStream_t stream);
+                               hipStream_t stream, int n_w64 = 0);
 
 // K4: ALPH planes (unfilter) -> A bytes of the RGBA output, one 1024-thread workgroup per
 // plane; runs after K2 and K3.

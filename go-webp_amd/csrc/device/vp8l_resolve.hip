@@ -66,6 +66,7 @@ constexpr int kWavePx = 64 * kPer;        // pixels per wave in a block
 constexpr int kSlots = 2048;              // 1 << MAX_CACHE_BITS (format_constants.go)
 constexpr int kMaskWords = 8192;          // 64 KB of 64-bit rank masks, split over the keys
 constexpr int kMaxW = 32;                 // mask words per key (the summary is 32 bits)
+constexpr int kW64Bits = 7;               // kW64: cache_bits <= 7 (<= 128 keys x 64 words)
 constexpr int kMaxRounds = 32;
 constexpr uint8_t kKnown = 1, kPendCopy = 2, kPendLookup = 3;
 constexpr uint32_t kDropOff = 0xffffffc0u;  // buffer offset past any stream: loads return 0
@@ -107,11 +108,24 @@ __device__ unsigned long long g_k7_wave[kWaves][16];  // per wave (lane 0): the 
 #define K7_COUNT(i, v) (void)0
 #endif
 
+// kW64 (streams with cache_bits <= 7, none included, chosen by the host): the instantiation for
+// dense updaters -- alpha planes and flat content, where nearly every pixel is a copy.
+//  * 64 mask words per key under a 64-bit summary, so a window holds 4096 ranks: every block is
+//    one window (at 32 words such a block ran as two windows of eight waves, each idling through
+//    the other's rounds).  The summaries of its <= 128 keys live in summ's first 1 KB as 64-bit
+//    words; stores that are not registrations are masked off (ranks reach uval's dummy slots).
+//  * Registration by consecutive ranks with the lanes of one key combined (reg_pass / reg_run):
+//    same-address LDS atomics serialize lane by lane, and a run of copies puts a wave's 64 lanes
+//    on one key.  Copies resolved in a round flag their ranks and register in one such pass.
+//  * The rounds' copy step gathers its four slots' states, values and links as independent LDS
+//    reads, and takes one first_pend min per wave.
+// C5-like streams (cache_bits 10, ~143 updaters per block) keep the 32-word instantiation, whose
+// code is unchanged by these (measured: the dense paths cost C5's K7 7 %, and gain c3a's 28 %).
 // kSingle: the one stream `single` passed by value (the stage entry wg_vp8l_resolve_device; err may
 // be null there: bad tokens then only resolve to 0, the serial path's rule); else stream
 // blockIdx.x of `descs`.  (Two instantiations: a descriptor chosen at run time between the two
 // loses its uniformity and the pointers' address space -- flat loads and spills.)
-template <bool kSingle>
+template <bool kSingle, bool kW64>
 __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __restrict__ descs, LLTokDesc single,
                                                             int* err) {
   __shared__ uint64_t mask[kMaskWords];          // per key k: words k*W .. k*W+W-1, bit = rank in window
@@ -144,8 +158,9 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
   const int n = D.n_px, cache_bits = D.cache_bits;
   const int nkeys = cache_bits > 0 ? 1 << cache_bits : 0;
   const int shift = 32 - cache_bits;
-  const int W = cache_bits > 0 ? min(kMaxW, kMaskWords >> cache_bits) : 1;  // mask words per key
-  const int cap = 64 * W;                                                    // ranks per window
+  const int W = kW64 ? 64 : cache_bits > 0 ? min(kMaxW, kMaskWords >> cache_bits) : 1;  // mask words per key
+  const int cap = 64 * W;                                                              // ranks per window
+  uint64_t* const summ64 = reinterpret_cast<uint64_t*>(summ);  // (kW64: key k's summary)
   // Buffer descriptors: out-of-range loads return 0 with no branch, so the prefetches below are
   // straight-line code and the waitcnt pass can count them precisely (a load under a lane
   // branch makes it wait for every outstanding load at the join).
@@ -226,9 +241,10 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
   auto pk = [](uint32_t ps, int j) { return (ps >> (2 * j)) & 3u; };
   auto is_upd = [](uint32_t ps, int j) { return (ps >> (8 + j)) & 1u; };
   auto set_known = [](uint32_t& ps, int j) { ps &= ~(3u << (2 * j)); };
-  // a uval slot beyond any rank for stores that are not registrations (ranks < cap <= 2048):
-  // one per thread, so the dropped stores of one instruction do not collide on one address
-  const int uval_dummy = 2048 + tid;
+  // a slot beyond any rank for stores that are not registrations (ranks < cap <= 2048): one per
+  // thread, so the dropped stores of one instruction do not collide on one address (kW64: ranks
+  // reach 4095, the dummies go to the straddle scratch, rewritten before every read of it)
+  const int uval_dummy = 2048 + tid;  // (kW64: not used; its ranks reach 4095)
   // A block's values go to the coded image (K3's input) from LDS during the NEXT block, ahead of
   // that block's prefetches: in the in-order vmcnt, a store issued at the end of its own block
   // would sit between the next block's loads and their first use.  Copies reaching back past
@@ -256,11 +272,13 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
   auto ds_or_b32 = [&](uint32_t* p, uint32_t v) { asm volatile("ds_or_b32 %0, %1" ::"v"(lds_addr(p)), "v"(v) : "memory"); };
   auto ds_max_u32 = [&](uint32_t* p, uint32_t v) { asm volatile("ds_max_u32 %0, %1" ::"v"(lds_addr(p)), "v"(v) : "memory"); };
   auto ds_min_i32 = [&](int* p, int v) { asm volatile("ds_min_i32 %0, %1" ::"v"(lds_addr(p)), "v"(v) : "memory"); };
+  auto ds_write_u32 = [&](uint32_t* p, uint32_t v) { asm volatile("ds_write_b32 %0, %1" ::"v"(lds_addr(p)), "v"(v) : "memory"); };
   // mask bit, summary, last rank of an updater whose value is in uval[r]
   auto reg_hash = [&](int r, uint32_t x) {
     const uint32_t h = hash_px(x, shift);
     ds_or_b64(&mask[h * W + (r >> 6)], 1ull << (r & 63));
-    ds_or_b32(&summ[h], 1u << (r >> 6));
+    if (kW64) ds_or_b64(&summ64[h], 1ull << (r >> 6));
+    else ds_or_b32(&summ[h], 1u << (r >> 6));
     ds_max_u32(&slotrec[h].x, (uint32_t)r + 1u);
   };
   // step 3 for one registered updater: if it is its key's last in the window, write the slot
@@ -270,8 +288,13 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
   auto table_update = [&](int r, uint32_t x, bool go_serial) {
     const uint32_t h = hash_px(x, shift);
     if (slotrec[h].x == (uint32_t)r + 1u) {
-      for (uint32_t sm = summ[h]; sm; sm &= sm - 1) mask[h * W + __builtin_ctz(sm)] = 0;
-      summ[h] = 0;
+      if (kW64) {
+        for (uint64_t sm = summ64[h]; sm; sm &= sm - 1) mask[h * W + __builtin_ctzll(sm)] = 0;
+        summ64[h] = 0;
+      } else {
+        for (uint32_t sm = summ[h]; sm; sm &= sm - 1) mask[h * W + __builtin_ctz(sm)] = 0;
+        summ[h] = 0;
+      }
       if (!go_serial) {
         slotrec[h] = make_uint2(0u, x);
         ds_or_b32(&slot_set[h >> 5], 1u << (h & 31));
@@ -288,17 +311,93 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   };
 
+  // Rank flags of a wave's updaters (waves with in-block copies): 2 = value known, to register;
+  // 3 = registered; 0 = pending.  They live in the straddle scratch: a wave sets and consumes its
+  // own ranks' flags within step 2 or within one round's (b), between barriers, and rewrites them
+  // first (the lookups (a) use the scratch in between).
+  uint8_t* const rflag = reinterpret_cast<uint8_t*>(sscr);
+  static_assert(sizeof(sscr) >= kBlock, "rflag: one byte per rank");
+  // Registration of a wave's updaters with CONSECUTIVE ranks rbase + lane (the lanes with `valid`).
+  // Dense runs of updaters (alpha planes, flat content: every pixel a copy) put many lanes on one
+  // key, and same-address LDS atomics serialize lane by lane; so in a dense pass (wave-uniform)
+  // the lanes of one key combine first -- their rank bits are the key's lane ballot shifted by
+  // rbase, one mask OR per word, one summary OR, one max -- key by key while a key still gathers
+  // four lanes; the rest register one lane at a time.
+  auto reg_run = [&](bool valid, int rbase, int r, uint32_t x, bool dense) {
+    const uint32_t h = hash_px(x, shift);
+    bool pend = valid;
+    if (dense) {
+      for (int it = 0; it < 8; ++it) {
+        const uint64_t pm = __ballot(pend);
+        if (pm == 0) break;
+        const int lead = __builtin_ctzll(pm);
+        const uint32_t hl = (uint32_t)__builtin_amdgcn_readlane((int)h, lead);
+        const uint64_t m = __ballot(pend && h == hl);
+        if (lane == lead) {
+          const int w0 = rbase >> 6, sh = rbase & 63;
+          const uint64_t lo = m << sh, hi = sh ? m >> (64 - sh) : 0ull;
+          if (lo) ds_or_b64(&mask[hl * W + w0], lo);
+          if (hi) ds_or_b64(&mask[hl * W + w0 + 1], hi);
+          if (kW64) {
+            ds_or_b64(&summ64[hl], (lo ? 1ull << w0 : 0ull) | (hi ? 2ull << w0 : 0ull));
+          } else {
+            ds_or_b32(&summ[hl], (lo ? 1u << w0 : 0u) | (hi ? 2u << w0 : 0u));
+          }
+          ds_max_u32(&slotrec[hl].x, (uint32_t)(rbase + 63 - __builtin_clzll(m)) + 1u);
+        }
+        pend = pend && h != hl;
+        if (__builtin_popcountll(m) < 4) break;
+      }
+    }
+    if (pend) reg_hash(r, x);
+  };
+  // this wave's updaters of ranks [r0w, r0w + cnt) (its whole range in the window): all of them,
+  // or (flagged) those flagged 2, which become 3
+  auto reg_pass = [&](int r0w, int cnt, bool flagged) {
+    wave_sync();
+    const bool dense = cnt >= 64;
+    for (int i0 = 0; i0 < cnt; i0 += 64) {
+      const int r = r0w + i0 + lane;
+      bool valid = i0 + lane < cnt;
+      if (flagged) {
+        valid = valid && rflag[valid ? r : 0] == 2;
+        if (valid) rflag[r] = 3;
+      }
+      reg_run(valid, r0w + i0, r, uval[valid ? r : 0], dense);
+    }
+  };
+  // one ds_min per wave for a pending position that grows with the lane (the lowest lane's wins)
+  auto wave_min_pos = [&](int* p, int pos) {
+    const uint64_t m = __ballot(pos < kBlock);
+    if (m) {
+      const int lead = __builtin_ctzll(m);
+      const int x = __builtin_amdgcn_readlane(pos, lead);
+      if (lane == lead) ds_min_i32(p, x);
+    }
+  };
+
   // A lookup whose key has window updaters on both sides of it: the highest bit of the key's
   // rank mask below rr (the window updaters before the pixel), from the summary's top one or
   // two words; ~0 if none.
   auto straddle_idx = [&](uint32_t k, int rr) -> uint32_t {
     const int wt = (rr - 1) >> 6;
-    const uint32_t sm = rr <= 0 ? 0u : summ[k] & (wt >= 31 ? ~0u : (2u << wt) - 1u);
-    const int w1 = sm ? 31 - __builtin_clz(sm) : 0;
-    const uint32_t sm2 = sm & ~(1u << w1);
-    const int w2 = sm2 ? 31 - __builtin_clz(sm2) : 0;
-    const uint64_t m1 = sm ? mask[k * W + w1] : 0ull;
-    const uint64_t m2 = sm2 ? mask[k * W + w2] : 0ull;
+    int w1, w2;
+    bool h1, h2;  // the top / second non-empty words below the pixel exist
+    if (kW64) {
+      const uint64_t sm = rr <= 0 ? 0ull : summ64[k] & (wt >= 63 ? ~0ull : (2ull << wt) - 1ull);
+      w1 = sm ? 63 - __builtin_clzll(sm) : 0;
+      const uint64_t sm2 = sm & ~(1ull << w1);
+      w2 = sm2 ? 63 - __builtin_clzll(sm2) : 0;
+      h1 = sm != 0, h2 = sm2 != 0;
+    } else {
+      const uint32_t sm = rr <= 0 ? 0u : summ[k] & (wt >= 31 ? ~0u : (2u << wt) - 1u);
+      w1 = sm ? 31 - __builtin_clz(sm) : 0;
+      const uint32_t sm2 = sm & ~(1u << w1);
+      w2 = sm2 ? 31 - __builtin_clz(sm2) : 0;
+      h1 = sm != 0, h2 = sm2 != 0;
+    }
+    const uint64_t m1 = h1 ? mask[k * W + w1] : 0ull;
+    const uint64_t m2 = h2 ? mask[k * W + w2] : 0ull;
     // the top word is the pixel's own word: keep only the ranks below it (lb = 1..64)
     const int lb = rr - 64 * w1;
     const uint64_t top = lb < 64 ? m1 & ((1ull << lb) - 1ull) : m1;
@@ -411,7 +510,7 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
     // each (a one-wave window has at most 256 <= cap); almost always one
     auto prefix = [&](int w) { return w <= 0 ? 0 : __builtin_amdgcn_readlane(scan, w - 1); };  // waves < w
     int wpw = kWaves;  // waves per window
-    if (nkeys && total > cap) {
+    if (!kW64 && nkeys && total > cap) {
       int l = 4;
       for (int lv = 3; lv >= 1; --lv) {
         const int span = kWaves >> lv;
@@ -491,29 +590,57 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
       //         slot, to a dummy slot when it is not one), then one updater per lane over the
       //         wave's ranks [woff - rb, woff - rb + my_wc) -- or per pixel slot when the wave
       //         has in-block copies, whose ranks lie in the same range unregistered
-#pragma unroll
-      for (int j = 0; j < kPer; ++j)
-        uval[in_win && is_upd(ps, j) && pk(ps, j) == kPK ? R(j) - rb : uval_dummy] = v[j];
-      if (in_win && nkeys) {
-        if (!wave_pc) {
-          wave_sync();
-          for (int i = lane; i < my_wc; i += 64) {
-            const int r = woff - rb + i;
-            reg_hash(r, uval[r]);
-          }
-        } else {
-#pragma unroll
-          for (int j = 0; j < kPer; ++j)
-            if (is_upd(ps, j) && pk(ps, j) == kPK) reg_hash(R(j) - rb, v[j]);
-        }
-      }
       const bool pc = in_win && my_pc;
-      if (pc) {
-        int fp = kBlock;
+      if constexpr (kW64) {
+        // Dense updaters (the small-cache instantiation): the value stores as inline asm (a plain
+        // LDS store here is the first LDS access after the next block's literal loads into LDS,
+        // and the waitcnt pass -- which cannot tell uval from their target -- would wait vmcnt(0)
+        // for them and the two-ahead token loads, every block; uval is read after bar()'s
+        // lgkmcnt(0), or by this wave in order), registration by consecutive ranks combined per
+        // key (a wave with in-block copies flags its known updaters first), one first_pend min
+        // per wave.
 #pragma unroll
-        for (int j = kPer - 1; j >= 0; --j)
-          if (pk(ps, j) == kPC) fp = li0 + j;
-        ds_min_i32(&first_pend[0], fp);
+        for (int j = 0; j < kPer; ++j)
+          if (in_win && is_upd(ps, j) && pk(ps, j) == kPK) ds_write_u32(&uval[R(j) - rb], v[j]);
+        if (in_win && nkeys) {
+          if (wave_pc) {
+#pragma unroll
+            for (int j = 0; j < kPer; ++j)
+              if (is_upd(ps, j)) rflag[R(j) - rb] = pk(ps, j) == kPK ? 2 : 0;
+          }
+          reg_pass(woff - rb, my_wc, wave_pc);
+        }
+        if (in_win && wave_pc) {
+          int fp = kBlock;
+#pragma unroll
+          for (int j = kPer - 1; j >= 0; --j)
+            if (pk(ps, j) == kPC) fp = li0 + j;
+          wave_min_pos(&first_pend[0], fp);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < kPer; ++j)
+          uval[in_win && is_upd(ps, j) && pk(ps, j) == kPK ? R(j) - rb : uval_dummy] = v[j];
+        if (in_win && nkeys) {
+          if (!wave_pc) {
+            wave_sync();
+            for (int i = lane; i < my_wc; i += 64) {
+              const int r = woff - rb + i;
+              reg_hash(r, uval[r]);
+            }
+          } else {
+#pragma unroll
+            for (int j = 0; j < kPer; ++j)
+              if (is_upd(ps, j) && pk(ps, j) == kPK) reg_hash(R(j) - rb, v[j]);
+          }
+        }
+        if (pc) {
+          int fp = kBlock;
+#pragma unroll
+          for (int j = kPer - 1; j >= 0; --j)
+            if (pk(ps, j) == kPC) fp = li0 + j;
+          ds_min_i32(&first_pend[0], fp);
+        }
       }
       // (a) of a round: lookups of the window before the first pending copy fp.  kRounds: the
       // window has in-block copies (fp varies, and copies read the lookups' states); instantiated
@@ -633,7 +760,70 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
         bar();
         // (b) pending copies: take a known source's value and register, else jump one link back
         bool still = false;  // a copy of mine still pending
-        if (in_win) {
+        if constexpr (kW64) {
+          uint32_t pcm = 0;    // my pending copies (slot bits)
+#pragma unroll
+          for (int j = 0; j < kPer; ++j) pcm |= (uint32_t)(pk(ps, j) == kPC) << j;
+          if (in_win && wave_pc && nkeys) {  // this wave's rank flags (the scratch held lookups)
+#pragma unroll
+            for (int j = 0; j < kPer; ++j)
+              if (is_upd(ps, j)) rflag[R(j) - rb] = 0;
+          }
+          int myfp = kBlock;  // my first copy still pending
+          bool got = false;   // a copy of mine resolved (to register)
+          if (in_win && pcm) {
+            // Gather first, apply after: the four slots' source pointers (one 8-byte read), their
+            // states, values and links as independent LDS reads in flight together -- not four
+            // chains of three dependent reads.  The hand-off from other waves is st / vcur in LDS,
+            // whose DS operations a wave issues and the LDS performs in order: a writer's vcur store
+            // lands before its st store, and a reader's vcur load is issued after its st load, so a
+            // state read as known comes with the value; the fences only stop the compiler
+            // (wavefront scope: no instruction; a workgroup release would also wait vmcnt(0) for the
+            // next block's staged literal loads into LDS).  A slot whose source is an earlier slot of
+            // this lane sees that slot's state from before the round: it jumps instead of resolving,
+            // and resolves a round later.
+            const uint2 rw = *reinterpret_cast<const uint2*>(&ref[li0]);
+            const int rv[kPer] = {(int16_t)(rw.x & 0xffffu), (int16_t)(rw.x >> 16), (int16_t)(rw.y & 0xffffu),
+                                  (int16_t)(rw.y >> 16)};
+            int src[kPer];
+            uint32_t ss[kPer], xs[kPer];
+            int nref[kPer];
+#pragma unroll
+            for (int j = 0; j < kPer; ++j) src[j] = (pcm >> j) & 1u ? rv[j] : li0 + j;
+#pragma unroll
+            for (int j = 0; j < kPer; ++j) ss[j] = st[src[j]];
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int j = 0; j < kPer; ++j) xs[j] = vcur[src[j]];
+#pragma unroll
+            for (int j = 0; j < kPer; ++j) nref[j] = ref[src[j]];
+#pragma unroll
+            for (int j = 0; j < kPer; ++j) {
+              const int li = li0 + j;
+              if (!((pcm >> j) & 1u)) continue;
+              if (ss[j] == kKnown) {
+                const uint32_t x = xs[j];
+                set_known(ps, j);
+                v[j] = x;
+                vcur[li] = x;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                st[li] = kKnown;
+                uval[R(j) - rb] = x;
+                rflag[R(j) - rb] = 2;
+                got = true;
+              } else {
+                if (ss[j] == kPendCopy) ref[li] = (int16_t)nref[j];  // (a stale or fresh link: both lie on the chain)
+                myfp = min(myfp, li);
+                still = true;
+              }
+            }
+          }
+          if (in_win && wave_pc) {
+            wave_min_pos(&first_pend[(r + 1) & 1], myfp);
+            // the copies resolved this round register by rank (consecutive across lanes: combined per key)
+            if (nkeys && __any(got)) reg_pass(woff - rb, my_wc, true);
+          }
+        } else if (in_win) {
 #pragma unroll
           for (int j = 0; j < kPer; ++j) {
             const int li = li0 + j;
@@ -757,11 +947,25 @@ extern "C" int wg_debug_k7_stats(unsigned long long* out, int reset) {
 }
 #endif
 
+bool vp8l_resolve_w64(int cache_bits) { return cache_bits <= kW64Bits; }
+
 hipError_t launch_vp8l_resolve(const LLTokDesc* d_descs, const LLTokDesc* single, int n, int* d_err,
-                               hipStream_t stream) {
+                               hipStream_t stream, int n_w64) {
   if (n <= 0) return hipSuccess;
-  if (single) hipLaunchKernelGGL(vp8l_resolve_kernel<true>, dim3(1), dim3(kThreads), 0, stream, nullptr, *single, d_err);
-  else hipLaunchKernelGGL(vp8l_resolve_kernel<false>, dim3(n), dim3(kThreads), 0, stream, d_descs, LLTokDesc{}, d_err);
+  if (single) {
+    if (vp8l_resolve_w64(single->cache_bits))
+      hipLaunchKernelGGL((vp8l_resolve_kernel<true, true>), dim3(1), dim3(kThreads), 0, stream, nullptr, *single, d_err);
+    else
+      hipLaunchKernelGGL((vp8l_resolve_kernel<true, false>), dim3(1), dim3(kThreads), 0, stream, nullptr, *single, d_err);
+    return hipGetLastError();
+  }
+  // the first n_w64 streams on the 64-word instantiation, the rest on the 32-word one
+  if (n_w64 > 0)
+    hipLaunchKernelGGL((vp8l_resolve_kernel<false, true>), dim3(n_w64), dim3(kThreads), 0, stream, d_descs, LLTokDesc{},
+                       d_err);
+  if (n > n_w64)
+    hipLaunchKernelGGL((vp8l_resolve_kernel<false, false>), dim3(n - n_w64), dim3(kThreads), 0, stream,
+                       d_descs + n_w64, LLTokDesc{}, d_err);
   return hipGetLastError();
 }
 

@@ -172,4 +172,8 @@ CASES = [
     ("dense_b2", 3 * 4096 + 9, 2, dict(p_lit=0.1, p_copy=0.85, dist=(1, 2, "w", "near"), run=40, width=300,
                                        palette=6)),
     ("dense_b10", 3 * 4096 + 70, 10, dict(p_lit=0.3, p_copy=0.6, dist=(1, "near", "far"), run=12, palette=3000)),
+    # the 64-mask-word instantiation (cache bits <= 7): one window of up to 4096 ranks, lookups
+    # straddling updaters of their key in the words above 32
+    ("w64_straddle", 4 * 4096 + 21, 6, dict(p_lit=0.55, p_copy=0.35, dist=(1, 2, "near"), run=4, palette=90)),
+    ("w64_b7_lits", 3 * 4096 + 5, 7, dict(p_lit=0.9, p_copy=0.02, palette=400)),
 ]
