@@ -289,8 +289,8 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
     const uint32_t h = hash_px(x, shift);
     if (slotrec[h].x == (uint32_t)r + 1u) {
       if (kW64) {
-        for (uint64_t sm = summ64[h]; sm; sm &= sm - 1) mask[h * W + __builtin_ctzll(sm)] = 0;
-        summ64[h] = 0;
+        // (the masks and summaries are cleared by the whole workgroup after the table: a key's
+        // last updater walking up to 64 words alone made the block's last wave the slowest)
       } else {
         for (uint32_t sm = summ[h]; sm; sm &= sm - 1) mask[h * W + __builtin_ctz(sm)] = 0;
         summ[h] = 0;
@@ -860,6 +860,10 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
       if (in_win && nkeys) {
         const int wtot = prefix(q * wpw + wpw) - rb, wi = wave - q * wpw;
         for (int i = wi * 64 + lane; i < wtot; i += wpw * 64) table_update(i, uval[i], go_serial);
+      }
+      if constexpr (kW64) {  // every key's masks and summary, spread over the workgroup (lookups are done)
+        for (int i = tid; i < nkeys * W; i += kThreads) mask[i] = 0;
+        for (int i = tid; i < nkeys; i += kThreads) summ64[i] = 0;
       }
       if (tid == 0) first_pend[0] = first_pend[1] = kBlock;
       if (go_serial) {
