@@ -213,6 +213,7 @@ struct wg_batch {
   int n_lossy = 0, n_lossless = 0, n_alpha = 0, n_k3 = 0, n_k6 = 0;  // n_k6: frames K6 converts
   bool tail_modes = true, no_tail = false;  // no_tail: frames emitted directly in a mode K1's tail lacks
   int n_tok_w64 = 0;                         // K7 streams on its 64-mask-word instantiation (first in tokdesc)
+  bool k2_modes = false;                     // K2 writes some frame in a non-RGBA colorspace (FrameDesc::emit)
   wg_decoder_options opt{};          // output colorspace, cropping, flip (f4)
   bool any_crop = false;             // K2 reads compact cropped planes through desc2
   bool fused = false;                // lossy RGBA emitted by K1's tail (wg::kFrameEmitRgba), no K2 launch
@@ -926,6 +927,8 @@ int batch_upload(wg_batch* b, const wg::StagingArena& arena) {
       d.rgba_stride = b->out_bpp * f.out_w;
       d.emit = b->opt.colorspace + 1;
       d.emit_flip = b->opt.flip ? 1 : 0;
+      // (RGBA and rgbA of these opaque frames are the plain RGBA stores, flipped or not)
+      b->k2_modes |= b->opt.colorspace != 1 && b->opt.colorspace != 7;
     }
   }
   // Fewer frames than CUs: K1's split kernel (split_k1_parts); it has no RGBA tail, K2 converts.
@@ -1101,7 +1104,7 @@ int wg_batch_run(wg_batch* b, void* stream) {
     }
     hipError_t e = wg::launch_yuv_to_rgba((b->any_crop ? b->d_desc2 : b->d_desc) + k2_from, nullptr, b->n - k2_from,
                                           b->max_out_w, b->max_out_h, (b->flags & WG_FLAG_NO_FANCY_UPSAMPLING) ? 0 : 1,
-                                          s);
+                                          s, b->k2_modes);
     if (e != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
   }
   hipEventRecord(t.ev[kStageK7], s);
@@ -1213,7 +1216,7 @@ int wg_batch_run_emit(wg_batch* b, void* stream) {
   t.ran[kStageK2] = true;
   for (int k = 0; k <= kStageK2; ++k) hipEventRecord(t.ev[k], s);
   hipError_t e = wg::launch_yuv_to_rgba(b->d_desc, nullptr, b->n, b->max_out_w, b->max_out_h,
-                                        (b->flags & WG_FLAG_NO_FANCY_UPSAMPLING) ? 0 : 1, s);
+                                        (b->flags & WG_FLAG_NO_FANCY_UPSAMPLING) ? 0 : 1, s, b->k2_modes);
   for (int k = kStageK2 + 1; k <= kStages; ++k) hipEventRecord(t.ev[k], s);
   if (e != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
   return batch_mark_done(b, s) == hipSuccess ? WG_STATUS_OK : WG_STATUS_OUT_OF_MEMORY;
@@ -1444,8 +1447,10 @@ int decode_pipelined(wg_ctx* ctx, const uint8_t* const* data, const size_t* size
     c.n = bounds[(size_t)k + 1] - c.a;
     c.arena = k % kRing;
     c.s = streams[k & 1];
+    // (blocking-sync events: the device thread's waits sleep instead of spinning on a CPU the
+    // entropy stage's 16 threads are using)
     for (hipEvent_t& e : c.ev)
-      if (hipEventCreate(&e) != hipSuccess) {
+      if (hipEventCreateWithFlags(&e, hipEventBlockingSync) != hipSuccess) {
         (void)hipGetLastError();
         e = nullptr;
         fail_frames(status, 0, n, WG_STATUS_OUT_OF_MEMORY);

@@ -21,7 +21,7 @@ hipError_t launch_vp8_recon_filter(const FrameDesc* d_frames, int n_frames, int 
 // K2: YUV420 -> RGBA (fancy 9-3-3-1 upsampling or point sampling) over a batch.
 // `single` (when non-null, n_frames == 1) is passed by value instead of d_frames.
 hipError_t launch_yuv_to_rgba(const FrameDesc* d_frames, const FrameDesc* single, int n_frames,
-                              int max_w, int max_h, int fancy, hipStream_t stream);
+                              int max_w, int max_h, int fancy, hipStream_t stream, bool modes = false);
 
 // K3: VP8L inverse transforms + BGRA->RGBA, one 1024-thread workgroup per lossless frame.
 size_t vp8l_lds_bytes();

@@ -588,7 +588,7 @@ __device__ __forceinline__ void emit_tail(const FrameDesc& F, uint32_t* progress
       if (lane == 0) atomicOr(err, 1);
       return;
     }
-    strip::convert_strip<kFancy, strip::kAuxSc1, false>(F, tx, band, lane);  // (RGBA / RGB_565 only)
+    strip::convert_strip<kFancy, strip::kAuxSc1, strip::kModesTail>(F, tx, band, lane);  // (RGBA / RGB_565 only)
   }
 }
 

@@ -251,15 +251,22 @@ __device__ __forceinline__ u32x4 conv4(u32x4 p) {
   return u32x4{emit_px<M>(p.x), emit_px<M>(p.y), emit_px<M>(p.z), emit_px<M>(p.w)};
 }
 
-// em = FrameDesc::emit (wave-uniform): 0 RGBA, else 1 + the mode.  kAllModes false (K1's tail,
-// whose code size is kept down: the switch sits at each of its eight unrolled store sites): RGBA,
-// rgbA and RGB_565 only -- capi.cpp sends batches in the other modes through K2.
-template <int kAux, bool kAllModes>
+// em = FrameDesc::emit (wave-uniform): 0 RGBA, else 1 + the mode.  kModes: kModesRgba = RGBA only
+// (K2 over batches without direct emission: no per-store mode test in the stage the metric names),
+// kModesTail = RGBA, rgbA and RGB_565 (K1's tail, whose code size is kept down: the switch sits at
+// each of its eight unrolled store sites; capi.cpp sends batches in the other modes through K2),
+// kModesAll = every mode (K2).
+constexpr int kModesRgba = 0, kModesTail = 1, kModesAll = 2;
+template <int kAux, int kModes>
 __device__ __forceinline__ void store_out(__amdgpu_buffer_rsrc_t o, int em, uint32_t roff, int x, u32x4 px, int nvalid,
                                           bool full) {
+  if (kModes == kModesRgba) {
+    store_group<kAux>(o, roff + 4u * (uint32_t)x, px, nvalid, full);
+    return;
+  }
   int bpp = 4;
   u32x4 c = px;
-  if (kAllModes) {
+  if (kModes == kModesAll) {
     switch (em) {
       case 1: c = conv4<0>(px), bpp = 3; break;            // RGB
       case 3: c = conv4<2>(px), bpp = 3; break;            // BGR
@@ -300,7 +307,7 @@ __device__ __forceinline__ int n_bands(int H, bool fancy) {
   return (npairs + kPairs - 1) / kPairs;
 }
 
-template <bool kFancy, int kAux, bool kAllModes = true>
+template <bool kFancy, int kAux, int kModes>
 __device__ __forceinline__ void convert_strip(const FrameDesc& F, int tx, int band, int lane) {
   const int W = F.width, H = F.height;
   const int uv_w = (W + 1) >> 1, uv_h = (H + 1) >> 1;
@@ -365,8 +372,8 @@ __device__ __forceinline__ void convert_strip(const FrameDesc& F, int tx, int ba
       for (int k = 0; k < kGroups; ++k) {
         const int x = xl + 256 * k;
         if (!live(k)) continue;
-        if (ya >= 0) store_out<kAux, kAllModes>(out, em, roff(ya), x, convert_group(prv, cur, k, yA[k]), W - x, full(k));
-        if (yb < H) store_out<kAux, kAllModes>(out, em, roff(yb), x, convert_group(cur, prv, k, yB[k]), W - x, full(k));
+        if (ya >= 0) store_out<kAux, kModes>(out, em, roff(ya), x, convert_group(prv, cur, k, yA[k]), W - x, full(k));
+        if (yb < H) store_out<kAux, kModes>(out, em, roff(yb), x, convert_group(cur, prv, k, yB[k]), W - x, full(k));
       }
       raw_cur = raw_next;
       // K1's tail yields the SIMD for a moment after each pair: its denser packed code otherwise
@@ -402,7 +409,7 @@ __device__ __forceinline__ void convert_strip(const FrameDesc& F, int tx, int ba
           const uint32_t yw = r ? yB[k] : yA[k];
           const uint2 a = yuv_to_rgba2(luma_lanes(yw, 0, 1), u0, v0), b = yuv_to_rgba2(luma_lanes(yw, 2, 3), u1, v1);
           const u32x4 px{a.x, a.y, b.x, b.y};
-          store_out<kAux, kAllModes>(out, em, roff(yr), x, px, W - x, full(k));
+          store_out<kAux, kModes>(out, em, roff(yr), x, px, W - x, full(k));
         }
       }
     }

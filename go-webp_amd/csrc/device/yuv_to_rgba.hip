@@ -16,7 +16,9 @@ namespace {
 
 constexpr int kWavesPerWG = 4;
 
-template <bool kFancy>
+// kModes: strip::kModesRgba (no frame of the launch is emitted directly: the plain RGBA stores) or
+// kModesAll (frames written straight in their output colorspace, FrameDesc::emit)
+template <bool kFancy, int kModes>
 __global__ void __launch_bounds__(64 * kWavesPerWG) yuv_to_rgba_kernel(const FrameDesc* __restrict__ frames,
                                                                        FrameDesc single, int use_single) {
   const FrameDesc& F = use_single ? single : frames[blockIdx.y];
@@ -24,25 +26,28 @@ __global__ void __launch_bounds__(64 * kWavesPerWG) yuv_to_rgba_kernel(const Fra
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int sx = strip::strips_x(F.width);
   const int tx = blockIdx.x % sx, ty = blockIdx.x / sx;
-  strip::convert_strip<kFancy, strip::kAuxNt>(F, tx, ty * kWavesPerWG + wave, lane);
+  strip::convert_strip<kFancy, strip::kAuxNt, kModes>(F, tx, ty * kWavesPerWG + wave, lane);
 }
 
 }  // namespace
 
 hipError_t launch_yuv_to_rgba(const FrameDesc* d_frames, const FrameDesc* single, int n_frames, int max_w,
-                              int max_h, int fancy, hipStream_t stream) {
+                              int max_h, int fancy, hipStream_t stream, bool modes) {
   const int strips_x = (max_w + strip::kStripPx - 1) / strip::kStripPx;
   const int npairs = (max_h >> 1) + 1;
   const int strips_y = (npairs + strip::kPairs * kWavesPerWG - 1) / (strip::kPairs * kWavesPerWG);
   const dim3 grid(strips_x * strips_y, single ? 1 : n_frames);
   FrameDesc s{};
   if (single) s = *single;
-  if (fancy)
-    hipLaunchKernelGGL(yuv_to_rgba_kernel<true>, grid, dim3(64 * kWavesPerWG), 0, stream, d_frames, s,
-                       single ? 1 : 0);
-  else
-    hipLaunchKernelGGL(yuv_to_rgba_kernel<false>, grid, dim3(64 * kWavesPerWG), 0, stream, d_frames, s,
-                       single ? 1 : 0);
+  const dim3 block(64 * kWavesPerWG);
+  const int us = single ? 1 : 0;
+  if (modes) {
+    if (fancy) hipLaunchKernelGGL((yuv_to_rgba_kernel<true, strip::kModesAll>), grid, block, 0, stream, d_frames, s, us);
+    else hipLaunchKernelGGL((yuv_to_rgba_kernel<false, strip::kModesAll>), grid, block, 0, stream, d_frames, s, us);
+  } else {
+    if (fancy) hipLaunchKernelGGL((yuv_to_rgba_kernel<true, strip::kModesRgba>), grid, block, 0, stream, d_frames, s, us);
+    else hipLaunchKernelGGL((yuv_to_rgba_kernel<false, strip::kModesRgba>), grid, block, 0, stream, d_frames, s, us);
+  }
   return hipGetLastError();
 }
 
