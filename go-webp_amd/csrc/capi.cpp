@@ -927,8 +927,9 @@ int batch_upload(wg_batch* b, const wg::StagingArena& arena) {
       d.rgba_stride = b->out_bpp * f.out_w;
       d.emit = b->opt.colorspace + 1;
       d.emit_flip = b->opt.flip ? 1 : 0;
-      // (RGBA and rgbA of these opaque frames are the plain RGBA stores, flipped or not)
-      b->k2_modes |= b->opt.colorspace != 1 && b->opt.colorspace != 7;
+      // (RGBA and rgbA of these opaque frames are the plain RGBA stores; K2's RGBA-only kernel
+      // does not flip)
+      b->k2_modes |= (b->opt.colorspace != 1 && b->opt.colorspace != 7) || b->opt.flip;
     }
   }
   // Fewer frames than CUs: K1's split kernel (split_k1_parts); it has no RGBA tail, K2 converts.

@@ -251,8 +251,9 @@ __device__ __forceinline__ u32x4 conv4(u32x4 p) {
   return u32x4{emit_px<M>(p.x), emit_px<M>(p.y), emit_px<M>(p.z), emit_px<M>(p.w)};
 }
 
-// em = FrameDesc::emit (wave-uniform): 0 RGBA, else 1 + the mode.  kModes: kModesRgba = RGBA only
-// (K2 over batches without direct emission: no per-store mode test in the stage the metric names),
+// em = FrameDesc::emit (wave-uniform): 0 RGBA, else 1 + the mode.  kModes: kModesRgba = RGBA only,
+// unflipped (K2 over batches without direct emission: no per-store mode or flip test in the stage
+// the metric names),
 // kModesTail = RGBA, rgbA and RGB_565 (K1's tail, whose code size is kept down: the switch sits at
 // each of its eight unrolled store sites; capi.cpp sends batches in the other modes through K2),
 // kModesAll = every mode (K2).
@@ -315,7 +316,7 @@ __device__ __forceinline__ void convert_strip(const FrameDesc& F, int tx, int ba
   const int cb0 = xl >> 1;
   // output: RGBA, or (emit) the frame's mode, rows bottom-up with emit_flip
   int em = __builtin_amdgcn_readfirstlane(F.emit);
-  const bool flip = __builtin_amdgcn_readfirstlane(F.emit_flip) != 0;
+  const bool flip = kModes != kModesRgba && __builtin_amdgcn_readfirstlane(F.emit_flip) != 0;  // (K2's RGBA-only kernel: never)
   const int bpp = em ? bpp_of(em - 1) : 4;
   const bool aligned = ((F.rgba_stride & (bpp == 4 ? 15 : 3)) == 0) && ((reinterpret_cast<uintptr_t>(F.rgba) & 15) == 0);
   // per group k, from the wave's first pixel x0 (scalar): some lane's group lies in the frame
