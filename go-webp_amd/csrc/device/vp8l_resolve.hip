@@ -648,6 +648,12 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
       // carries none of it.
       auto lookups = [&](const int fp, auto kRoundsC) __attribute__((always_inline)) {
         constexpr bool kRounds = decltype(kRoundsC)::value;
+        if constexpr (kW64) {  // (dense streams: most waves hold no lookup at all)
+          uint32_t any_pl = 0;
+#pragma unroll
+          for (int j = 0; j < kPer; ++j) any_pl |= (uint32_t)(pk(ps, j) == kPL);
+          if (!__any(any_pl)) return;
+        }
         // (a) lookups before the first pending copy: the key's last updater in the window if it
         //     precedes the pixel, none (the slot as the previous window left it), or -- it
         //     straddles the pixel -- the highest mask bit below the pixel's rank count
@@ -764,7 +770,8 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
           uint32_t pcm = 0;    // my pending copies (slot bits)
 #pragma unroll
           for (int j = 0; j < kPer; ++j) pcm |= (uint32_t)(pk(ps, j) == kPC) << j;
-          if (in_win && wave_pc && nkeys) {  // this wave's rank flags (the scratch held lookups)
+          const bool wpend = __any(pcm != 0);  // (later rounds: most waves have nothing pending)
+          if (in_win && wpend && nkeys) {  // this wave's rank flags (the scratch held lookups)
 #pragma unroll
             for (int j = 0; j < kPer; ++j)
               if (is_upd(ps, j)) rflag[R(j) - rb] = 0;
@@ -818,7 +825,7 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
               }
             }
           }
-          if (in_win && wave_pc) {
+          if (in_win && wpend) {
             wave_min_pos(&first_pend[(r + 1) & 1], myfp);
             // the copies resolved this round register by rank (consecutive across lanes: combined per key)
             if (nkeys && __any(got)) reg_pass(woff - rb, my_wc, true);
