@@ -480,7 +480,7 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
     }
     // ranks: updaters before each pixel, a block-wide prefix count (per-thread count 0..4 in
     // three ballots).  wsum: the wave's updaters, bit 16 a copy reaching back past the last
-    // block, bit 17 an in-block copy (pending).
+    // block, bit 17 an in-block copy (pending), bit 18 (kW64) a cache lookup.
     const uint32_t cm = ps & (ps >> 1) & 0x55u, pm = ps & ~(ps >> 1) & 0x55u;  // codes kPF / kPC
     const bool my_pc = pm != 0u;
     const bool wave_pc = __any(my_pc);
@@ -488,9 +488,10 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
     const uint64_t b0 = __ballot(cnt & 1), b1 = __ballot(cnt & 2), b2 = __ballot(cnt & 4);
     const int excl = count_below(b0) + 2 * count_below(b1) + 4 * count_below(b2);
     const bool wave_far = __any(cm != 0u);
+    const bool wave_pl = kW64 && __any((~ps & (ps >> 1) & 0x55u) != 0u);  // (kW64) a cache lookup, code kPL
     if (lane == 0)
       wsum[wave] = (uint32_t)(__builtin_popcountll(b0) + 2 * __builtin_popcountll(b1) + 4 * __builtin_popcountll(b2)) |
-                   (wave_far ? 0x10000u : 0u) | (wave_pc ? 0x20000u : 0u);
+                   (wave_far ? 0x10000u : 0u) | (wave_pc ? 0x20000u : 0u) | (wave_pl ? 0x40000u : 0u);
     bar();
     K7_T(4);
     // the sixteen wave counts in lanes 0..15 (one DPP row): inclusive scan, then read lanes
@@ -506,6 +507,9 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
     const int woff = __builtin_amdgcn_readlane(scan, wave) - my_wc;
     const uint64_t fl = __ballot(lane < 16 && (wraw & 0x10000u)), plm = __ballot(lane < 16 && (wraw & 0x20000u));
     const bool blk_pc = plm != 0;
+    // kW64: a block with no cache lookup needs no rank masks -- only each key's last updater for
+    // the slot table (one max pass after the rounds); most ALPH blocks have none
+    const bool blk_pl = !kW64 || __ballot(lane < 16 && (wraw & 0x40000u)) != 0;
     // windows: the fewest (1, 2, 4, 8 or 16 runs of whole waves) with at most `cap` updaters
     // each (a one-wave window has at most 256 <= cap); almost always one
     auto prefix = [&](int w) { return w <= 0 ? 0 : __builtin_amdgcn_readlane(scan, w - 1); };  // waves < w
@@ -602,7 +606,7 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
 #pragma unroll
         for (int j = 0; j < kPer; ++j)
           if (in_win && is_upd(ps, j) && pk(ps, j) == kPK) ds_write_u32(&uval[R(j) - rb], v[j]);
-        if (in_win && nkeys) {
+        if (in_win && nkeys && blk_pl) {
           if (wave_pc) {
 #pragma unroll
             for (int j = 0; j < kPer; ++j)
@@ -771,7 +775,8 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
 #pragma unroll
           for (int j = 0; j < kPer; ++j) pcm |= (uint32_t)(pk(ps, j) == kPC) << j;
           const bool wpend = __any(pcm != 0);  // (later rounds: most waves have nothing pending)
-          if (in_win && wpend && nkeys) {  // this wave's rank flags (the scratch held lookups)
+          const bool regs = nkeys && blk_pl;  // copies register as they resolve (lookups follow)
+          if (in_win && wpend && regs) {  // this wave's rank flags (the scratch held lookups)
 #pragma unroll
             for (int j = 0; j < kPer; ++j)
               if (is_upd(ps, j)) rflag[R(j) - rb] = 0;
@@ -816,7 +821,7 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 st[li] = kKnown;
                 uval[R(j) - rb] = x;
-                rflag[R(j) - rb] = 2;
+                if (regs) rflag[R(j) - rb] = 2;
                 got = true;
               } else {
                 if (ss[j] == kPendCopy) ref[li] = (int16_t)nref[j];  // (a stale or fresh link: both lie on the chain)
@@ -828,7 +833,7 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
           if (in_win && wpend) {
             wave_min_pos(&first_pend[(r + 1) & 1], myfp);
             // the copies resolved this round register by rank (consecutive across lanes: combined per key)
-            if (nkeys && __any(got)) reg_pass(woff - rb, my_wc, true);
+            if (regs && __any(got)) reg_pass(woff - rb, my_wc, true);
           }
         } else if (in_win) {
 #pragma unroll
@@ -859,6 +864,32 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
       }
       bar();  // every lookup has read the slot table; the masks are complete
       const bool go_serial = slow[b & 1] != 0;
+      if constexpr (kW64) {
+        // a block without lookups registered nothing: each key's last updater (slotrec.x) from one
+        // pass over the ranks, combined per key like reg_run
+        if (!blk_pl && nkeys && !go_serial) {
+          if (in_win) {
+            for (int i0 = 0; i0 < my_wc; i0 += 64) {
+              const int r = woff - rb + i0 + lane;
+              const bool valid = i0 + lane < my_wc;
+              const uint32_t h = hash_px(uval[valid ? r : 0], shift);
+              bool pend = valid;
+              for (int it = 0; it < 8; ++it) {
+                const uint64_t pm = __ballot(pend);
+                if (pm == 0) break;
+                const int lead = __builtin_ctzll(pm);
+                const uint32_t hl = (uint32_t)__builtin_amdgcn_readlane((int)h, lead);
+                const uint64_t m = __ballot(pend && h == hl);
+                if (lane == lead) ds_max_u32(&slotrec[hl].x, (uint32_t)(woff - rb + i0 + 63 - __builtin_clzll(m)) + 1u);
+                pend = pend && h != hl;
+                if (__builtin_popcountll(m) < 4) break;
+              }
+              if (pend) ds_max_u32(&slotrec[h].x, (uint32_t)r + 1u);
+            }
+          }
+          bar();
+        }
+      }
       // ---- 3. each key's last updater writes its slot and clears the key's masks
       // the window's updaters packed 64 to a wave by rank (uval is complete after the barrier):
       // C5's ~143 per block take three waves' single pass instead of a sparse pass in each of

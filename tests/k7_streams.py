@@ -22,11 +22,12 @@ def hash_px(v, bits):
 
 
 def make_stream(n, bits, seed, p_lit=0.035, p_copy=0.0, dist=(1,), palette=256, width=2048, run=1,
-                p_empty=0.0, chain=False):
+                p_empty=0.0, chain=False, quiet=()):
     """-> (tokens uint32[n], lits uint32[]).  p_lit / p_copy: probabilities of a literal / a copy
     run (length 1..run, distances drawn from `dist`: ints, or "w" (the row above), "near"
     (1..64), "far" (4096..20000)); the rest are cache lookups of keys whose slot holds a value
-    (p_empty of them of a never-written slot instead).  chain: alternate one-pixel copies of
+    (p_empty of them of a never-written slot instead).  quiet: (start, end) pixel ranges with no
+    lookups (their lookups become copies): lookup-free blocks between blocks with lookups.  chain: alternate one-pixel copies of
     distance 1 and lookups (each copy's source is a lookup: one round per pair)."""
     rng = np.random.default_rng(seed)
     pal = rng.integers(0, 1 << 32, size=palette, dtype=np.uint64).astype(np.uint32)
@@ -69,7 +70,7 @@ def make_stream(n, bits, seed, p_lit=0.035, p_copy=0.0, dist=(1,), palette=256, 
             vals.append(v)
             insert(v)
             i += 1
-        elif r < p_lit + p_copy or not nk:
+        elif r < p_lit + p_copy or not nk or any(a <= i < e for a, e in quiet):
             d = dist[int(rng.integers(len(dist)))]
             if d == "w":
                 d = width
@@ -176,4 +177,8 @@ CASES = [
     # straddling updaters of their key in the words above 32
     ("w64_straddle", 4 * 4096 + 21, 6, dict(p_lit=0.55, p_copy=0.35, dist=(1, 2, "near"), run=4, palette=90)),
     ("w64_b7_lits", 3 * 4096 + 5, 7, dict(p_lit=0.9, p_copy=0.02, palette=400)),
+    # lookup-free blocks (no rank masks: the slot table from one max pass) between blocks whose
+    # lookups read what they left
+    ("w64_quiet_blocks", 6 * 4096 + 17, 4, dict(p_lit=0.1, p_copy=0.8, dist=(1, "w", 3), run=30, width=900,
+                                                palette=40, quiet=((4096, 3 * 4096), (4 * 4096 + 100, 5 * 4096 + 7)))),
 ]
