@@ -176,3 +176,24 @@ def test_k7_random_streams():
         got = device_resolve(toks, lits, bits)
         bad = np.nonzero(got != want)[0]
         assert bad.size == 0, f"case {case} (n={n}, bits={bits}, {kw}): {bad.size} pixels differ, first at {bad[:5]}"
+
+
+def test_k7_random_dense_streams():
+    """Randomised dense streams for the small-cache instantiation (cache_bits 0..7): nearly every
+    pixel a copy (runs up to 3,000 of distance 1, one row, or short distances), few literals, a
+    few lookups, and random lookup-free stretches -- each bit-exact against the oracle."""
+    rng = np.random.default_rng(20261018)
+    dist_sets = [(1,), (1, "w"), (1, 1, "w", 2), ("w", "near"), (1, 3, "near")]
+    for case in range(16):
+        bits = int(rng.integers(0, 8))
+        n = int(rng.integers(4096, 5 * 4096 + 300))
+        p_lit = float(rng.uniform(0.003, 0.15))
+        a = int(rng.integers(0, n))
+        kw = dict(p_lit=p_lit, p_copy=float(rng.uniform(0.6, 0.995 - p_lit)), dist=dist_sets[int(rng.integers(len(dist_sets)))],
+                  run=int(rng.integers(2, 3000)), palette=int(rng.integers(2, 64)), width=int(rng.integers(64, 2048)),
+                  quiet=((a, a + int(rng.integers(0, 2 * 4096))),))
+        toks, lits = k7_streams.make_stream(n, bits, seed=2000 + case, **kw)
+        want = oracle_resolve(toks, lits, bits)
+        got = device_resolve(toks, lits, bits)
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, f"case {case} (bits {bits}, {kw}): {bad.size} pixels differ, first at {bad[:5]}"
