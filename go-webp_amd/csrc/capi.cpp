@@ -172,6 +172,9 @@ struct wg_ctx {
   // upload -- so an upload never queues behind an earlier chunk's download
   std::unique_ptr<wg::StagingArena> arena_ring[2];  // with `arena`, a ring of three
   hipStream_t work[2] = {nullptr, nullptr};
+  // K7 beside K1 / K2 (wg_batch_run: small batches whose grids fit on the chip together)
+  hipStream_t side = nullptr;
+  std::mutex side_mu;
   int chunk_frames = 0;  // frames per pipeline chunk, 0 = automatic (wg_ctx_set_chunk_frames)
   wg_pipeline_stats stats{};  // of the last pipelined decode
   wg::WorkerPool* workers() {
@@ -193,7 +196,23 @@ constexpr int kPublicOfStage[kStages] = {0, 1, 4, 2, 3, 5, 6};
 struct Timing {
   hipEvent_t ev[kStages + 1] = {};
   bool ran[kStages] = {};
+  hipEvent_t side[2] = {};  // K7's start / end when it ran on the context's side stream
+  bool forked = false;
 };
+
+hipError_t timing_create(Timing& t) {
+  for (auto& e : t.ev)
+    if (hipError_t r = hipEventCreate(&e); r != hipSuccess) return r;
+  for (auto& e : t.side)
+    if (hipError_t r = hipEventCreate(&e); r != hipSuccess) return r;
+  return hipSuccess;
+}
+void timing_destroy(Timing& t) {
+  for (auto& e : t.ev)
+    if (e) hipEventDestroy(e);
+  for (auto& e : t.side)
+    if (e) hipEventDestroy(e);
+}
 
 }  // namespace
 
@@ -470,6 +489,7 @@ void wg_ctx_destroy(wg_ctx* c) {
   if (dev_ok && c->stream) hipStreamSynchronize(c->stream);
   for (hipStream_t w : c->work)
     if (dev_ok && w) hipStreamSynchronize(w);
+  if (dev_ok && c->side) hipStreamSynchronize(c->side);
   c->pool.reset();
   c->arena.reset();
   for (auto& a : c->arena_ring) a.reset();
@@ -477,6 +497,7 @@ void wg_ctx_destroy(wg_ctx* c) {
   if (c->stream) hipStreamDestroy(c->stream);
   for (hipStream_t w : c->work)
     if (w) hipStreamDestroy(w);
+  if (c->side) hipStreamDestroy(c->side);
   delete c;
 }
 
@@ -496,9 +517,7 @@ int wg_set_default_device(int device) {
 void wg_batch_destroy(wg_batch* b) {
   if (!b) return;
   if (set_device(b->ctx->device)) batch_wait(b);  // nothing may still use the buffers handed back to the cache
-  for (auto& t : b->timings)
-    for (auto& e : t.ev)
-      if (e) hipEventDestroy(e);
+  for (auto& t : b->timings) timing_destroy(t);
   for (auto& d : b->done) hipEventDestroy(d.second);
   DeviceCache& c = b->ctx->cache;
   c.put(b->d_desc);
@@ -1048,6 +1067,26 @@ wg_batch* batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t* si
 
 extern "C" {
 
+namespace {
+// The context's side stream for K7 when K1's and K7's grids fit on the chip together (one
+// workgroup per CU each: K1's one-workgroup or split kernel, one K7 workgroup per stream), else
+// null.  Created on first use.  WG_K7_SIDE=0 keeps K7 on the batch's stream.
+hipStream_t k7_side_stream(wg_batch* b) {
+  static const bool off = [] {
+    const char* e = getenv("WG_K7_SIDE");
+    return e && atoi(e) == 0;
+  }();
+  constexpr int kCUs = 256;
+  const int head = b->split_parts >= 2 ? b->split_from : b->n;
+  const int k1_wgs = head + (b->split_parts >= 2 ? (b->n - head + 7) / 8 * 8 * b->split_parts : 0);
+  if (off || k1_wgs + (int)b->tokdesc.size() > kCUs) return nullptr;
+  wg_ctx* c = b->ctx;
+  std::lock_guard<std::mutex> lock(c->side_mu);
+  if (!c->side && hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess) c->side = nullptr;
+  return c->side;
+}
+}  // namespace
+
 int wg_batch_run(wg_batch* b, void* stream) {
   if (!b) return WG_STATUS_INVALID_PARAM;
   if (b->n_valid == 0) return WG_STATUS_OK;
@@ -1055,8 +1094,10 @@ int wg_batch_run(wg_batch* b, void* stream) {
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : b->home;
   if (b->n_runs_pending >= b->timings.size()) {
     Timing t;
-    for (auto& e : t.ev)
-      if (hipEventCreate(&e) != hipSuccess) return WG_STATUS_OUT_OF_MEMORY;
+    if (timing_create(t) != hipSuccess) {
+      timing_destroy(t);
+      return WG_STATUS_OUT_OF_MEMORY;
+    }
     b->timings.push_back(t);
   }
   Timing& t = b->timings[b->n_runs_pending++];
@@ -1070,6 +1111,17 @@ int wg_batch_run(wg_batch* b, void* stream) {
   t.ran[kStageK6] = b->k6 && b->n_k6 > 0;
   t.ran[kStageK5] = b->anim;
   hipEventRecord(t.ev[kStageK1], s);
+  // K7 only feeds K3 / K4: when its grid fits on the chip beside K1's, it runs on the context's
+  // side stream, concurrently with K1 and K2, and K3 waits for it
+  hipStream_t side = b->n_lossy > 0 && b->n_k3 > 0 ? k7_side_stream(b) : nullptr;
+  t.forked = side != nullptr;
+  if (side) {
+    hipError_t e = hipStreamWaitEvent(side, t.ev[kStageK1], 0);
+    if (e == hipSuccess) e = hipEventRecord(t.side[0], side);
+    if (e == hipSuccess) e = wg::launch_vp8l_resolve(b->d_tokdesc, nullptr, (int)b->tokdesc.size(), b->d_err, side, b->n_tok_w64);
+    if (e == hipSuccess) e = hipEventRecord(t.side[1], side);
+    if (e != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
+  }
   if (b->n_lossy > 0) {
     hipError_t e = hipSuccess;
     const int head = b->split_parts >= 2 ? b->split_from : b->n;  // frames on the one-workgroup kernels
@@ -1109,7 +1161,9 @@ int wg_batch_run(wg_batch* b, void* stream) {
     if (e != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
   }
   hipEventRecord(t.ev[kStageK7], s);
-  if (b->n_k3 > 0) {  // K7: the lossless streams' color cache and back-references
+  if (t.forked) {
+    if (hipStreamWaitEvent(s, t.side[1], 0) != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
+  } else if (b->n_k3 > 0) {  // K7: the lossless streams' color cache and back-references
     hipError_t e = wg::launch_vp8l_resolve(b->d_tokdesc, nullptr, (int)b->tokdesc.size(), b->d_err, s, b->n_tok_w64);
     if (e != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
   }
@@ -1150,7 +1204,10 @@ int wg_batch_kernel_ms(const wg_batch* bc, float* ms, int n_ms) {
     for (int k = 0; k < kStages; ++k) {
       if (!t.ran[k]) continue;
       float a = 0;
-      hipEventElapsedTime(&a, t.ev[k], t.ev[k + 1]);
+      if (k == kStageK7 && t.forked)
+        hipEventElapsedTime(&a, t.side[0], t.side[1]);
+      else
+        hipEventElapsedTime(&a, t.ev[k], t.ev[k + 1]);
       acc[k] += a;
       cnt[k]++;
     }
@@ -1208,12 +1265,15 @@ int wg_batch_run_emit(wg_batch* b, void* stream) {
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : b->home;
   if (b->n_runs_pending >= b->timings.size()) {
     Timing t;
-    for (auto& e : t.ev)
-      if (hipEventCreate(&e) != hipSuccess) return WG_STATUS_OUT_OF_MEMORY;
+    if (timing_create(t) != hipSuccess) {
+      timing_destroy(t);
+      return WG_STATUS_OUT_OF_MEMORY;
+    }
     b->timings.push_back(t);
   }
   Timing& t = b->timings[b->n_runs_pending++];
   for (bool& r : t.ran) r = false;
+  t.forked = false;
   t.ran[kStageK2] = true;
   for (int k = 0; k <= kStageK2; ++k) hipEventRecord(t.ev[k], s);
   hipError_t e = wg::launch_yuv_to_rgba(b->d_desc, nullptr, b->n, b->max_out_w, b->max_out_h,
