@@ -198,6 +198,7 @@ struct Timing {
   bool ran[kStages] = {};
   hipEvent_t side[2] = {};  // K7's start / end when it ran on the context's side stream
   bool forked = false;
+  int8_t order[kStages] = {0, 1, 2, 3, 4, 5, 6};  // launch order: ev[i] .. ev[i + 1] bracket stage order[i]
 };
 
 hipError_t timing_create(Timing& t) {
@@ -236,6 +237,7 @@ struct wg_batch {
   wg_decoder_options opt{};          // output colorspace, cropping, flip (f4)
   bool any_crop = false;             // K2 reads compact cropped planes through desc2
   bool fused = false;                // lossy RGBA emitted by K1's tail (wg::kFrameEmitRgba), no K2 launch
+  bool alpha_first = false;          // K4 before K1: the strips take A from K4's planes (batch_upload)
   std::vector<FrameDesc> desc2;
   FrameDesc* d_desc2 = nullptr;
   int max_out_w = 1, max_out_h = 1;
@@ -766,10 +768,10 @@ void batch_layout(wg_batch* b, wg::StagingArena& arena, int32_t* status) {
       } else {
         k4 += px;
       }
-      if (!f.alpha_direct) {
-        f.off_aplane = pl_b;
-        pl_b = align_up(pl_b + (size_t)f.width * f.height);
-      }
+      // (a scratch plane for every alpha frame: vertical / gradient unfilter in it, and
+      // alpha-first batches leave every unfiltered plane there)
+      f.off_aplane = pl_b;
+      pl_b = align_up(pl_b + (size_t)f.width * f.height);
       k4 += 8.0 * px;
     }
   }
@@ -841,6 +843,20 @@ int split_k1_parts(const wg_batch* b, int* from = nullptr) {
   if (parts < 2 || parts < want) return 1;
   if (from) *from = head;
   return parts;
+}
+
+// K7 can run beside K1 / K2 (wg_batch_run) when their grids fit on the chip together: one
+// workgroup per CU each -- K1's one-workgroup or split kernel, one K7 workgroup per stream.
+// WG_K7_SIDE=0 keeps K7 in stream order.
+bool k7_side_fits(const wg_batch* b) {
+  static const bool off = [] {
+    const char* e = getenv("WG_K7_SIDE");
+    return e && atoi(e) == 0;
+  }();
+  constexpr int kCUs = 256;
+  const int head = b->split_parts >= 2 ? b->split_from : b->n;
+  const int k1_wgs = head + (b->split_parts >= 2 ? (b->n - head + 7) / 8 * 8 * b->split_parts : 0);
+  return !off && b->n_lossy > 0 && b->n_k3 > 0 && k1_wgs + (int)b->tokdesc.size() <= kCUs;
 }
 
 // Tags of the split kernel's progress flags: a fresh value per launch, never 0 (the flags are
@@ -967,6 +983,31 @@ int batch_upload(wg_batch* b, const wg::StagingArena& arena) {
   if (b->fused)
     for (int i = 0; i < n; ++i)
       if (b->desc[(size_t)i].valid) b->desc[(size_t)i].flags |= wg::kFrameEmitRgba;
+  // Alpha-first: K7 -> K3 -> K4 before K1, K4 leaving each alpha plane unfiltered in its scratch
+  // plane and the YUV -> RGBA strips (K1's tail or K2) taking A from it -- instead of K4
+  // read-modify-writing the RGBA's A bytes afterwards (8 B/px -> 1 B/px written + 1 B/px read).
+  // Not with crop windows (K4 would need the window's plane), nor where K7 runs beside K1 (small
+  // batches: there the overlap is worth more).  WG_ALPHA_FIRST=0 disables it (measurement).
+  static const bool alpha_first_off = [] {
+    const char* e = getenv("WG_ALPHA_FIRST");
+    return e && atoi(e) == 0;
+  }();
+  b->alpha_first = b->n_alpha > 0 && !b->any_crop && !alpha_first_off && !k7_side_fits(b);
+  if (b->alpha_first) {
+    size_t j = 0;
+    for (int i = 0; i < n; ++i) {
+      const FrameParse& f = b->fp[(size_t)i];
+      if (f.status != WG_STATUS_OK || f.lossless || !f.alpha) continue;
+      AlphaDesc& a = b->adesc[j++];
+      a.plane = b->d_planes + f.off_aplane;
+      a.to_plane = 1;
+      b->desc[(size_t)i].alpha_off16 = (int32_t)((f.off_aplane - f.off_y) / 16);
+      const double px = (double)f.width * f.height;
+      b->kbytes[3] -= 7.0 * px;  // (K4: 1 B/px written instead of the 8 B/px read-modify-write)
+      b->k1_fused_bytes += px;   // (the strips read it: K1's tail, or K2)
+      b->kbytes[1] += px;
+    }
+  }
   if (b->any_crop) {  // K2's view: cropped lossy frames read their compact planes
     b->desc2 = b->desc;
     for (int i = 0; i < n; ++i) {
@@ -1068,18 +1109,10 @@ wg_batch* batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t* si
 extern "C" {
 
 namespace {
-// The context's side stream for K7 when K1's and K7's grids fit on the chip together (one
-// workgroup per CU each: K1's one-workgroup or split kernel, one K7 workgroup per stream), else
-// null.  Created on first use.  WG_K7_SIDE=0 keeps K7 on the batch's stream.
+// The context's side stream for K7 (k7_side_fits; not in alpha-first batches, whose K1 waits for
+// K4 and so for K7), else null.  Created on first use.
 hipStream_t k7_side_stream(wg_batch* b) {
-  static const bool off = [] {
-    const char* e = getenv("WG_K7_SIDE");
-    return e && atoi(e) == 0;
-  }();
-  constexpr int kCUs = 256;
-  const int head = b->split_parts >= 2 ? b->split_from : b->n;
-  const int k1_wgs = head + (b->split_parts >= 2 ? (b->n - head + 7) / 8 * 8 * b->split_parts : 0);
-  if (off || k1_wgs + (int)b->tokdesc.size() > kCUs) return nullptr;
+  if (b->alpha_first || !k7_side_fits(b)) return nullptr;
   wg_ctx* c = b->ctx;
   std::lock_guard<std::mutex> lock(c->side_mu);
   if (!c->side && hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess) c->side = nullptr;
@@ -1110,82 +1143,87 @@ int wg_batch_run(wg_batch* b, void* stream) {
   t.ran[kStageK4] = b->n_alpha > 0;
   t.ran[kStageK6] = b->k6 && b->n_k6 > 0;
   t.ran[kStageK5] = b->anim;
-  hipEventRecord(t.ev[kStageK1], s);
+  // launch order (ev[i] .. ev[i + 1] bracket stage order[i]): K1 / K2 first, or, alpha-first,
+  // the alpha planes (K7 -> K3 -> K4) before the strips that take A from them
+  static constexpr int8_t kOrderAlphaFirst[kStages] = {kStageK7, kStageK3, kStageK4, kStageK1,
+                                                       kStageK2, kStageK6, kStageK5};
+  for (int i = 0; i < kStages; ++i) t.order[i] = b->alpha_first ? kOrderAlphaFirst[i] : (int8_t)i;
+  hipEventRecord(t.ev[0], s);
   // K7 only feeds K3 / K4: when its grid fits on the chip beside K1's, it runs on the context's
   // side stream, concurrently with K1 and K2, and K3 waits for it
-  hipStream_t side = b->n_lossy > 0 && b->n_k3 > 0 ? k7_side_stream(b) : nullptr;
+  hipStream_t side = k7_side_stream(b);
   t.forked = side != nullptr;
   if (side) {
-    hipError_t e = hipStreamWaitEvent(side, t.ev[kStageK1], 0);
+    hipError_t e = hipStreamWaitEvent(side, t.ev[0], 0);
     if (e == hipSuccess) e = hipEventRecord(t.side[0], side);
     if (e == hipSuccess) e = wg::launch_vp8l_resolve(b->d_tokdesc, nullptr, (int)b->tokdesc.size(), b->d_err, side, b->n_tok_w64);
     if (e == hipSuccess) e = hipEventRecord(t.side[1], side);
     if (e != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
   }
-  if (b->n_lossy > 0) {
+  auto stage = [&](int k) -> int {
     hipError_t e = hipSuccess;
-    const int head = b->split_parts >= 2 ? b->split_from : b->n;  // frames on the one-workgroup kernels
-    if (head > 0)
-      e = wg::launch_vp8_recon_filter(b->d_desc, head, b->max_mb_w, b->n_lossy > b->n_wide, b->n_wide > 0, b->d_err, s);
-    if (e == hipSuccess && b->split_parts >= 2)
-      e = wg::launch_vp8_recon_filter(b->d_desc + head, b->n - head, b->max_mb_w, false, false, b->d_err, s,
-                                      b->split_parts, next_epoch());
-    if (e != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
-  }
-  hipEventRecord(t.ev[kStageK2], s);
-  if (t.ran[kStageK2]) {
-    if (b->any_crop) {
-      // the crop windows of the reconstructed planes (even left/top, so chroma is aligned):
-      // upsampled as standalone images, as EmitFancyRGB / EmitSampledRGB see them
-      for (int i = 0; i < b->n; ++i) {
-        const FrameParse& f = b->fp[i];
-        if (f.status != WG_STATUS_OK || f.lossless || !f.cropped) continue;
-        const FrameDesc& d = b->desc[i];
-        const FrameDesc& d2 = b->desc2[i];
-        const int x = b->opt.crop_left & ~1, y = b->opt.crop_top & ~1;
-        const int uw = (f.out_w + 1) >> 1, uh = (f.out_h + 1) >> 1;
-        hipError_t e = hipMemcpy2DAsync(d2.y, d2.y_stride, d.y + (size_t)y * d.y_stride + x, d.y_stride, f.out_w,
-                                        f.out_h, hipMemcpyDeviceToDevice, s);
-        if (e == hipSuccess)
-          e = hipMemcpy2DAsync(d2.u, d2.uv_stride, d.u + (size_t)(y >> 1) * d.uv_stride + (x >> 1), d.uv_stride, uw,
-                               uh, hipMemcpyDeviceToDevice, s);
-        if (e == hipSuccess)
-          e = hipMemcpy2DAsync(d2.v, d2.uv_stride, d.v + (size_t)(y >> 1) * d.uv_stride + (x >> 1), d.uv_stride, uw,
-                               uh, hipMemcpyDeviceToDevice, s);
-        if (e != hipSuccess) return WG_STATUS_USER_ABORT;
-      }
+    switch (k) {
+      case kStageK1:
+        if (b->n_lossy > 0) {
+          const int head = b->split_parts >= 2 ? b->split_from : b->n;  // frames on the one-workgroup kernels
+          if (head > 0)
+            e = wg::launch_vp8_recon_filter(b->d_desc, head, b->max_mb_w, b->n_lossy > b->n_wide, b->n_wide > 0, b->d_err, s);
+          if (e == hipSuccess && b->split_parts >= 2)
+            e = wg::launch_vp8_recon_filter(b->d_desc + head, b->n - head, b->max_mb_w, false, false, b->d_err, s,
+                                            b->split_parts, next_epoch());
+        }
+        break;
+      case kStageK2:
+        if (!t.ran[kStageK2]) break;
+        if (b->any_crop) {
+          // the crop windows of the reconstructed planes (even left/top, so chroma is aligned):
+          // upsampled as standalone images, as EmitFancyRGB / EmitSampledRGB see them
+          for (int i = 0; i < b->n; ++i) {
+            const FrameParse& f = b->fp[i];
+            if (f.status != WG_STATUS_OK || f.lossless || !f.cropped) continue;
+            const FrameDesc& d = b->desc[i];
+            const FrameDesc& d2 = b->desc2[i];
+            const int x = b->opt.crop_left & ~1, y = b->opt.crop_top & ~1;
+            const int uw = (f.out_w + 1) >> 1, uh = (f.out_h + 1) >> 1;
+            e = hipMemcpy2DAsync(d2.y, d2.y_stride, d.y + (size_t)y * d.y_stride + x, d.y_stride, f.out_w, f.out_h,
+                                 hipMemcpyDeviceToDevice, s);
+            if (e == hipSuccess)
+              e = hipMemcpy2DAsync(d2.u, d2.uv_stride, d.u + (size_t)(y >> 1) * d.uv_stride + (x >> 1), d.uv_stride, uw,
+                                   uh, hipMemcpyDeviceToDevice, s);
+            if (e == hipSuccess)
+              e = hipMemcpy2DAsync(d2.v, d2.uv_stride, d.v + (size_t)(y >> 1) * d.uv_stride + (x >> 1), d.uv_stride, uw,
+                                   uh, hipMemcpyDeviceToDevice, s);
+            if (e != hipSuccess) return WG_STATUS_USER_ABORT;
+          }
+        }
+        e = wg::launch_yuv_to_rgba((b->any_crop ? b->d_desc2 : b->d_desc) + k2_from, nullptr, b->n - k2_from,
+                                   b->max_out_w, b->max_out_h, (b->flags & WG_FLAG_NO_FANCY_UPSAMPLING) ? 0 : 1, s,
+                                   b->k2_modes);
+        break;
+      case kStageK7:  // the lossless streams' color cache and back-references
+        if (t.forked) e = hipStreamWaitEvent(s, t.side[1], 0);
+        else if (b->n_k3 > 0)
+          e = wg::launch_vp8l_resolve(b->d_tokdesc, nullptr, (int)b->tokdesc.size(), b->d_err, s, b->n_tok_w64);
+        break;
+      case kStageK3:
+        if (!b->lldesc.empty()) e = wg::launch_vp8l_transforms(b->d_lldesc, b->ll_groups, b->d_err, s);
+        break;
+      case kStageK4:  // after K3 (alpha streams) and K2 / K1's tail (A = 255), or alpha-first before them
+        if (b->n_alpha > 0) e = wg::launch_alpha(b->d_adesc, b->n_alpha, s);
+        break;
+      case kStageK6:  // the output colorspace / flip over every frame's final RGBA
+        if (t.ran[kStageK6]) e = wg::launch_emit(b->d_edesc, b->n, b->k6_maxpx, s);
+        break;
+      case kStageK5:  // an animation's canvases from its decoded frames
+        if (b->anim) e = wg::launch_anim_compose(b->d_fdesc, b->n, b->d_canvases, b->canvas_w, b->canvas_h, s);
+        break;
     }
-    hipError_t e = wg::launch_yuv_to_rgba((b->any_crop ? b->d_desc2 : b->d_desc) + k2_from, nullptr, b->n - k2_from,
-                                          b->max_out_w, b->max_out_h, (b->flags & WG_FLAG_NO_FANCY_UPSAMPLING) ? 0 : 1,
-                                          s, b->k2_modes);
-    if (e != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
-  }
-  hipEventRecord(t.ev[kStageK7], s);
-  if (t.forked) {
-    if (hipStreamWaitEvent(s, t.side[1], 0) != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
-  } else if (b->n_k3 > 0) {  // K7: the lossless streams' color cache and back-references
-    hipError_t e = wg::launch_vp8l_resolve(b->d_tokdesc, nullptr, (int)b->tokdesc.size(), b->d_err, s, b->n_tok_w64);
-    if (e != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
-  }
-  hipEventRecord(t.ev[kStageK3], s);
-  if (!b->lldesc.empty()) {
-    hipError_t e = wg::launch_vp8l_transforms(b->d_lldesc, b->ll_groups, b->d_err, s);
-    if (e != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
-  }
-  hipEventRecord(t.ev[kStageK4], s);
-  if (b->n_alpha > 0) {  // after K2 (A = 255) and K3 (alpha streams)
-    hipError_t e = wg::launch_alpha(b->d_adesc, b->n_alpha, s);
-    if (e != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
-  }
-  hipEventRecord(t.ev[kStageK6], s);
-  if (t.ran[kStageK6]) {  // the output colorspace / flip over every frame's final RGBA
-    hipError_t e = wg::launch_emit(b->d_edesc, b->n, b->k6_maxpx, s);
-    if (e != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
-  }
-  hipEventRecord(t.ev[kStageK5], s);
-  if (b->anim) {  // an animation's canvases from its decoded frames
-    hipError_t e = wg::launch_anim_compose(b->d_fdesc, b->n, b->d_canvases, b->canvas_w, b->canvas_h, s);
-    if (e != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
+    return e == hipSuccess ? WG_STATUS_OK : WG_STATUS_UNSUPPORTED_FEATURE;
+  };
+  for (int i = 0; i < kStages; ++i) {
+    if (i > 0) hipEventRecord(t.ev[i], s);
+    const int st = stage(t.order[i]);
+    if (st != WG_STATUS_OK) return st;
   }
   hipEventRecord(t.ev[kStages], s);
   return batch_mark_done(b, s) == hipSuccess ? WG_STATUS_OK : WG_STATUS_OUT_OF_MEMORY;
@@ -1201,13 +1239,14 @@ int wg_batch_kernel_ms(const wg_batch* bc, float* ms, int n_ms) {
   for (size_t i = 0; i < b->n_runs_pending; ++i) {
     Timing& t = b->timings[i];
     if (hipEventSynchronize(t.ev[kStages]) != hipSuccess) return WG_STATUS_USER_ABORT;
-    for (int k = 0; k < kStages; ++k) {
+    for (int i = 0; i < kStages; ++i) {
+      const int k = t.order[i];
       if (!t.ran[k]) continue;
       float a = 0;
       if (k == kStageK7 && t.forked)
         hipEventElapsedTime(&a, t.side[0], t.side[1]);
       else
-        hipEventElapsedTime(&a, t.ev[k], t.ev[k + 1]);
+        hipEventElapsedTime(&a, t.ev[i], t.ev[i + 1]);
       acc[k] += a;
       cnt[k]++;
     }
@@ -1274,6 +1313,7 @@ int wg_batch_run_emit(wg_batch* b, void* stream) {
   Timing& t = b->timings[b->n_runs_pending++];
   for (bool& r : t.ran) r = false;
   t.forked = false;
+  for (int i = 0; i < kStages; ++i) t.order[i] = (int8_t)i;
   t.ran[kStageK2] = true;
   for (int k = 0; k <= kStageK2; ++k) hipEventRecord(t.ev[k], s);
   hipError_t e = wg::launch_yuv_to_rgba(b->d_desc, nullptr, b->n, b->max_out_w, b->max_out_h,

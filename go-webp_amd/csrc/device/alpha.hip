@@ -26,6 +26,11 @@
 //   3. write the plane (its output window when cropping) into the A bytes (dword
 //      read-modify-write, coalesced).
 // The gradient wavefront is latency-bound (one barrier per column step) and is the slow case.
+//
+// Alpha-first batches (AlphaDesc::to_plane; capi.cpp decides): K4 runs before K1 and leaves the
+// unfiltered plane in `plane` (width-byte rows, the whole plane: no crop window) for the YUV -> RGBA
+// strips to take A from, instead of read-modify-writing the RGBA's A bytes afterwards -- 1 B/px
+// written here and read there instead of 8 B/px.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -160,10 +165,12 @@ __device__ void alpha_rows_direct(const AlphaDesc& F, int part, int parts, uint8
   }
   const bool gvec = F.green && (reinterpret_cast<uintptr_t>(F.green) & 15) == 0 && (W & 3) == 0;
   const bool ovec = ((reinterpret_cast<uintptr_t>(F.rgba) | (uintptr_t)F.rgba_stride) & 15) == 0 && (F.win_x & 3) == 0;
+  const bool pvec = (W & 3) == 0;  // to_plane: the rows' dwords are aligned (the plane is)
   const int xe = F.win_x + F.win_w;  // window columns [win_x, xe)
   for (int yo = part * kWaves + wave; yo < F.win_h; yo += parts * kWaves) {
     const int y = yo + F.win_y;
     uint8_t* orow = F.rgba + (size_t)yo * F.rgba_stride - 4 * (size_t)F.win_x;  // (pixel x at orow + 4x)
+    uint8_t* prow = F.plane + (size_t)y * W;  // (to_plane: the whole plane, window = plane)
     uint32_t carry = horiz && y > 0 ? rowbuf[y - 1] : 0u;
     // (horizontal: every chunk from x = 0, the prefix needs it; none: the window's chunks)
     for (int x0 = horiz ? 0 : (F.win_x & ~255); x0 < xe; x0 += 256) {
@@ -181,7 +188,15 @@ __device__ void alpha_rows_direct(const AlphaDesc& F, int part, int parts, uint8
         carry += (uint32_t)__shfl((int)incl, 63, 64);
       }
       if (x0 + 256 <= F.win_x) continue;
-      if (ovec && x >= F.win_x && x + 3 < xe) {
+      if (F.to_plane) {
+        if (pvec && x + 3 < W) {
+          *reinterpret_cast<uint32_t*>(prow + x) = o;
+        } else {
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if (x + k < W) prow[x + k] = (uint8_t)(o >> (8 * k));
+        }
+      } else if (ovec && x >= F.win_x && x + 3 < xe) {
         uint4* d = reinterpret_cast<uint4*>(orow + 4 * (size_t)x);
         uint4 v = *d;
         v.x = (v.x & 0x00ffffffu) | o << 24;
@@ -327,6 +342,7 @@ __global__ void __launch_bounds__(kThreads) alpha_kernel(const AlphaDesc* __rest
   __syncthreads();
 
   // ---- 3. plane window -> A bytes (the RGBA holds the window: the whole plane unless cropping)
+  if (F.to_plane) return;  // (alpha-first: the strips read the plane)
   for (int y = wave; y < F.win_h; y += kWaves) {
     uint32_t* dst = reinterpret_cast<uint32_t*>(F.rgba + (size_t)y * F.rgba_stride);
     const uint8_t* src = plane + (size_t)(y + F.win_y) * W + F.win_x;

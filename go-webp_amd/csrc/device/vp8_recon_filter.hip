@@ -588,7 +588,10 @@ __device__ __forceinline__ void emit_tail(const FrameDesc& F, uint32_t* progress
       if (lane == 0) atomicOr(err, 1);
       return;
     }
-    strip::convert_strip<kFancy, strip::kAuxSc1, strip::kModesTail>(F, tx, band, lane);  // (RGBA / RGB_565 only)
+    if (__builtin_amdgcn_readfirstlane(F.alpha_off16) != 0)  // (an alpha-first frame: RGBA, A from its plane)
+      strip::convert_strip<kFancy, strip::kAuxSc1, strip::kModesRgba, true>(F, tx, band, lane);
+    else
+      strip::convert_strip<kFancy, strip::kAuxSc1, strip::kModesTail>(F, tx, band, lane);  // (RGBA / RGB_565 only)
   }
 }
 

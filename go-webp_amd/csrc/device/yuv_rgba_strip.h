@@ -299,6 +299,13 @@ __device__ __forceinline__ void store_out(__amdgpu_buffer_rsrc_t o, int em, uint
   }
 }
 
+// Alpha-first frames (FrameDesc::alpha_off16): the 4 pixels' A bytes from the dword of the
+// unfiltered alpha plane (EmitAlphaRGB's A, io_dec.c.go:175-195), one v_perm each.
+__device__ __forceinline__ u32x4 with_alpha(u32x4 px, uint32_t a) {
+  return u32x4{__builtin_amdgcn_perm(a, px.x, 0x04020100u), __builtin_amdgcn_perm(a, px.y, 0x05020100u),
+               __builtin_amdgcn_perm(a, px.z, 0x06020100u), __builtin_amdgcn_perm(a, px.w, 0x07020100u)};
+}
+
 // Strips and bands of a frame: strip tx covers x in [1024 tx, 1024 tx + 1024), band j the
 // row pairs [kPairs j, kPairs j + kPairs) (fancy: pair p = output rows 2p-1, 2p; point:
 // rows 2p, 2p+1).
@@ -308,7 +315,10 @@ __device__ __forceinline__ int n_bands(int H, bool fancy) {
   return (npairs + kPairs - 1) / kPairs;
 }
 
-template <bool kFancy, int kAux, int kModes>
+// kAlpha: an alpha-first frame (FrameDesc::alpha_off16 != 0, RGBA): A from its alpha plane.  A
+// separate instantiation, chosen per frame by the callers, so the strips of frames without alpha
+// keep their code (and K1's tail its I-cache footprint).
+template <bool kFancy, int kAux, int kModes, bool kAlpha = false>
 __device__ __forceinline__ void convert_strip(const FrameDesc& F, int tx, int band, int lane) {
   const int W = F.width, H = F.height;
   const int uv_w = (W + 1) >> 1, uv_h = (H + 1) >> 1;
@@ -346,6 +356,16 @@ __device__ __forceinline__ void convert_strip(const FrameDesc& F, int tx, int ba
 #pragma unroll
     for (int k = 0; k < kGroups; ++k) yw[k] = __builtin_amdgcn_raw_buffer_load_b32(yd, off + 256 * k, 0, 0);
   };
+  // kAlpha: the alpha plane's dwords of a row (W-byte rows).  The range check drops a whole dword
+  // that crosses the end, so the range runs 3 bytes past the plane (inside its 256-byte-aligned
+  // allocation): the last row's last group keeps its valid bytes.
+  constexpr bool ha = kAlpha;
+  const __amdgpu_buffer_rsrc_t ad = plane_rsrc(F.y + 16 * (ptrdiff_t)(kAlpha ? F.alpha_off16 : 0), W * H + 3);
+  auto load_alpha = [&](int row, uint32_t aw[kGroups]) {
+    const uint32_t off = row >= 0 && row < H ? (uint32_t)(xl + row * W) : kOffDrop;
+#pragma unroll
+    for (int k = 0; k < kGroups; ++k) aw[k] = __builtin_amdgcn_raw_buffer_load_b32(ad, off + 256 * k, 0, 0);
+  };
 
   if (kFancy) {
     const int npairs = (H >> 1) + 1;  // pair p: output rows 2p-1, 2p
@@ -363,9 +383,13 @@ __device__ __forceinline__ void convert_strip(const FrameDesc& F, int tx, int ba
     auto pair_step = [&](int p, const ChromaCols& prv) __attribute__((always_inline)) {
       const int ya = 2 * p - 1, yb = 2 * p;
       asm volatile("" : "+s"(em));  // (no loop copy per output mode: only the conversion switches)
-      uint32_t yA[kGroups], yB[kGroups];
+      uint32_t yA[kGroups], yB[kGroups], aA[kGroups] = {}, aB[kGroups] = {};
       load_luma(ya, yA);
       load_luma(yb, yB);
+      if (ha) {
+        load_alpha(ya, aA);
+        load_alpha(yb, aB);
+      }
       const int rn = min(p + 1, uv_h - 1);  // chroma row for the next pair
       const ChromaRaw raw_next = load_chroma(ud, vd, U, V, rn, uvs, cb0, uv_w, lane, p + 1 < p1);
       const ChromaCols cur = make_cols(raw_cur, cb0, uv_w, lane);
@@ -373,8 +397,16 @@ __device__ __forceinline__ void convert_strip(const FrameDesc& F, int tx, int ba
       for (int k = 0; k < kGroups; ++k) {
         const int x = xl + 256 * k;
         if (!live(k)) continue;
-        if (ya >= 0) store_out<kAux, kModes>(out, em, roff(ya), x, convert_group(prv, cur, k, yA[k]), W - x, full(k));
-        if (yb < H) store_out<kAux, kModes>(out, em, roff(yb), x, convert_group(cur, prv, k, yB[k]), W - x, full(k));
+        if (ya >= 0) {
+          u32x4 px = convert_group(prv, cur, k, yA[k]);
+          if (ha) px = with_alpha(px, aA[k]);
+          store_out<kAux, kModes>(out, em, roff(ya), x, px, W - x, full(k));
+        }
+        if (yb < H) {
+          u32x4 px = convert_group(cur, prv, k, yB[k]);
+          if (ha) px = with_alpha(px, aB[k]);
+          store_out<kAux, kModes>(out, em, roff(yb), x, px, W - x, full(k));
+        }
       }
       raw_cur = raw_next;
       // K1's tail yields the SIMD for a moment after each pair: its denser packed code otherwise
@@ -392,9 +424,13 @@ __device__ __forceinline__ void convert_strip(const FrameDesc& F, int tx, int ba
     const int p1 = min(p0 + kPairs, npairs);
     for (int p = p0; p < p1; ++p) {
       asm volatile("" : "+s"(em));
-      uint32_t yA[kGroups], yB[kGroups];
+      uint32_t yA[kGroups], yB[kGroups], aA[kGroups] = {}, aB[kGroups] = {};
       load_luma(2 * p, yA);
       load_luma(2 * p + 1, yB);
+      if (ha) {
+        load_alpha(2 * p, aA);
+        load_alpha(2 * p + 1, aB);
+      }
       const ChromaRaw c = load_chroma(ud, vd, U, V, p, uvs, cb0, uv_w, lane, true);
 #pragma unroll
       for (int k = 0; k < kGroups; ++k) {
@@ -409,7 +445,8 @@ __device__ __forceinline__ void convert_strip(const FrameDesc& F, int tx, int ba
           if (yr >= H) break;
           const uint32_t yw = r ? yB[k] : yA[k];
           const uint2 a = yuv_to_rgba2(luma_lanes(yw, 0, 1), u0, v0), b = yuv_to_rgba2(luma_lanes(yw, 2, 3), u1, v1);
-          const u32x4 px{a.x, a.y, b.x, b.y};
+          u32x4 px{a.x, a.y, b.x, b.y};
+          if (ha) px = with_alpha(px, r ? aB[k] : aA[k]);
           store_out<kAux, kModes>(out, em, roff(yr), x, px, W - x, full(k));
         }
       }

@@ -26,7 +26,10 @@ __global__ void __launch_bounds__(64 * kWavesPerWG) yuv_to_rgba_kernel(const Fra
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int sx = strip::strips_x(F.width);
   const int tx = blockIdx.x % sx, ty = blockIdx.x / sx;
-  strip::convert_strip<kFancy, strip::kAuxNt, kModes>(F, tx, ty * kWavesPerWG + wave, lane);
+  if (__builtin_amdgcn_readfirstlane(F.alpha_off16) != 0)  // (an alpha-first frame: RGBA, A from its plane)
+    strip::convert_strip<kFancy, strip::kAuxNt, strip::kModesRgba, true>(F, tx, ty * kWavesPerWG + wave, lane);
+  else
+    strip::convert_strip<kFancy, strip::kAuxNt, kModes>(F, tx, ty * kWavesPerWG + wave, lane);
 }
 
 }  // namespace

@@ -71,7 +71,10 @@ struct FrameDesc {
                   // (kFrameGlobalCols) and by the split kernel, which runs every frame from it
   int32_t width, height, mb_w, mb_h;
   int32_t y_stride, uv_stride, rgba_stride, filter_type;
-  int32_t flags, valid, blocks_bytes, pad2;  // blocks_bytes: size of `blocks` (K1 bounds)
+  int32_t flags, valid, blocks_bytes;  // blocks_bytes: size of `blocks` (K1 bounds)
+  // alpha-first batches (K4 before K1): the frame's unfiltered alpha plane (width-byte rows) at
+  // y + 16 * alpha_off16, which the YUV -> RGBA strips take A from; 0: none (A = 255)
+  int32_t alpha_off16;
   uint32_t* gprog;  // split kernel: one progress flag per part boundary, 128 B apart (kGProgBytes)
   // K1's tail / K2 output: 0 RGBA at `rgba`; else 1 + the WEBP_CSP_MODE written straight into
   // `rgba` (the frame's output slot, rgba_stride = bpp * width), rows bottom-up if emit_flip
@@ -128,7 +131,8 @@ struct AlphaDesc {
   uint8_t* rgba;         // the frame's RGBA output; K4 writes its A bytes
   int32_t width, height, rgba_stride, filter;  // plane size; filter: 0 none, 1 horizontal, 2 vertical, 3 gradient
   int32_t valid, win_x, win_y, win_w;           // the output window of the plane (cropping)
-  int32_t win_h, cbits, coded_width, pad0;
+  int32_t win_h, cbits, coded_width;
+  int32_t to_plane;  // alpha-first: the unfiltered bytes into `plane` (width-byte rows), not the A bytes
   // a lossless alpha stream whose only transform is color indexing (or that has none), filter
   // none / horizontal: K7's coded image read directly (K3 skipped) -- green of pal[index of
   // pixel x in coded[x >> cbits]], or of the coded pixel itself when pal is null

@@ -213,7 +213,8 @@ int wg_batch_set_k1_parts(wg_batch* b, int parts);
 
 /* The YUV420->RGBA stage alone (K2: EmitFancyRGB / EmitSampledRGB, io_dec.c.go:53-115) over the batch's
  * reconstructed planes (after a wg_batch_run): the stage-roofline measurement of the
- * metric.  Its duration is reported as ms[1] by wg_batch_kernel_ms(). */
+ * metric.  Its duration is reported as ms[1] by wg_batch_kernel_ms().  (Frames with alpha take A
+ * from the planes the run's K4 left when the batch runs alpha-first, else A = 255.) */
 int wg_batch_run_emit(wg_batch* b, void* stream);
 
 /* Per-launch kernel durations averaged over the runs since the last query:
