@@ -237,7 +237,8 @@ struct wg_batch {
   wg_decoder_options opt{};          // output colorspace, cropping, flip (f4)
   bool any_crop = false;             // K2 reads compact cropped planes through desc2
   bool fused = false;                // lossy RGBA emitted by K1's tail (wg::kFrameEmitRgba), no K2 launch
-  bool alpha_first = false;          // K4 before K1: the strips take A from K4's planes (batch_upload)
+  bool alpha_first = false;          // K4 before the strips, which take A from its planes (set_alpha_first)
+  double alpha_px = 0;               // pixels of the alpha planes (algorithmic bytes)
   std::vector<FrameDesc> desc2;
   FrameDesc* d_desc2 = nullptr;
   int max_out_w = 1, max_out_h = 1;
@@ -773,6 +774,7 @@ void batch_layout(wg_batch* b, wg::StagingArena& arena, int32_t* status) {
       f.off_aplane = pl_b;
       pl_b = align_up(pl_b + (size_t)f.width * f.height);
       k4 += 8.0 * px;
+      b->alpha_px += px;
     }
   }
   // K6 batches: one output window per frame in d_out; K6 reads the RGBA window of the frames not
@@ -857,6 +859,35 @@ bool k7_side_fits(const wg_batch* b) {
   const int head = b->split_parts >= 2 ? b->split_from : b->n;
   const int k1_wgs = head + (b->split_parts >= 2 ? (b->n - head + 7) / 8 * 8 * b->split_parts : 0);
   return !off && b->n_lossy > 0 && b->n_k3 > 0 && k1_wgs + (int)b->tokdesc.size() <= kCUs;
+}
+
+// Alpha-first: K7 -> K3 -> K4 before the YUV -> RGBA strips, K4 leaving each alpha plane
+// unfiltered in its scratch plane and the strips (K1's tail or K2) taking A from it -- instead of
+// K4 read-modify-writing the RGBA's A bytes afterwards (8 B/px -> 1 B/px written + 1 B/px read).
+// Not with crop windows (K4 would need the window's plane), nor where K7 runs beside K1 and K1's
+// tail converts (the overlap is worth more); without the tail only K2 waits for K4, so the split
+// kernel's batches keep K7 beside K1 and run alpha-first too.  Decided for the batch's current K1
+// configuration (upload, wg_batch_set_emit, wg_batch_set_k1_parts) into the host descriptors;
+// returns whether the choice changed (the caller copies desc / adesc to the device).
+// WG_ALPHA_FIRST=0 disables it (measurement).
+bool set_alpha_first(wg_batch* b) {
+  static const bool off = [] {
+    const char* e = getenv("WG_ALPHA_FIRST");
+    return e && atoi(e) == 0;
+  }();
+  const bool af = b->n_alpha > 0 && !b->any_crop && !off && (!b->fused || !k7_side_fits(b));
+  const bool changed = af != b->alpha_first;
+  b->alpha_first = af;
+  size_t j = 0;
+  for (int i = 0; i < b->n; ++i) {
+    const FrameParse& f = b->fp[(size_t)i];
+    if (f.status != WG_STATUS_OK || f.lossless || !f.alpha) continue;
+    AlphaDesc& a = b->adesc[j++];
+    a.plane = af || !f.alpha_direct ? b->d_planes + f.off_aplane : nullptr;
+    a.to_plane = af ? 1 : 0;
+    b->desc[(size_t)i].alpha_off16 = af ? (int32_t)((f.off_aplane - f.off_y) / 16) : 0;
+  }
+  return changed;
 }
 
 // Tags of the split kernel's progress flags: a fresh value per launch, never 0 (the flags are
@@ -983,31 +1014,7 @@ int batch_upload(wg_batch* b, const wg::StagingArena& arena) {
   if (b->fused)
     for (int i = 0; i < n; ++i)
       if (b->desc[(size_t)i].valid) b->desc[(size_t)i].flags |= wg::kFrameEmitRgba;
-  // Alpha-first: K7 -> K3 -> K4 before K1, K4 leaving each alpha plane unfiltered in its scratch
-  // plane and the YUV -> RGBA strips (K1's tail or K2) taking A from it -- instead of K4
-  // read-modify-writing the RGBA's A bytes afterwards (8 B/px -> 1 B/px written + 1 B/px read).
-  // Not with crop windows (K4 would need the window's plane), nor where K7 runs beside K1 (small
-  // batches: there the overlap is worth more).  WG_ALPHA_FIRST=0 disables it (measurement).
-  static const bool alpha_first_off = [] {
-    const char* e = getenv("WG_ALPHA_FIRST");
-    return e && atoi(e) == 0;
-  }();
-  b->alpha_first = b->n_alpha > 0 && !b->any_crop && !alpha_first_off && !k7_side_fits(b);
-  if (b->alpha_first) {
-    size_t j = 0;
-    for (int i = 0; i < n; ++i) {
-      const FrameParse& f = b->fp[(size_t)i];
-      if (f.status != WG_STATUS_OK || f.lossless || !f.alpha) continue;
-      AlphaDesc& a = b->adesc[j++];
-      a.plane = b->d_planes + f.off_aplane;
-      a.to_plane = 1;
-      b->desc[(size_t)i].alpha_off16 = (int32_t)((f.off_aplane - f.off_y) / 16);
-      const double px = (double)f.width * f.height;
-      b->kbytes[3] -= 7.0 * px;  // (K4: 1 B/px written instead of the 8 B/px read-modify-write)
-      b->k1_fused_bytes += px;   // (the strips read it: K1's tail, or K2)
-      b->kbytes[1] += px;
-    }
-  }
+  set_alpha_first(b);
   if (b->any_crop) {  // K2's view: cropped lossy frames read their compact planes
     b->desc2 = b->desc;
     for (int i = 0; i < n; ++i) {
@@ -1109,10 +1116,10 @@ wg_batch* batch_create(wg_ctx* ctx, const uint8_t* const* data, const size_t* si
 extern "C" {
 
 namespace {
-// The context's side stream for K7 (k7_side_fits; not in alpha-first batches, whose K1 waits for
-// K4 and so for K7), else null.  Created on first use.
+// The context's side stream for K7 (k7_side_fits; not when K1's tail converts alpha-first frames:
+// it waits for K4 and so for K7), else null.  Created on first use.
 hipStream_t k7_side_stream(wg_batch* b) {
-  if (b->alpha_first || !k7_side_fits(b)) return nullptr;
+  if ((b->alpha_first && b->fused) || !k7_side_fits(b)) return nullptr;
   wg_ctx* c = b->ctx;
   std::lock_guard<std::mutex> lock(c->side_mu);
   if (!c->side && hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess) c->side = nullptr;
@@ -1144,10 +1151,14 @@ int wg_batch_run(wg_batch* b, void* stream) {
   t.ran[kStageK6] = b->k6 && b->n_k6 > 0;
   t.ran[kStageK5] = b->anim;
   // launch order (ev[i] .. ev[i + 1] bracket stage order[i]): K1 / K2 first, or, alpha-first,
-  // the alpha planes (K7 -> K3 -> K4) before the strips that take A from them
+  // the alpha planes (K7 -> K3 -> K4) before the strips that take A from them: before K1 when its
+  // tail converts, else before K2 alone
   static constexpr int8_t kOrderAlphaFirst[kStages] = {kStageK7, kStageK3, kStageK4, kStageK1,
                                                        kStageK2, kStageK6, kStageK5};
-  for (int i = 0; i < kStages; ++i) t.order[i] = b->alpha_first ? kOrderAlphaFirst[i] : (int8_t)i;
+  static constexpr int8_t kOrderAlphaK2[kStages] = {kStageK1, kStageK7, kStageK3, kStageK4,
+                                                    kStageK2, kStageK6, kStageK5};
+  for (int i = 0; i < kStages; ++i)
+    t.order[i] = !b->alpha_first ? (int8_t)i : b->fused ? kOrderAlphaFirst[i] : kOrderAlphaK2[i];
   hipEventRecord(t.ev[0], s);
   // K7 only feeds K3 / K4: when its grid fits on the chip beside K1's, it runs on the context's
   // side stream, concurrently with K1 and K2, and K3 waits for it
@@ -1265,22 +1276,39 @@ int wg_batch_kernel_bytes(const wg_batch* b, double* bytes, int n_bytes) {
   if (!b || !bytes || n_bytes < 1) return WG_STATUS_INVALID_PARAM;
   for (int k = 0; k < n_bytes; ++k) bytes[k] = k < kStages ? b->kbytes[k] : 0.0;
   if (b->fused) bytes[0] = b->k1_fused_bytes;
+  if (b->alpha_first) {  // K4 writes 1 B/px instead of the 8 B/px read-modify-write; the strips read it
+    if (n_bytes > 3) bytes[3] -= 7.0 * b->alpha_px;
+    if (b->fused) bytes[0] += b->alpha_px;
+    if (n_bytes > 1) bytes[1] += b->alpha_px;
+  }
   return WG_STATUS_OK;
 }
+
+namespace {
+// The frame and alpha descriptors to the device again (after a change of the K1 configuration).
+int batch_upload_desc(wg_batch* b) {
+  if (!set_device(b->ctx->device)) return WG_STATUS_INVALID_PARAM;
+  hipError_t e = hipMemcpyAsync(b->d_desc, b->desc.data(), sizeof(FrameDesc) * (size_t)b->n, hipMemcpyHostToDevice,
+                                b->home);
+  if (e == hipSuccess && !b->adesc.empty())
+    e = hipMemcpyAsync(b->d_adesc, b->adesc.data(), sizeof(AlphaDesc) * b->adesc.size(), hipMemcpyHostToDevice, b->home);
+  if (e == hipSuccess) e = hipStreamSynchronize(b->home);
+  return e == hipSuccess ? WG_STATUS_OK : WG_STATUS_USER_ABORT;
+}
+// Alpha-first for the current K1 configuration; the descriptors uploaded if the choice changed.
+int batch_set_alpha_first(wg_batch* b) { return set_alpha_first(b) ? batch_upload_desc(b) : WG_STATUS_OK; }
+}  // namespace
 
 int wg_batch_set_emit(wg_batch* b, int separate) {
   if (!b) return WG_STATUS_INVALID_PARAM;
   if (!separate && (b->any_crop || b->no_tail)) return WG_STATUS_INVALID_PARAM;  // crop windows / modes K2 emits
   if (!separate) b->split_parts = 1, b->split_from = 0;  // K1's RGBA tail: the one-workgroup kernels
-  if (b->fused == !separate) return WG_STATUS_OK;
+  if (b->fused == !separate) return batch_set_alpha_first(b);
   b->fused = !separate;
   for (FrameDesc& d : b->desc)
     if (d.valid) d.flags = b->fused ? (d.flags | wg::kFrameEmitRgba) : (d.flags & ~wg::kFrameEmitRgba);
-  if (!set_device(b->ctx->device)) return WG_STATUS_INVALID_PARAM;
-  hipError_t e = hipMemcpyAsync(b->d_desc, b->desc.data(), sizeof(FrameDesc) * (size_t)b->n, hipMemcpyHostToDevice,
-                                b->home);
-  if (e == hipSuccess) e = hipStreamSynchronize(b->home);
-  return e == hipSuccess ? WG_STATUS_OK : WG_STATUS_USER_ABORT;
+  set_alpha_first(b);
+  return batch_upload_desc(b);
 }
 
 int wg_batch_set_k1_parts(wg_batch* b, int parts) {
@@ -1294,7 +1322,7 @@ int wg_batch_set_k1_parts(wg_batch* b, int parts) {
   if (p >= 2 && from > 0 && b->any_crop) return WG_STATUS_OK;  // (cropped: whole rounds only)
   b->split_parts = p;
   b->split_from = p >= 2 ? from : 0;
-  return WG_STATUS_OK;
+  return batch_set_alpha_first(b);
 }
 
 int wg_batch_run_emit(wg_batch* b, void* stream) {

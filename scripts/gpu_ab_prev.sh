@@ -1,7 +1,7 @@
 #!/bin/bash
 # Same-call A/B of the committed library (variant "prev", scripts/build_prev_lib.sh) against the
 # working tree: the GPU tests in $TESTS (default and, with NOSIDE=1, again with K7 kept in stream
-# order), then $REPS alternating bench runs of each workload in $WLS.
+# order), then $REPS alternating bench runs of each workload in $WLS (name or name:batch).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/${TAG:-abprev}
 mkdir -p $OUT
@@ -19,7 +19,8 @@ for rep in $(seq 1 ${REPS:-2}); do
   for v in prev new; do
     for w in ${WLS:-c3a}; do
       lib=$v; [ $v = new ] && lib=""
-      WG_LIB_VARIANT=$lib timeout -k 10 300 python bench.py --workload $w --steps 10 --warmup 3 --no-cpu-baseline --no-e2e \
+      wl=${w%%:*}; bt=256; [ "$wl" != "$w" ] && bt=${w#*:}  # (workload:batch)
+      WG_LIB_VARIANT=$lib timeout -k 10 300 python bench.py --workload $wl --batch $bt --steps 10 --warmup 3 --no-cpu-baseline --no-e2e \
         > $OUT/ab_${w}_${v}_$rep.log 2>&1 || { tail $OUT/ab_${w}_${v}_$rep.log; exit 1; }
       python -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); print(sys.argv[2], sys.argv[3], d['value'], d['ms_per_step'], {k: round(x, 3) for k, x in d['kernel_ms'].items()})" \
         $OUT/ab_${w}_${v}_$rep.log $v $w
