@@ -46,15 +46,20 @@ constexpr int kThreads = 1024;
 constexpr int kWaves = kThreads / 64;
 constexpr int kMaxDim = 16384;
 
+// Inclusive scan over the wave in DPP moves (no LDS traffic): row_shr 1 / 2 / 4 / 8 within each
+// 16-lane row (lanes without a source add 0, the `old` operand), then row_bcast:15 adds row r's
+// total to row r + 1 (rows 1, 3) and row_bcast:31 lane 31's to rows 2 and 3.
 __device__ __forceinline__ int wave_incl_scan(int v) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const int u = __shfl_up(v, d, 64);
-    if (lane >= d) v += u;
-  }
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);  // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);  // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);  // row_bcast:31
   return v;
 }
+
+__device__ __forceinline__ int lane63(int v) { return __builtin_amdgcn_readlane(v, 63); }
 
 // Exclusive scan of one int per thread over the block; `tot` gets the block total.
 __device__ __forceinline__ int block_excl_scan(int v, int* wsum, int* tot) {
@@ -82,7 +87,7 @@ __device__ __forceinline__ void scan_row(uint8_t* row, int W, uint32_t pred) {
     const int v = x < W ? row[x] : 0;
     const int inc = wave_incl_scan(v);
     if (x < W) row[x] = (uint8_t)(carry + (uint32_t)inc);
-    carry += (uint32_t)__shfl(inc, 63, 64);
+    carry += (uint32_t)lane63(inc);
   }
 }
 
@@ -185,7 +190,7 @@ __device__ void alpha_rows_direct(const AlphaDesc& F, int part, int parts, uint8
         const uint32_t incl = (uint32_t)wave_incl_scan((int)(b3 & 0xff));
         const uint32_t base = carry + incl - (b3 & 0xff);
         o = ((base + b0) & 0xff) | ((base + b1) & 0xff) << 8 | ((base + b2) & 0xff) << 16 | (base + b3) << 24;
-        carry += (uint32_t)__shfl((int)incl, 63, 64);
+        carry += (uint32_t)lane63((int)incl);
       }
       if (x0 + 256 <= F.win_x) continue;
       if (F.to_plane) {
