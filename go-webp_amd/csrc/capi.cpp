@@ -239,6 +239,7 @@ struct wg_batch {
   bool fused = false;                // lossy RGBA emitted by K1's tail (wg::kFrameEmitRgba), no K2 launch
   bool alpha_first = false;          // K4 before the strips, which take A from its planes (set_alpha_first)
   double alpha_px = 0;               // pixels of the alpha planes (algorithmic bytes)
+  bool no_side = false;              // K7 always in stream order (the pipelined decode's chunks)
   std::vector<FrameDesc> desc2;
   FrameDesc* d_desc2 = nullptr;
   int max_out_w = 1, max_out_h = 1;
@@ -849,7 +850,9 @@ int split_k1_parts(const wg_batch* b, int* from = nullptr) {
 
 // K7 can run beside K1 / K2 (wg_batch_run) when their grids fit on the chip together: one
 // workgroup per CU each -- K1's one-workgroup or split kernel, one K7 workgroup per stream.
-// WG_K7_SIDE=0 keeps K7 in stream order.
+// WG_K7_SIDE=0 keeps K7 in stream order, and so does the pipelined decode (its chunks already
+// overlap on two work streams; a side stream shared by them measured 7.45-7.59k -> 5.27-5.44k
+// MPix/s on c3a end to end, its K7s holding up the uploads and downloads).
 bool k7_side_fits(const wg_batch* b) {
   static const bool off = [] {
     const char* e = getenv("WG_K7_SIDE");
@@ -858,7 +861,7 @@ bool k7_side_fits(const wg_batch* b) {
   constexpr int kCUs = 256;
   const int head = b->split_parts >= 2 ? b->split_from : b->n;
   const int k1_wgs = head + (b->split_parts >= 2 ? (b->n - head + 7) / 8 * 8 * b->split_parts : 0);
-  return !off && b->n_lossy > 0 && b->n_k3 > 0 && k1_wgs + (int)b->tokdesc.size() <= kCUs;
+  return !off && !b->no_side && b->n_lossy > 0 && b->n_k3 > 0 && k1_wgs + (int)b->tokdesc.size() <= kCUs;
 }
 
 // Alpha-first: K7 -> K3 -> K4 before the YUV -> RGBA strips, K4 leaving each alpha plane
@@ -1590,6 +1593,7 @@ int decode_pipelined(wg_ctx* ctx, const uint8_t* const* data, const size_t* size
   std::vector<int> chunk_of((size_t)n);
   for (int k = 0; k < K; ++k) {
     ch[(size_t)k].b = batch_init(ctx, ctx->stream, ch[(size_t)k].n, &o);  // home: the upload stream
+    if (ch[(size_t)k].b) ch[(size_t)k].b->no_side = true;
     for (int j = 0; j < ch[(size_t)k].n; ++j) chunk_of[(size_t)(ch[(size_t)k].a + j)] = k;
   }
   std::mutex qmu;
