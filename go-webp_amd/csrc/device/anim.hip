@@ -12,7 +12,8 @@
 //
 // The canvas recurrence is per pixel, so the kernel is data-parallel over the canvas: each
 // thread owns four horizontally adjacent pixels (one 16-byte store per frame) and walks the
-// frames in order with the current and the disposed value in registers.  The per-frame
+// frames in order with the current and the disposed value in registers, loading four frames'
+// pixels ahead.  The per-frame
 // descriptors are wave-uniform.  Bytes per frame: the canvas write (4 B/px) + the frame's
 // rectangle read -- HBM-bound.
 #include <hip/hip_runtime.h>
@@ -60,29 +61,49 @@ __global__ void __launch_bounds__(kThreads) anim_compose_kernel(const AnimFrameD
   const int npx = min(4, cw - cx0);
   const size_t canvas_bytes = (size_t)cw * ch * 4;
   uint32_t cur[4], disp[4] = {0, 0, 0, 0};
-  for (int f = 0; f < n_frames; ++f) {
-    const AnimFrameDesc& F = frames[f];
-    const bool row_in = cy >= F.y && cy < F.y + F.height;
-    const bool prow_in = cy >= F.py && cy < F.py + F.ph;
+  // the frames' pixels kAhead frames at a time: all their loads issued before the first is used
+  // (the recurrence is serial in f, its loads are not: one frame at a time left each wave waiting
+  // out a load per frame)
+  constexpr int kAhead = 4;
+  for (int f0 = 0; f0 < n_frames; f0 += kAhead) {
+    uint32_t src[kAhead][4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int cx = cx0 + k;
-      uint32_t c = F.key ? 0u : disp[k];
-      const bool in = row_in && cx >= F.x && cx < F.x + F.width && k < npx;
-      if (in) {
-        const uint32_t src = *reinterpret_cast<const uint32_t*>(
-            F.rgba + ((size_t)(cy - F.y) * F.width + (cx - F.x)) * 4);
-        const bool in_prev = prow_in && cx >= F.px && cx < F.px + F.pw;
-        c = (F.blend && !(F.prev_dispose_bg && in_prev)) ? blend_px(src, disp[k], scale_tab) : src;
+    for (int j = 0; j < kAhead; ++j) {
+      const int f = min(f0 + j, n_frames - 1);
+      const AnimFrameDesc& F = frames[f];
+      const bool row_in = cy >= F.y && cy < F.y + F.height;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int cx = cx0 + k;
+        const bool in = row_in && cx >= F.x && cx < F.x + F.width && k < npx;
+        src[j][k] = in ? *reinterpret_cast<const uint32_t*>(F.rgba + ((size_t)(cy - F.y) * F.width + (cx - F.x)) * 4) : 0u;
       }
-      cur[k] = c;
-      disp[k] = (F.dispose_bg && in) ? 0u : c;
     }
-    uint8_t* out = canvases + (size_t)f * canvas_bytes + ((size_t)cy * cw + cx0) * 4;
-    if (npx == 4 && (cw & 3) == 0) {
-      *reinterpret_cast<uint4*>(out) = make_uint4(cur[0], cur[1], cur[2], cur[3]);
-    } else {
-      for (int k = 0; k < npx; ++k) reinterpret_cast<uint32_t*>(out)[k] = cur[k];
+#pragma unroll
+    for (int j = 0; j < kAhead; ++j) {
+      const int f = f0 + j;
+      if (f >= n_frames) break;
+      const AnimFrameDesc& F = frames[f];
+      const bool row_in = cy >= F.y && cy < F.y + F.height;
+      const bool prow_in = cy >= F.py && cy < F.py + F.ph;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int cx = cx0 + k;
+        uint32_t c = F.key ? 0u : disp[k];
+        const bool in = row_in && cx >= F.x && cx < F.x + F.width && k < npx;
+        if (in) {
+          const bool in_prev = prow_in && cx >= F.px && cx < F.px + F.pw;
+          c = (F.blend && !(F.prev_dispose_bg && in_prev)) ? blend_px(src[j][k], disp[k], scale_tab) : src[j][k];
+        }
+        cur[k] = c;
+        disp[k] = (F.dispose_bg && in) ? 0u : c;
+      }
+      uint8_t* out = canvases + (size_t)f * canvas_bytes + ((size_t)cy * cw + cx0) * 4;
+      if (npx == 4 && (cw & 3) == 0) {
+        *reinterpret_cast<uint4*>(out) = make_uint4(cur[0], cur[1], cur[2], cur[3]);
+      } else {
+        for (int k = 0; k < npx; ++k) reinterpret_cast<uint32_t*>(out)[k] = cur[k];
+      }
     }
   }
 }
