@@ -76,6 +76,38 @@ def test_mixed_alpha_lossy_lossless_batch_and_timing(ctx, k1):
     b.close()
 
 
+@pytest.mark.parametrize("n", [5, 260])
+def test_alpha_first_follows_k1_configuration(ctx, n):
+    """Alpha-first batches (K4 before the YUV -> RGBA strips, which take A from its planes; capi.cpp
+    set_alpha_first) are re-decided whenever the K1 configuration changes: the automatic choice (a
+    small batch: the split K1 with K7 on the side stream and K4 -> K2; 260 frames: alpha-first with
+    K1's tail), then K1's RGBA tail (set_emit(False): with K7 beside K1 no longer alpha-first), K2
+    (set_emit(True)), forced split parts and back -- every frame equal to libwebp 1.6.0 after each
+    run, the descriptors re-uploaded on every switch."""
+    names = ["a_ll_h_130x70", "a_raw_h_71x33", "a_raw_g_64x64", "a_ll_v_97x81", "a_raw_g_40x1030"]
+    datas = [load_alpha(x)[0] for x in names]
+    golds = [load_alpha(x)[1]["rgba"] for x in names]
+    idx = [i % len(names) for i in range(n)]
+    b = ctx.batch([datas[i] for i in idx])
+    try:
+        assert (b.status == 0).all()
+        steps = [("auto", None), ("tail", lambda: b.set_emit(False)), ("k2", lambda: b.set_emit(True))]
+        if n < 256:  # (the split kernel is for batches of fewer frames than CUs)
+            steps.append(("split3", lambda: b.set_k1_parts(3)))
+        steps += [("one", lambda: b.set_k1_parts(1)), ("tail2", lambda: b.set_emit(False)),
+                  ("auto2", lambda: b.set_k1_parts(0))]
+        for name, act in steps:
+            if act is not None:
+                act()
+            b.run()
+            ms = b.kernel_ms()
+            assert ms[0] > 0 and ms[3] > 0, (name, ms)
+            for i in sorted({0, 1, 2, 3, 4, n - 1}):
+                np.testing.assert_array_equal(b.rgba(i), golds[idx[i]], err_msg=f"{name} frame {i}")
+    finally:
+        b.close()
+
+
 def test_alpha_single_decode_dropin():
     data, gold = load_alpha("a_ll_q50_80x80")
     np.testing.assert_array_equal(webp_amd.decode(data), gold["rgba"])
