@@ -74,7 +74,11 @@ __device__ __forceinline__ uint32_t sat_x4(u16x2 a) {
 // no add: two wrapping v_pk_mad_u16 on the biased lane, (133 yl + 4864) mod 2^16 = 133 y + 1024
 // (so t4 = ((133 y) >> 8) + 4) and 74 yl mod 2^16 = 74 y + 8704.  y1g + MultHi(v, 26149) and
 // y1g + MultHi(u, 33050) stay below 2^16 (tests/test_oracle.py::test_packed_yuv_formulas).
-__device__ __forceinline__ uint2 yuv_to_rgba2(u16x2 yl, u16x2 u, u16x2 v) {
+//
+// kAlpha (alpha-first frames): A from `a` instead of 0xff -- the B bytes and the two pixels' A bytes
+// (`asel`: a's bytes 0, 1 or 2, 3) packed into one dword first, so the pixels stay one v_perm each.
+template <bool kAlpha = false>
+__device__ __forceinline__ uint2 yuv_to_rgba2(u16x2 yl, u16x2 u, u16x2 v, uint32_t a = 0, uint32_t asel = 0) {
   const u16x2 y1g = yl * splat(74) + ((yl * splat(133) + splat(4864)) >> 8);  // MultHi(y, 19077) + 8708
   const uint32_t r = sat_x4(sat_sub(y1g + v * splat(102) + ((v * splat(37)) >> 8), 14234 + 8708));  // + MultHi(v, 26149)
   const u16x2 gu = u * splat(25) + ((u * splat(19)) >> 8);                                 // MultHi(u, 6419)
@@ -84,8 +88,14 @@ __device__ __forceinline__ uint2 yuv_to_rgba2(u16x2 yl, u16x2 u, u16x2 v) {
   // the channel values are the high bytes of the 16-bit lanes: t = R0 G0 R1 G1; px = R G B 0xff
   // (perm selector 0x0d = 0xff)
   const uint32_t t = __builtin_amdgcn_perm(g, r, 0x07030501u);
+  if constexpr (kAlpha) {
+    const uint32_t ba = __builtin_amdgcn_perm(a, b, asel);  // B0 A0 B1 A1
+    return make_uint2(__builtin_amdgcn_perm(ba, t, 0x05040100u), __builtin_amdgcn_perm(ba, t, 0x07060302u));
+  }
   return make_uint2(__builtin_amdgcn_perm(b, t, 0x0d050100u), __builtin_amdgcn_perm(b, t, 0x0d070302u));
 }
+// yuv_to_rgba2's asel for pixels 0, 1 and 2, 3 of a group's alpha dword
+constexpr uint32_t kASel01 = 0x05030401u, kASel23 = 0x07030601u;
 
 // bytes i and j of w as the two 16-bit halves
 __device__ __forceinline__ u16x2 bytes2(uint32_t w, int i, int j) {
@@ -210,12 +220,15 @@ __device__ __forceinline__ void upsample4(u16x2 n02, u16x2 n13, u16x2 f02, u16x2
   p23 = as_u16x2(h23) >> 4;  // (3a2 + a1 + 8, 3a2 + a3 + 8) >> 4
 }
 
-// group k of a row: n = the near row's taps, f = the far row's
-__device__ __forceinline__ u32x4 convert_group(const ChromaCols& n, const ChromaCols& f, int k, uint32_t yw) {
+// group k of a row: n = the near row's taps, f = the far row's; kAlpha: A from the dword aw
+template <bool kAlpha = false>
+__device__ __forceinline__ u32x4 convert_group(const ChromaCols& n, const ChromaCols& f, int k, uint32_t yw,
+                                               uint32_t aw = 0) {
   u16x2 u01, u23, v01, v23;
   upsample4(n.u02[k], n.u13[k], f.u02f[k], f.u13f[k], u01, u23);
   upsample4(n.v02[k], n.v13[k], f.v02f[k], f.v13f[k], v01, v23);
-  const uint2 a = yuv_to_rgba2(luma_lanes(yw, 0, 1), u01, v01), b = yuv_to_rgba2(luma_lanes(yw, 2, 3), u23, v23);
+  const uint2 a = yuv_to_rgba2<kAlpha>(luma_lanes(yw, 0, 1), u01, v01, aw, kASel01),
+              b = yuv_to_rgba2<kAlpha>(luma_lanes(yw, 2, 3), u23, v23, aw, kASel23);
   return u32x4{a.x, a.y, b.x, b.y};
 }
 
@@ -297,13 +310,6 @@ __device__ __forceinline__ void store_out(__amdgpu_buffer_rsrc_t o, int em, uint
     __builtin_amdgcn_raw_buffer_store_b16((unsigned short)ov[k], o, a, 0, 0);
     if (bpp == 3) __builtin_amdgcn_raw_buffer_store_b8((unsigned char)(ov[k] >> 16), o, nvalid > k ? a + 2 : kOffDrop, 0, 0);
   }
-}
-
-// Alpha-first frames (FrameDesc::alpha_off16): the 4 pixels' A bytes from the dword of the
-// unfiltered alpha plane (EmitAlphaRGB's A, io_dec.c.go:175-195), one v_perm each.
-__device__ __forceinline__ u32x4 with_alpha(u32x4 px, uint32_t a) {
-  return u32x4{__builtin_amdgcn_perm(a, px.x, 0x04020100u), __builtin_amdgcn_perm(a, px.y, 0x05020100u),
-               __builtin_amdgcn_perm(a, px.z, 0x06020100u), __builtin_amdgcn_perm(a, px.w, 0x07020100u)};
 }
 
 // Strips and bands of a frame: strip tx covers x in [1024 tx, 1024 tx + 1024), band j the
@@ -397,16 +403,8 @@ __device__ __forceinline__ void convert_strip(const FrameDesc& F, int tx, int ba
       for (int k = 0; k < kGroups; ++k) {
         const int x = xl + 256 * k;
         if (!live(k)) continue;
-        if (ya >= 0) {
-          u32x4 px = convert_group(prv, cur, k, yA[k]);
-          if (ha) px = with_alpha(px, aA[k]);
-          store_out<kAux, kModes>(out, em, roff(ya), x, px, W - x, full(k));
-        }
-        if (yb < H) {
-          u32x4 px = convert_group(cur, prv, k, yB[k]);
-          if (ha) px = with_alpha(px, aB[k]);
-          store_out<kAux, kModes>(out, em, roff(yb), x, px, W - x, full(k));
-        }
+        if (ya >= 0) store_out<kAux, kModes>(out, em, roff(ya), x, convert_group<ha>(prv, cur, k, yA[k], aA[k]), W - x, full(k));
+        if (yb < H) store_out<kAux, kModes>(out, em, roff(yb), x, convert_group<ha>(cur, prv, k, yB[k], aB[k]), W - x, full(k));
       }
       raw_cur = raw_next;
       // K1's tail yields the SIMD for a moment after each pair: its denser packed code otherwise
@@ -444,9 +442,10 @@ __device__ __forceinline__ void convert_strip(const FrameDesc& F, int tx, int ba
           const int yr = 2 * p + r;
           if (yr >= H) break;
           const uint32_t yw = r ? yB[k] : yA[k];
-          const uint2 a = yuv_to_rgba2(luma_lanes(yw, 0, 1), u0, v0), b = yuv_to_rgba2(luma_lanes(yw, 2, 3), u1, v1);
-          u32x4 px{a.x, a.y, b.x, b.y};
-          if (ha) px = with_alpha(px, r ? aB[k] : aA[k]);
+          const uint32_t aw = r ? aB[k] : aA[k];
+          const uint2 a = yuv_to_rgba2<ha>(luma_lanes(yw, 0, 1), u0, v0, aw, kASel01),
+                      b = yuv_to_rgba2<ha>(luma_lanes(yw, 2, 3), u1, v1, aw, kASel23);
+          const u32x4 px{a.x, a.y, b.x, b.y};
           store_out<kAux, kModes>(out, em, roff(yr), x, px, W - x, full(k));
         }
       }
