@@ -839,8 +839,10 @@ int split_k1_parts(const wg_batch* b, int* from = nullptr) {
     if (f.status == WG_STATUS_OK && !f.lossless) max_quads = std::max(max_quads, (f.info.mb_h + kQuadRows - 1) / kQuadRows);
   }
   const int cap = kCUs / std::max(1, (b->n - head + 7) / 8 * 8);  // (the grid rounds the frames up to XCD groups)
-  const int want = (max_quads + kRecon - 1) / kRecon;              // slabs of 12 quads
-  const int parts = std::min({3, cap, want});
+  const int want = (max_quads + kRecon - 1) / kRecon;              // slabs of at most 12 quads
+  // as many parts as fit (up to 3), the quads balanced over them (split_slab): a 1080p frame's 17
+  // quads on 3 parts of 6 instead of 2 of 12 + 5 -- anim K1 1.965 -> 1.880 ms (k1_split_slab/)
+  const int parts = want >= 2 ? std::min(3, cap) : 1;
   // (fewer parts than slabs would leave the taller frames on part 0 alone, without the RGBA tail:
   // slower than the one-workgroup kernel -- 128 4K frames on 2 parts: 7.8 vs 7.5 ms)
   if (parts < 2 || parts < want) return 1;
@@ -891,6 +893,19 @@ bool set_alpha_first(wg_batch* b) {
     b->desc[(size_t)i].alpha_off16 = af ? (int32_t)((f.off_aplane - f.off_y) / 16) : 0;
   }
   return changed;
+}
+
+// The split kernel's slab (MB-row quads per part): the split frames' quads balanced over the parts,
+// at most 12 (one per reconstructing wave); a frame with more quads than parts * slab runs on part 0.
+int split_slab(const wg_batch* b, int from) {
+  constexpr int kRecon = 12, kQuadRows = 4;
+  int max_quads = 0;
+  for (int i = from; i < b->n; ++i) {
+    const FrameParse& f = b->fp[(size_t)i];
+    if (f.status == WG_STATUS_OK && !f.lossless) max_quads = std::max(max_quads, (f.info.mb_h + kQuadRows - 1) / kQuadRows);
+  }
+  const int p = std::max(2, b->split_parts);
+  return std::min(kRecon, std::max(1, (max_quads + p - 1) / p));
 }
 
 // Tags of the split kernel's progress flags: a fresh value per launch, never 0 (the flags are
@@ -1184,7 +1199,7 @@ int wg_batch_run(wg_batch* b, void* stream) {
             e = wg::launch_vp8_recon_filter(b->d_desc, head, b->max_mb_w, b->n_lossy > b->n_wide, b->n_wide > 0, b->d_err, s);
           if (e == hipSuccess && b->split_parts >= 2)
             e = wg::launch_vp8_recon_filter(b->d_desc + head, b->n - head, b->max_mb_w, false, false, b->d_err, s,
-                                            b->split_parts, next_epoch());
+                                            b->split_parts, next_epoch(), split_slab(b, head));
         }
         break;
       case kStageK2:

@@ -13,10 +13,10 @@ int vp8_recon_max_mb_w();
 // d_err: device int, OR-ed with 1 if a wave gave up waiting (bounded spin).
 // split_parts >= 2: the split kernel (split_parts workgroups per frame, every frame, no RGBA
 // tail; `epoch` tags its part-boundary flags and must differ from the previous launch's on the
-// same descriptors).
+// same descriptors); `slab`: MB-row quads per part (one per reconstructing wave, at most 12; 0 = 12).
 hipError_t launch_vp8_recon_filter(const FrameDesc* d_frames, int n_frames, int max_mb_w, bool lds_frames,
                                    bool wide_frames, int* d_err, hipStream_t stream, int split_parts = 1,
-                                   uint32_t epoch = 0);
+                                   uint32_t epoch = 0, int slab = 0);
 
 // K2: YUV420 -> RGBA (fancy 9-3-3-1 upsampling or point sampling) over a batch.
 // `single` (when non-null, n_frames == 1) is passed by value instead of d_frames.

@@ -1236,7 +1236,8 @@ size_t vp8_recon_lds_bytes(int mb_w) {
 int vp8_recon_max_mb_w() { return (int)((163840 - kHdrBytes - kMaxRecon * kRows * kSlotBytes) / kColBytes); }
 
 hipError_t launch_vp8_recon_filter(const FrameDesc* d_frames, int n_frames, int max_mb_w, bool lds_frames,
-                                   bool wide_frames, int* d_err, hipStream_t stream, int split_parts, uint32_t epoch) {
+                                   bool wide_frames, int* d_err, hipStream_t stream, int split_parts, uint32_t epoch,
+                                   int slab) {
   // WG_K1_LEAD overrides the inter-quad lead (tuning experiments only).
   static const int lead = [] {
     const char* e = getenv("WG_K1_LEAD");
@@ -1259,8 +1260,10 @@ hipError_t launch_vp8_recon_filter(const FrameDesc* d_frames, int n_frames, int 
       configured = true;
     }
     const int grid = ((n_frames + 7) / 8) * 8 * split_parts;
+    // (the slab: balanced over the parts by the caller -- fewer reconstructing waves per CU, each
+    // issuing faster; WG_K1_RECON_WAVES still overrides it for measurements)
     hipLaunchKernelGGL((vp8_recon_filter_kernel<true, true>), dim3(grid), dim3(1024), lds, stream, d_frames, d_err,
-                       lead, recon_waves, n_frames, split_parts, epoch);
+                       lead, recon_waves > 0 ? recon_waves : slab, n_frames, split_parts, epoch);
     return hipGetLastError();
   }
   if (lds_frames) {

@@ -20,7 +20,7 @@ for rep in $(seq 1 ${REPS:-2}); do
     for w in ${WLS:-c3a}; do
       lib=$v; [ $v = new ] && lib=""
       wl=${w%%:*}; bt=256; [ "$wl" != "$w" ] && bt=${w#*:}  # (workload:batch)
-      WG_LIB_VARIANT=$lib timeout -k 10 300 python bench.py --workload $wl --batch $bt --steps 10 --warmup 3 --no-cpu-baseline --no-e2e \
+      WG_LIB_VARIANT=$lib timeout -k 10 300 python bench.py --workload $wl --batch $bt --steps 10 --warmup 3 --no-cpu-baseline --no-e2e $BENCH_ARGS \
         > $OUT/ab_${w}_${v}_$rep.log 2>&1 || { tail $OUT/ab_${w}_${v}_$rep.log; exit 1; }
       python -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); print(sys.argv[2], sys.argv[3], d['value'], d['ms_per_step'], {k: round(x, 3) for k, x in d['kernel_ms'].items()})" \
         $OUT/ab_${w}_${v}_$rep.log $v $w
