@@ -140,6 +140,28 @@ __device__ __forceinline__ uint32_t src_quad(const AlphaDesc& F, const uint8_t* 
          src_byte(F, palg, y, x + 3) << 24;
 }
 
+// An 8-bit alpha stream with a map of at most 16 colours (bits >= 1): the four pixels' filtered
+// bytes straight from the map's green bytes held in four uniform dwords `pg` (entries 4j .. 4j + 3
+// in pg[j]), by v_perm on the four indices at once instead of four LDS reads.
+__device__ __forceinline__ uint32_t pal_quad(const AlphaDesc& F, const uint32_t pg[4], int y, int x) {
+  const uint32_t* c = F.coded + (size_t)y * F.coded_width;
+  uint32_t i4;
+  if (F.cbits == 1) {
+    const uint32_t a = (c[x >> 1] >> 8) & 0xff, b = (c[(x >> 1) + 1] >> 8) & 0xff;
+    i4 = (a & 15) | (a >> 4) << 8 | (b & 15) << 16 | (b >> 4) << 24;
+  } else if (F.cbits == 2) {
+    const uint32_t g = (c[x >> 2] >> 8) & 0xff;
+    i4 = (g & 3) | ((g >> 2) & 3) << 8 | ((g >> 4) & 3) << 16 | (g >> 6) << 24;
+  } else {
+    const uint32_t t = ((c[x >> 3] >> 8) & 0xff) >> (x & 7);
+    i4 = (t & 1) | ((t >> 1) & 1) << 8 | ((t >> 2) & 1) << 16 | ((t >> 3) & 1) << 24;
+  }
+  const uint32_t sel = i4 & 0x07070707u;
+  const uint32_t lo = __builtin_amdgcn_perm(pg[1], pg[0], sel), hi = __builtin_amdgcn_perm(pg[3], pg[2], sel);
+  const uint32_t m = ((i4 >> 3) & 0x01010101u) * 0xffu;
+  return (hi & m) | (lo & ~m);
+}
+
 // Filters none / horizontal straight from the filtered bytes into the A bytes, one wave per
 // output row, no plane: HorizontalUnfilter_C (filters.go:130-140) is out[y][x] = out[y-1][0] +
 // sum_{i<=x} in[y][i] (mod 256), and out[y-1][0] is the column-0 prefix c[y-1], so the rows are
@@ -168,6 +190,14 @@ __device__ void alpha_rows_direct(const AlphaDesc& F, int part, int parts, uint8
     }
     __syncthreads();
   }
+  const bool ppal = F.coded && F.pal && F.cbits >= 1;  // (pal_quad)
+  uint32_t pg[4] = {0u, 0u, 0u, 0u};
+  if (ppal) {
+    const int ne = 1 << (8 >> F.cbits);
+#pragma unroll
+    for (int e = 0; e < 16; ++e)
+      if (e < ne) pg[e >> 2] |= ((F.pal[e] >> 8) & 0xffu) << (8 * (e & 3));
+  }
   const bool gvec = F.green && (reinterpret_cast<uintptr_t>(F.green) & 15) == 0 && (W & 3) == 0;
   const bool ovec = ((reinterpret_cast<uintptr_t>(F.rgba) | (uintptr_t)F.rgba_stride) & 15) == 0 && (F.win_x & 3) == 0;
   const bool pvec = (W & 3) == 0;  // to_plane: the rows' dwords are aligned (the plane is)
@@ -181,7 +211,7 @@ __device__ void alpha_rows_direct(const AlphaDesc& F, int part, int parts, uint8
     for (int x0 = horiz ? 0 : (F.win_x & ~255); x0 < xe; x0 += 256) {
       const int x = x0 + 4 * lane;
       uint32_t q = 0;
-      if (x + 3 < W) q = src_quad(F, palg, y, x, gvec);
+      if (x + 3 < W) q = ppal ? pal_quad(F, pg, y, x) : src_quad(F, palg, y, x, gvec);
       else
         for (int k = 0; k < 4 && x + k < W; ++k) q |= src_byte(F, palg, y, x + k) << (8 * k);
       uint32_t o = q;
