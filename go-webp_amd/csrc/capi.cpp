@@ -157,6 +157,9 @@ void* pinned_alloc(size_t bytes) {
 }
 void pinned_free(void* p) { hipHostFree(p); }
 
+// the split kernel's launch-tag counter (next_epoch, below)
+std::atomic<uint32_t> g_epoch{0};
+
 }  // namespace
 
 struct wg_ctx {
@@ -321,6 +324,8 @@ int guarded(F&& f) {
 extern "C" {
 
 int wg_version(void) { return 0x000100; }
+
+uint32_t wg_debug_set_epoch(uint32_t value) { return g_epoch.exchange(value, std::memory_order_relaxed); }
 
 int wg_device_count(void) {
   int n = 0;
@@ -908,12 +913,17 @@ int split_slab(const wg_batch* b, int from) {
   return std::min(kRecon, std::max(1, (max_quads + p - 1) / p));
 }
 
-// Tags of the split kernel's progress flags: a fresh value per launch, never 0 (the flags are
-// zeroed at upload), so a flag left by an earlier launch on the same buffers never matches.
+// Tags of the split kernel's progress flags (epoch << 16 | columns done): a fresh value per launch,
+// never 0.  The tag is 16 bits and the counter process-wide, so it repeats every 65,535 split
+// launches: correctness does not rest on it.  wg_batch_run zeroes the batch's flags on the launch
+// stream before every split launch (hipMemsetAsync, 512 B per frame), so a flag left by an earlier
+// launch reads 0 whatever its tag; the tag only keeps a flag from a launch still running on
+// another stream (two concurrent runs of one batch, which race on its planes anyway) from being
+// taken for this one's.  wg_debug_set_epoch moves the counter (tests: a re-run exactly one tag
+// cycle later).
 uint32_t next_epoch() {
-  static std::atomic<uint32_t> epoch{0};
   uint32_t e;
-  do e = (epoch.fetch_add(1, std::memory_order_relaxed) + 1) & 0xffffu;
+  do e = (g_epoch.fetch_add(1, std::memory_order_relaxed) + 1) & 0xffffu;
   while (e == 0);
   return e;
 }
@@ -1197,6 +1207,9 @@ int wg_batch_run(wg_batch* b, void* stream) {
           const int head = b->split_parts >= 2 ? b->split_from : b->n;  // frames on the one-workgroup kernels
           if (head > 0)
             e = wg::launch_vp8_recon_filter(b->d_desc, head, b->max_mb_w, b->n_lossy > b->n_wide, b->n_wide > 0, b->d_err, s);
+          // (the split frames' progress flags cleared first, in stream order: see next_epoch)
+          if (e == hipSuccess && b->split_parts >= 2)
+            e = hipMemsetAsync(b->d_planes + b->off_gprog, 0, b->gprog_bytes, s);
           if (e == hipSuccess && b->split_parts >= 2)
             e = wg::launch_vp8_recon_filter(b->d_desc + head, b->n - head, b->max_mb_w, false, false, b->d_err, s,
                                             b->split_parts, next_epoch(), split_slab(b, head));
@@ -1252,7 +1265,14 @@ int wg_batch_run(wg_batch* b, void* stream) {
   for (int i = 0; i < kStages; ++i) {
     if (i > 0) hipEventRecord(t.ev[i], s);
     const int st = stage(t.order[i]);
-    if (st != WG_STATUS_OK) return st;
+    if (st != WG_STATUS_OK) {
+      // a K7 already forked onto the side stream may still write the batch's planes and error word:
+      // the side stream's work joins the batch's completion events, so batch_wait (and
+      // wg_batch_destroy, before the buffers go back to the cache) waits for it
+      if (t.forked) (void)batch_mark_done(b, side);
+      (void)batch_mark_done(b, s);
+      return st;
+    }
   }
   hipEventRecord(t.ev[kStages], s);
   return batch_mark_done(b, s) == hipSuccess ? WG_STATUS_OK : WG_STATUS_OUT_OF_MEMORY;
@@ -1338,6 +1358,11 @@ int wg_batch_set_k1_parts(wg_batch* b, int parts) {
     if (st != WG_STATUS_OK) return st;
   }
   if (p >= 2 && from > 0 && b->any_crop) return WG_STATUS_OK;  // (cropped: whole rounds only)
+  // back to one part from a whole-batch split (which had switched the batch to K2): the kernels with
+  // the RGBA tail again, where the batch can take them (no crop window, no frame emitted in a mode
+  // the tail lacks).  A batch set to K2 by wg_batch_set_emit(b, 1) keeps K2.
+  if (p == 1 && b->split_parts >= 2 && b->split_from == 0 && !b->fused && !b->any_crop && !b->no_tail)
+    return wg_batch_set_emit(b, 0);
   b->split_parts = p;
   b->split_from = p >= 2 ? from : 0;
   return batch_set_alpha_first(b);

@@ -728,7 +728,9 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
     // Rows above exist for y > 0 only: kDrop + 16x stays beyond the planes.
     uint32_t sb_y, sb_c;
     {
-      const int m0 = lane & 15, rc = m0 & 7;
+      int lid0;  // (opaque, like the loop's lane roles: lane-constant terms hoisted out of the quad loop spilled)
+      asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lid0));
+      const int m0 = lid0 & 15, rc = m0 & 7;
       // (minus 4: the per-MB offset adds the segment's window column, 0 or 4)
       sb_y = m0 >= 13 ? (y > 0 ? (uint32_t)__mul24(16 * y - 16 + m0, ys) - 4u : kDrop)
                       : (uint32_t)__mul24(16 * y + m0, ys) - 4u;
@@ -791,6 +793,10 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
             }
           }
         }
+        // Compiler barrier: the relaxed sc1 column-store loads below must not be moved above the
+        // relaxed poll (the hardware orders them: the poll's value is waited for and branched on
+        // before they issue).  tests/test_k1_isa.py checks the machine code at this marker.
+        asm volatile("; wg-gprog-polled" ::: "memory");
       } else if (k > 0 && i < mb_w) {
         const uint32_t need = ((uint32_t)(k - 1) << 16) | (uint32_t)min(i + lead, mb_w);
         uint32_t* pr = progress + ((k - 1) & (kWaves - 1));
@@ -1167,7 +1173,9 @@ __global__ void __launch_bounds__(1024) vp8_recon_filter_kernel(const FrameDesc*
         // wave's sc1 column-store stores have completed: vmcnt(0), then the sc1 flag store)
         const int xl = i - 2 * (kRows - 1);
         if (xl >= 0 && ((xl & 3) == 3 || xl + 1 == mb_w)) {
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          // (also a compiler barrier: the flag store stays behind every sc1 column-store store;
+          // tests/test_k1_isa.py checks the machine code at this marker)
+          asm volatile("s_waitcnt vmcnt(0) ; wg-gprog-publish" ::: "memory");
           if (lane == 16 * (kRows - 1))
             __hip_atomic_store(gprog + 32 * part, ((epoch & 0xffffu) << 16) | (uint32_t)(xl + 1), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);

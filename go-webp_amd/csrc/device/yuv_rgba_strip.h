@@ -243,6 +243,9 @@ __device__ __forceinline__ void store_group(__amdgpu_buffer_rsrc_t o, uint32_t o
   if (full) {  // (wave-uniform: every lane's group is whole and the rows 16-byte aligned)
     __builtin_amdgcn_raw_buffer_store_b128(px, o, off, 0, kAux);
   } else {  // dword stores, those past the width dropped through the buffer range
+    // (nvalid made opaque here: the lane masks of the four compares would otherwise be hoisted out
+    // of the pair loop for every group, 32 SGPRs live across it, and spilled)
+    asm volatile("" : "+v"(nvalid));
     __builtin_amdgcn_raw_buffer_store_b32(px.x, o, nvalid > 0 ? off : kOffDrop, 0, 0);
     __builtin_amdgcn_raw_buffer_store_b32(px.y, o, nvalid > 1 ? off + 4 : kOffDrop, 0, 0);
     __builtin_amdgcn_raw_buffer_store_b32(px.z, o, nvalid > 2 ? off + 8 : kOffDrop, 0, 0);
@@ -298,6 +301,7 @@ __device__ __forceinline__ void store_out(__amdgpu_buffer_rsrc_t o, int em, uint
     return;
   }
   const uint32_t off = roff + (uint32_t)(bpp * x);
+  asm volatile("" : "+v"(nvalid));  // (as in store_group: no hoisted per-group lane masks)
   if (full) {
     if (bpp == 2) __builtin_amdgcn_raw_buffer_store_b64(u32x2{c.x | c.y << 16, c.z | c.w << 16}, o, off, 0, kAux);
     else __builtin_amdgcn_raw_buffer_store_b96(u32x3{c.x | c.y << 24, c.y >> 8 | c.z << 16, c.z >> 16 | c.w << 8}, o, off, 0, kAux);
@@ -338,8 +342,16 @@ __device__ __forceinline__ void convert_strip(const FrameDesc& F, int tx, int ba
   // per group k, from the wave's first pixel x0 (scalar): some lane's group lies in the frame
   // (else skipped), every lane's group is whole (one 16-byte store each)
   const int x0 = tx * kStripPx;
-  auto live = [&](int k) { return x0 + 256 * k < W; };
-  auto full = [&](int k) { return aligned && x0 + 256 * k + 256 <= W; };
+  // groups of the strip in the frame / whole (one 16-byte store each), as two scalar counts compared
+  // per group: eight uniform booleans would be eight 64-bit lane masks held across the pair loop
+  // (K1's tail spilled them).  refresh() makes the counts opaque at the top of each pair, so the
+  // compares are not hoisted back out of it.
+  // (wave-uniform: one frame per wave strip; readfirstlane where the compiler cannot prove it)
+  int n_live = __builtin_amdgcn_readfirstlane((W - x0 + 255) >> 8);
+  int n_full = __builtin_amdgcn_readfirstlane(aligned ? (W - x0) >> 8 : 0);
+  auto refresh = [&] { asm volatile("" : "+s"(n_live), "+s"(n_full)); };
+  auto live = [&](int k) { return k < n_live; };
+  auto full = [&](int k) { return k < n_full; };
   const gptr<const uint8_t> U = as_global(static_cast<const uint8_t*>(F.u));
   const gptr<const uint8_t> V = as_global(static_cast<const uint8_t*>(F.v));
   const int ys = F.y_stride, uvs = F.uv_stride, os = F.rgba_stride;
@@ -389,6 +401,7 @@ __device__ __forceinline__ void convert_strip(const FrameDesc& F, int tx, int ba
     auto pair_step = [&](int p, const ChromaCols& prv) __attribute__((always_inline)) {
       const int ya = 2 * p - 1, yb = 2 * p;
       asm volatile("" : "+s"(em));  // (no loop copy per output mode: only the conversion switches)
+      refresh();
       uint32_t yA[kGroups], yB[kGroups], aA[kGroups] = {}, aB[kGroups] = {};
       load_luma(ya, yA);
       load_luma(yb, yB);
@@ -422,6 +435,7 @@ __device__ __forceinline__ void convert_strip(const FrameDesc& F, int tx, int ba
     const int p1 = min(p0 + kPairs, npairs);
     for (int p = p0; p < p1; ++p) {
       asm volatile("" : "+s"(em));
+      refresh();
       uint32_t yA[kGroups], yB[kGroups], aA[kGroups] = {}, aB[kGroups] = {};
       load_luma(2 * p, yA);
       load_luma(2 * p + 1, yB);

@@ -219,6 +219,7 @@ _SIGS = {
     "wg_anim_batch_create": (_P, [_P, _P, C.c_size_t, C.c_int32, _P]),
     "wg_anim_batch_info": (C.c_int, [_P, _P, _P, _P]),
     "wg_anim_batch_download": (C.c_int, [_P, _P, C.c_size_t, _P]),
+    "wg_debug_set_epoch": (C.c_uint32, [C.c_uint32]),
 }
 EXPORTED = tuple(_SIGS)
 

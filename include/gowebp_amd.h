@@ -59,6 +59,12 @@ int wg_version(void);
 /* Number of HIP devices visible (0 when no GPU). */
 int wg_device_count(void);
 
+/* Test hook (no libwebp counterpart): sets the process-wide counter behind the split K1 kernel's
+ * 16-bit launch tags and returns its previous value, so a test can re-run a batch exactly one tag
+ * cycle (65,535 split launches) later.  Correctness does not depend on the tags: every split launch
+ * clears its batch's progress flags first. */
+uint32_t wg_debug_set_epoch(uint32_t value);
+
 /* Replaces WebPGetFeatures (pkg/libwebp/webp/decode.go:54-56 -> webp.go:764-779,
  * ParseHeadersInternal webp.go:300-440).  Host only, no GPU needed.
  * Backs Go's webp.DecodeConfig (decode.go:12-14). */
@@ -205,8 +211,10 @@ int wg_batch_run(wg_batch* b, void* stream);
  * inside the decode loop, io_dec.c.go:65-115). */
 int wg_batch_set_emit(wg_batch* b, int separate);
 
-/* Workgroups per frame for K1 (tests, measurement): 1 = one per frame (the kernels with the
- * RGBA tail); 2..4 = the split kernel, each frame's MB-row quads spread over that many CUs (K2
+/* Workgroups per frame for K1 (tests, measurement): 1 = one per frame -- coming from a split of
+ * the whole batch, the kernels with the RGBA tail again when the batch can take them (no crop
+ * window, no frame emitted in a mode the tail lacks); a batch set to K2 by wg_batch_set_emit(b, 1)
+ * keeps K2; 2..4 = the split kernel, each frame's MB-row quads spread over that many CUs (K2
  * converts); 0 = the automatic choice, which a batch makes at creation: split when it holds
  * fewer frames than CUs and a frame has more quads than one workgroup runs at once. */
 int wg_batch_set_k1_parts(wg_batch* b, int parts);
@@ -238,7 +246,8 @@ int64_t wg_batch_pixels(const wg_batch* b);
 /* Copy results of frame i back to host: RGBA of the output window (stride >= 4*width; no flip,
  * whatever the batch's colorspace -- except a lossy frame without alpha or crop window in a
  * non-RGBA / flipped batch, which is written straight in the batch's colorspace and has no RGBA
- * copy: UNSUPPORTED_FEATURE), the batch's colorspace / flip (wg_batch_download, stride >=
+ * copy: UNSUPPORTED_FEATURE; such a batch is read with wg_batch_download, and a caller that needs
+ * RGBA creates the batch in MODE_RGBA), the batch's colorspace / flip (wg_batch_download, stride >=
  * bpp*width), and/or the full frame's Y/U/V planes (strides width, (width+1)/2).
  * wg_batch_download_rgba's destination may also be device memory (e.g. a torch tensor on the
  * batch's device): the copy is then device to device and the frame never crosses PCIe. */

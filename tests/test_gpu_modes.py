@@ -105,9 +105,10 @@ def test_resident_batch_runs_k6_as_a_stage(ctx, key):
                             for (_, g), dr in zip(sub, direct) if not dr)
         for i, (_, g) in enumerate(sub):
             np.testing.assert_array_equal(b.download(i), g[key], err_msg=f"{key} frame {i}")
-            if direct[i]:
-                with pytest.raises(webp_amd.WebPError):
+            if direct[i]:  # (written in the batch's mode only: no RGBA copy to download)
+                with pytest.raises(webp_amd.WebPError) as ei:
                     b.rgba(i)
+                assert ei.value.status == webp_amd.Status.UNSUPPORTED_FEATURE
     finally:
         b.close()
 

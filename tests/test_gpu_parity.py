@@ -315,6 +315,66 @@ def test_split_k1_fixtures(ctx, parts):
         b.close()
 
 
+def test_split_k1_epoch_wrap(ctx):
+    """The split kernel's progress-flag tags are 16 bits from a process-wide counter, so they
+    repeat every 65,535 split launches.  Run 1 (3 parts: 4K slabs of 12 + 12 + 10 quads) leaves
+    its boundary flags at "tag T, all columns done"; run 2 (2 parts: 34 quads > 2 x 12, the frame
+    on part 0 alone) publishes no flag and leaves the frame's BOTTOM row in the column store; run
+    3 (3 parts again) gets tag T once more -- as a run one tag cycle later would
+    (wg_debug_set_epoch moves the counter back).  Had run 1's flags survived, parts 1 and 2 would
+    start at once and read run 2's bottom-row columns: the flags are cleared before every split
+    launch, so every frame's RGBA is still libwebp's (c3 and the dense c3s 4K frames)."""
+    L = webp_amd.lib()
+    m = manifest()["bench"]
+    paths = bench_files("c3_4k")[:3] + bench_files("c3s_4k")[:2]
+    b = ctx.batch([open(p, "rb").read() for p in paths])
+
+    def check(tag):
+        for i, p in enumerate(paths):
+            assert _sha(b.rgba(i)) == m[os.path.basename(p)]["sha256"]["rgba"], (tag, i)
+    try:
+        for rep in range(2):
+            b.set_k1_parts(3)
+            b.run()
+            check(("run1", rep))
+            last = L.wg_debug_set_epoch(0)  # the counter after run 1: its low 16 bits are run 1's tag
+            L.wg_debug_set_epoch(last)
+            b.set_k1_parts(2)
+            b.run()
+            check(("run2", rep))
+            L.wg_debug_set_epoch((last - 1) & 0xffffffff)  # run 3 takes tag T again
+            b.set_k1_parts(3)
+            b.run()
+            check(("run3", rep))
+    finally:
+        b.close()
+
+
+def test_one_part_after_split_restores_tail(ctx):
+    """wg_batch_set_k1_parts(b, 1) after a split of the whole batch runs the one-workgroup kernel
+    with its RGBA tail again (no K2 launch: kernel_ms[1] == 0); a batch set to K2 by set_emit(True)
+    keeps K2.  RGBA = libwebp's either way."""
+    m = manifest()["bench"]
+    paths = bench_files("c2_1080p")[:3]
+    b = ctx.batch([open(p, "rb").read() for p in paths])
+    try:
+        def check(k2):
+            b.run()
+            ms = b.kernel_ms()
+            assert (ms[1] > 0) == k2, ms
+            for i, p in enumerate(paths):
+                assert _sha(b.rgba(i)) == m[os.path.basename(p)]["sha256"]["rgba"], (k2, i)
+        b.set_k1_parts(3)
+        check(True)
+        b.set_k1_parts(1)
+        check(False)
+        b.set_emit(True)
+        b.set_k1_parts(1)
+        check(True)
+    finally:
+        b.close()
+
+
 def test_single_frame_decode_uses_split_and_matches():
     """The single-frame drop-in (webp.Decode's path) on a 4K frame -- one frame, so the automatic
     choice runs the split kernel: libwebp's RGBA."""
