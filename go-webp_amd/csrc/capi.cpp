@@ -35,6 +35,7 @@ using wg::FrameDesc;
 using wg::FrameParse;
 using wg::LLDesc;
 using wg::MbRec;
+using wg::YuvaDesc;
 
 namespace {
 
@@ -279,6 +280,12 @@ struct wg_batch {
   uint8_t* d_out = nullptr;
   size_t out_bytes = 0;
   std::vector<size_t> off_out;
+  // K8: MODE_YUV / MODE_YUVA (yuv, yuva) -- every frame's output planes in its slot of d_out (Y, U,
+  // V, A back to back, yuva_planes), written by K8 in the K6 stage; no RGBA for lossy frames
+  bool yuv = false, yuva = false;
+  std::vector<YuvaDesc> ydesc;
+  YuvaDesc* d_ydesc = nullptr;
+  int yuv_max_uw = 1, yuv_max_uh = 1;
   // K5 (f3): an animation batch (wg_anim_batch_create) composites its canvases in wg_batch_run
   bool anim = false;
   int canvas_w = 0, canvas_h = 0;
@@ -542,6 +549,7 @@ void wg_batch_destroy(wg_batch* b) {
   c.put(b->d_out);
   c.put(b->d_fdesc);
   c.put(b->d_canvases);
+  c.put(b->d_ydesc);
   delete b;
 }
 
@@ -681,15 +689,18 @@ void batch_layout(wg_batch* b, wg::StagingArena& arena, int32_t* status) {
   // K6: a non-RGBA colorspace or flip.  Lossy frames without alpha or crop window leave the
   // YUV -> RGB strips (K1's tail or K2) in the output colorspace, straight into their output slot:
   // no RGBA copy for them, and K6 converts only the others.
-  b->k6 = !(b->opt.colorspace == 1 && !b->opt.flip);
-  const int obpp = wg::output_bpp(b->opt.colorspace);
+  b->yuv = b->opt.colorspace == 11 || b->opt.colorspace == 12;
+  b->yuva = b->opt.colorspace == 12;
+  b->k6 = !b->yuv && !(b->opt.colorspace == 1 && !b->opt.flip);
+  const int obpp = b->yuv ? 4 : wg::output_bpp(b->opt.colorspace);
   for (int i = 0; i < n; ++i) {
     FrameParse& f = b->fp[(size_t)i];
     if (status) status[i] = f.status;
     if (f.status != WG_STATUS_OK) continue;
     f.emit_direct = b->k6 && !f.lossless && !f.alpha && !f.cropped;
     f.off_rgba = rg_b;
-    if (!f.emit_direct) rg_b = align_up(rg_b + (size_t)f.rgba_w * f.rgba_h * 4);
+    // (YUV output: a lossy frame's planes are its output, only lossless frames have an RGBA)
+    if (!f.emit_direct && !(b->yuv && !f.lossless)) rg_b = align_up(rg_b + (size_t)f.rgba_w * f.rgba_h * 4);
     b->max_w = std::max(b->max_w, f.width);
     b->max_h = std::max(b->max_h, f.height);
     b->max_out_w = std::max(b->max_out_w, f.out_w);
@@ -728,7 +739,7 @@ void batch_layout(wg_batch* b, wg::StagingArena& arena, int32_t* status) {
     pl_b = align_up(pl_b + (size_t)inf.mb_w * 160);
     f.off_gprog = b->gprog_bytes;
     b->gprog_bytes += wg::kGProgBytes;
-    if (f.cropped) {  // K2 reads the crop window from compact planes (copied after K1)
+    if (f.cropped && !b->yuv) {  // K2 reads the crop window from compact planes (copied after K1)
       b->any_crop = true;
       f.yc_stride = (f.out_w + 15) & ~15;
       f.uvc_stride = ((((f.out_w + 1) >> 1) + 7) & ~7);
@@ -799,6 +810,24 @@ void batch_layout(wg_batch* b, wg::StagingArena& arena, int32_t* status) {
       b->n_k6++;
       b->k6_maxpx = std::max(b->k6_maxpx, f.out_w * f.out_h);
       k6 += (4.0 + b->out_bpp) * f.out_w * (double)f.out_h;
+    }
+    b->out_bytes = std::max<size_t>(ob, kAlign);
+  }
+  // K8 batches (MODE_YUV / MODE_YUVA): one slot of planes per frame in d_out; K8 reads the lossless
+  // frames' RGBA window / the lossy frames' plane windows (and alpha planes) and writes the planes
+  if (b->yuv) {
+    b->off_out.assign((size_t)n, 0);
+    size_t ob = 0;
+    for (int i = 0; i < n; ++i) {
+      const FrameParse& f = b->fp[(size_t)i];
+      if (f.status != WG_STATUS_OK) continue;
+      b->off_out[(size_t)i] = ob;
+      const double px = (double)f.out_w * f.out_h, uv = 2.0 * ((f.out_w + 1) / 2) * (double)((f.out_h + 1) / 2);
+      const double planes = px + uv + (b->yuva ? px : 0.0);
+      ob = align_up(ob + (size_t)planes);
+      k6 += planes + (f.lossless ? 4.0 * px : planes);
+      b->yuv_max_uw = std::max(b->yuv_max_uw, (f.out_w + 1) / 2);
+      b->yuv_max_uh = std::max(b->yuv_max_uh, (f.out_h + 1) / 2);
     }
     b->out_bytes = std::max<size_t>(ob, kAlign);
   }
@@ -885,7 +914,8 @@ bool set_alpha_first(wg_batch* b) {
     const char* e = getenv("WG_ALPHA_FIRST");
     return e && atoi(e) == 0;
   }();
-  const bool af = b->n_alpha > 0 && !b->any_crop && !off && (!b->fused || !k7_side_fits(b));
+  // (YUV output: always -- K8 takes A from the unfiltered planes)
+  const bool af = b->n_alpha > 0 && (b->yuv || (!b->any_crop && !off && (!b->fused || !k7_side_fits(b))));
   const bool changed = af != b->alpha_first;
   b->alpha_first = af;
   size_t j = 0;
@@ -1038,7 +1068,7 @@ int batch_upload(wg_batch* b, const wg::StagingArena& arena) {
   b->tail_modes = cs == 1 || cs == 7 || cs == 6;
   for (int i = 0; i < n && !b->tail_modes; ++i) b->no_tail |= b->fp[(size_t)i].emit_direct;
   if (b->no_tail && b->split_parts >= 2 && b->split_from > 0) b->split_parts = 1, b->split_from = 0;
-  b->fused = !b->any_crop && !b->no_tail && (b->split_parts < 2 || b->split_from > 0);
+  b->fused = !b->any_crop && !b->no_tail && !b->yuv && (b->split_parts < 2 || b->split_from > 0);
   if (b->fused)
     for (int i = 0; i < n; ++i)
       if (b->desc[(size_t)i].valid) b->desc[(size_t)i].flags |= wg::kFrameEmitRgba;
@@ -1069,6 +1099,46 @@ int batch_upload(wg_batch* b, const wg::StagingArena& arena) {
       const uint8_t* src = d.rgba + (size_t)f.win_y * d.rgba_stride + 4 * (size_t)f.win_x;
       b->edesc[(size_t)i] = EmitDesc{src, b->d_out + b->off_out[(size_t)i], d.rgba_stride, b->out_bpp * f.out_w,
                                      f.out_w, f.out_h, b->opt.colorspace, b->opt.flip ? 1 : 0, 1, 0};
+    }
+  }
+  // K8's descriptors: every frame's output window -> its slot of planes in d_out
+  if (b->yuv) {
+    b->d_out = static_cast<uint8_t*>(cache.get(b->out_bytes));
+    b->d_ydesc = static_cast<YuvaDesc*>(cache.get(sizeof(YuvaDesc) * (size_t)n));
+    if (!b->d_out || !b->d_ydesc) return WG_STATUS_OUT_OF_MEMORY;
+    b->ydesc.assign((size_t)n, YuvaDesc{});
+    for (int i = 0; i < n; ++i) {
+      const FrameParse& f = b->fp[(size_t)i];
+      if (f.status != WG_STATUS_OK) continue;
+      const FrameDesc& d = b->desc[(size_t)i];
+      YuvaDesc& y = b->ydesc[(size_t)i];
+      // the window origin: lossless exact (f.win_x / win_y), lossy snapped to even
+      const int wx = f.lossless ? f.win_x : (b->opt.use_cropping ? b->opt.crop_left & ~1 : 0);
+      const int wy = f.lossless ? f.win_y : (b->opt.use_cropping ? b->opt.crop_top & ~1 : 0);
+      y.width = f.out_w;
+      y.height = f.out_h;
+      y.flip = b->opt.flip ? 1 : 0;
+      y.valid = 1;
+      if (f.lossless) {
+        y.lossless = 1;
+        y.rgba = d.rgba + (size_t)wy * d.rgba_stride + 4 * (size_t)wx;
+        y.rgba_stride = d.rgba_stride;
+      } else {
+        y.y = d.y + (size_t)wy * d.y_stride + wx;
+        y.u = d.u + (size_t)(wy >> 1) * d.uv_stride + (wx >> 1);
+        y.v = d.v + (size_t)(wy >> 1) * d.uv_stride + (wx >> 1);
+        y.y_stride = d.y_stride;
+        y.uv_stride = d.uv_stride;
+        if (f.alpha && b->yuva) {  // (K4 leaves the unfiltered plane: to_plane, set_alpha_first)
+          y.a = b->d_planes + f.off_aplane + (size_t)wy * f.width + wx;
+          y.a_stride = f.width;
+        }
+      }
+      const size_t px = (size_t)f.out_w * f.out_h, uv = (size_t)((f.out_w + 1) / 2) * ((f.out_h + 1) / 2);
+      y.oy = b->d_out + b->off_out[(size_t)i];
+      y.ou = y.oy + px;
+      y.ov = y.ou + uv;
+      y.oa = b->yuva ? y.ov + uv : nullptr;
     }
   }
   // the staged inputs: one copy per arena chunk, from pinned memory
@@ -1107,6 +1177,8 @@ int batch_upload(wg_batch* b, const wg::StagingArena& arena) {
                        home);
   if (e == hipSuccess && b->k6)
     e = hipMemcpyAsync(b->d_edesc, b->edesc.data(), sizeof(EmitDesc) * (size_t)n, hipMemcpyHostToDevice, home);
+  if (e == hipSuccess && b->yuv)
+    e = hipMemcpyAsync(b->d_ydesc, b->ydesc.data(), sizeof(YuvaDesc) * (size_t)n, hipMemcpyHostToDevice, home);
   if (e != hipSuccess) {
     (void)hipGetLastError();
     return WG_STATUS_OUT_OF_MEMORY;
@@ -1172,11 +1244,11 @@ int wg_batch_run(wg_batch* b, void* stream) {
   t.ran[kStageK1] = b->n_lossy > 0;
   // (a split remainder behind fused rounds: K2 over the remainder)
   const int k2_from = b->fused ? b->split_from : 0;
-  t.ran[kStageK2] = b->n_lossy > 0 && (!b->fused || (b->split_parts >= 2 && b->split_from > 0));
+  t.ran[kStageK2] = b->n_lossy > 0 && !b->yuv && (!b->fused || (b->split_parts >= 2 && b->split_from > 0));
   t.ran[kStageK7] = b->n_k3 > 0;
   t.ran[kStageK3] = !b->lldesc.empty();
   t.ran[kStageK4] = b->n_alpha > 0;
-  t.ran[kStageK6] = b->k6 && b->n_k6 > 0;
+  t.ran[kStageK6] = (b->k6 && b->n_k6 > 0) || b->yuv;  // (YUV output: K8 in K6's place)
   t.ran[kStageK5] = b->anim;
   // launch order (ev[i] .. ev[i + 1] bracket stage order[i]): K1 / K2 first, or, alpha-first,
   // the alpha planes (K7 -> K3 -> K4) before the strips that take A from them: before K1 when its
@@ -1253,8 +1325,9 @@ int wg_batch_run(wg_batch* b, void* stream) {
       case kStageK4:  // after K3 (alpha streams) and K2 / K1's tail (A = 255), or alpha-first before them
         if (b->n_alpha > 0) e = wg::launch_alpha(b->d_adesc, b->n_alpha, s);
         break;
-      case kStageK6:  // the output colorspace / flip over every frame's final RGBA
-        if (t.ran[kStageK6]) e = wg::launch_emit(b->d_edesc, b->n, b->k6_maxpx, s);
+      case kStageK6:  // the output colorspace / flip over every frame's final RGBA (YUV output: K8)
+        if (b->yuv) e = wg::launch_emit_yuva(b->d_ydesc, b->n, b->yuv_max_uw, b->yuv_max_uh, s);
+        else if (t.ran[kStageK6]) e = wg::launch_emit(b->d_edesc, b->n, b->k6_maxpx, s);
         break;
       case kStageK5:  // an animation's canvases from its decoded frames
         if (b->anim) e = wg::launch_anim_compose(b->d_fdesc, b->n, b->d_canvases, b->canvas_w, b->canvas_h, s);
@@ -1339,7 +1412,8 @@ int batch_set_alpha_first(wg_batch* b) { return set_alpha_first(b) ? batch_uploa
 
 int wg_batch_set_emit(wg_batch* b, int separate) {
   if (!b) return WG_STATUS_INVALID_PARAM;
-  if (!separate && (b->any_crop || b->no_tail)) return WG_STATUS_INVALID_PARAM;  // crop windows / modes K2 emits
+  // crop windows / modes K2 emits / YUV output (no RGBA for lossy frames): no tail
+  if (!separate && (b->any_crop || b->no_tail || b->yuv)) return WG_STATUS_INVALID_PARAM;
   if (!separate) b->split_parts = 1, b->split_from = 0;  // K1's RGBA tail: the one-workgroup kernels
   if (b->fused == !separate) return batch_set_alpha_first(b);
   b->fused = !separate;
@@ -1361,7 +1435,7 @@ int wg_batch_set_k1_parts(wg_batch* b, int parts) {
   // back to one part from a whole-batch split (which had switched the batch to K2): the kernels with
   // the RGBA tail again, where the batch can take them (no crop window, no frame emitted in a mode
   // the tail lacks).  A batch set to K2 by wg_batch_set_emit(b, 1) keeps K2.
-  if (p == 1 && b->split_parts >= 2 && b->split_from == 0 && !b->fused && !b->any_crop && !b->no_tail)
+  if (p == 1 && b->split_parts >= 2 && b->split_from == 0 && !b->fused && !b->any_crop && !b->no_tail && !b->yuv)
     return wg_batch_set_emit(b, 0);
   b->split_parts = p;
   b->split_from = p >= 2 ? from : 0;
@@ -1370,6 +1444,7 @@ int wg_batch_set_k1_parts(wg_batch* b, int parts) {
 
 int wg_batch_run_emit(wg_batch* b, void* stream) {
   if (!b) return WG_STATUS_INVALID_PARAM;
+  if (b->yuv) return WG_STATUS_UNSUPPORTED_FEATURE;  // (YUV output: no RGBA stage)
   if (b->n_lossy == 0 || b->any_crop) return WG_STATUS_OK;
   if (!set_device(b->ctx->device)) return WG_STATUS_INVALID_PARAM;
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : b->home;
@@ -1763,6 +1838,7 @@ int wg_batch_download_rgba(wg_batch* b, int i, uint8_t* rgba, int stride) {
   if (b->fp[i].status != WG_STATUS_OK) return b->fp[i].status;
   const FrameParse& f = b->fp[i];
   if (f.emit_direct) return WG_STATUS_UNSUPPORTED_FEATURE;  // emitted in the batch's colorspace only
+  if (b->yuv && !f.lossless) return WG_STATUS_UNSUPPORTED_FEATURE;  // (YUV output: planes only)
   if (stride < 4 * f.out_w) return WG_STATUS_INVALID_PARAM;
   int st = batch_sync(b);
   if (st != WG_STATUS_OK) return st;
@@ -1774,6 +1850,7 @@ int wg_batch_download_rgba(wg_batch* b, int i, uint8_t* rgba, int stride) {
 int wg_batch_download(wg_batch* b, int i, uint8_t* out, int stride) {
   if (!b || i < 0 || i >= b->n || !out) return WG_STATUS_INVALID_PARAM;
   if (b->fp[i].status != WG_STATUS_OK) return b->fp[i].status;
+  if (b->yuv) return WG_STATUS_UNSUPPORTED_FEATURE;  // planes: wg_batch_download_yuva
   const FrameParse& f = b->fp[i];
   const int bpp = wg::output_bpp(b->opt.colorspace);
   if (stride < bpp * f.out_w) return WG_STATUS_INVALID_PARAM;
@@ -1799,6 +1876,86 @@ int wg_batch_download_yuv(wg_batch* b, int i, uint8_t* y, uint8_t* u, uint8_t* v
   if (e == hipSuccess && u) e = hipMemcpy2D(u, uw, d.u, d.uv_stride, uw, uh, hipMemcpyDeviceToHost);
   if (e == hipSuccess && v) e = hipMemcpy2D(v, uw, d.v, d.uv_stride, uw, uh, hipMemcpyDeviceToHost);
   return e == hipSuccess ? WG_STATUS_OK : WG_STATUS_USER_ABORT;
+}
+
+}  // extern "C"
+
+namespace {
+// CheckDecBuffer's test of external YUV(A) memory (buffer_dec.c.go): every plane present, strides at
+// least the plane widths, sizes at least stride * (h - 1) + width; the A plane only for MODE_YUVA.
+bool yuva_out_ok(const wg_yuva_buffer* o, int w, int h, bool yuva) {
+  if (!o || !o->y || !o->u || !o->v || (yuva && !o->a)) return false;
+  const int uw = (w + 1) / 2, uh = (h + 1) / 2;
+  auto fits = [](int stride, size_t size, int pw, int ph) {
+    return stride >= pw && size >= (size_t)stride * (size_t)(ph - 1) + (size_t)pw;
+  };
+  return fits(o->y_stride, o->y_size, w, h) && fits(o->u_stride, o->u_size, uw, uh) &&
+         fits(o->v_stride, o->v_size, uw, uh) && (!yuva || fits(o->a_stride, o->a_size, w, h));
+}
+
+// Queue frame i's planes (its slot of d_out, K8's output) to the caller's buffers on `s`.
+hipError_t queue_yuva_download(wg_batch* b, int i, const wg_yuva_buffer* o, hipStream_t s) {
+  const FrameParse& f = b->fp[(size_t)i];
+  const int w = f.out_w, h = f.out_h, uw = (w + 1) / 2, uh = (h + 1) / 2;
+  const uint8_t* base = b->d_out + b->off_out[(size_t)i];
+  const uint8_t* py = base;
+  const uint8_t* pu = py + (size_t)w * h;
+  const uint8_t* pv = pu + (size_t)uw * uh;
+  hipError_t e = hipMemcpy2DAsync(o->y, o->y_stride, py, w, w, h, hipMemcpyDefault, s);
+  if (e == hipSuccess) e = hipMemcpy2DAsync(o->u, o->u_stride, pu, uw, uw, uh, hipMemcpyDefault, s);
+  if (e == hipSuccess) e = hipMemcpy2DAsync(o->v, o->v_stride, pv, uw, uw, uh, hipMemcpyDefault, s);
+  if (e == hipSuccess && b->yuva) e = hipMemcpy2DAsync(o->a, o->a_stride, pv + (size_t)uw * uh, w, w, h, hipMemcpyDefault, s);
+  return e;
+}
+}  // namespace
+
+extern "C" {
+
+int wg_batch_download_yuva(wg_batch* b, int i, const wg_yuva_buffer* out) {
+  if (!b || i < 0 || i >= b->n) return WG_STATUS_INVALID_PARAM;
+  if (b->fp[(size_t)i].status != WG_STATUS_OK) return b->fp[(size_t)i].status;
+  if (!b->yuv) return WG_STATUS_UNSUPPORTED_FEATURE;  // an RGB-family batch: wg_batch_download
+  const FrameParse& f = b->fp[(size_t)i];
+  if (!yuva_out_ok(out, f.out_w, f.out_h, b->yuva)) return WG_STATUS_INVALID_PARAM;
+  int st = batch_sync(b);
+  if (st != WG_STATUS_OK) return st;
+  hipError_t e = queue_yuva_download(b, i, out, b->home);
+  if (e == hipSuccess) e = hipStreamSynchronize(b->home);
+  return e == hipSuccess ? WG_STATUS_OK : WG_STATUS_USER_ABORT;
+}
+
+int wg_decode_yuv_batch(wg_ctx* ctx, const uint8_t* const* data, const size_t* sizes, int n,
+                        const wg_decoder_options* opt, const wg_yuva_buffer* outs, int32_t* status) {
+  if (!ctx || !data || !sizes || !outs || !status || !opt || n <= 0 || (opt->colorspace != 11 && opt->colorspace != 12))
+    return WG_STATUS_INVALID_PARAM;
+  wg_batch* b = wg_batch_create_ex(ctx, data, sizes, n, opt, status);
+  if (!b) return WG_STATUS_OUT_OF_MEMORY;
+  int st = wg_batch_run(b, nullptr);
+  if (st == WG_STATUS_OK) st = batch_sync(b);
+  hipError_t e = hipSuccess;
+  for (int i = 0; st == WG_STATUS_OK && i < n && e == hipSuccess; ++i) {
+    if (status[i] != WG_STATUS_OK) continue;
+    const FrameParse& f = b->fp[(size_t)i];
+    if (!yuva_out_ok(&outs[i], f.out_w, f.out_h, b->yuva)) {
+      status[i] = WG_STATUS_INVALID_PARAM;
+      continue;
+    }
+    e = queue_yuva_download(b, i, &outs[i], b->home);
+  }
+  if (st == WG_STATUS_OK && (e != hipSuccess || hipStreamSynchronize(b->home) != hipSuccess)) st = WG_STATUS_USER_ABORT;
+  wg_batch_destroy(b);
+  return st;
+}
+
+int wg_decode_yuv_into(const uint8_t* data, size_t size, const wg_decoder_options* opt, const wg_yuva_buffer* out) {
+  if (!data || !opt || !out || (opt->colorspace != 11 && opt->colorspace != 12)) return WG_STATUS_INVALID_PARAM;
+  const std::shared_ptr<wg_ctx> ctx = default_ctx();  // held until this call returns
+  if (!ctx) return WG_STATUS_UNSUPPORTED_FEATURE;    // no GPU: no CPU fallback by design
+  const uint8_t* d[1] = {data};
+  const size_t s[1] = {size};
+  int32_t fs[1] = {0};
+  const int st = wg_decode_yuv_batch(ctx.get(), d, s, 1, opt, out, fs);
+  return st != WG_STATUS_OK ? st : fs[0];
 }
 
 int wg_decode_rgba_batch(wg_ctx* ctx, const uint8_t* const* data, const size_t* sizes, int n,
@@ -1863,6 +2020,7 @@ int wg_decode_batch(wg_ctx* ctx, const uint8_t* const* data, const size_t* sizes
                     uint8_t* const* out, const int32_t* strides, const size_t* caps, int32_t* status) {
   if (!ctx || !data || !sizes || !out || !strides || !caps || !status || !opt || n <= 0)
     return WG_STATUS_INVALID_PARAM;
+  if (opt->colorspace == 11 || opt->colorspace == 12) return WG_STATUS_INVALID_PARAM;  // wg_decode_yuv_batch
   wg_batch* b = wg_batch_create_ex(ctx, data, sizes, n, opt, status);
   if (!b) return WG_STATUS_OUT_OF_MEMORY;
   int st = wg_batch_run(b, nullptr);
@@ -1891,6 +2049,7 @@ int wg_decode_batch(wg_ctx* ctx, const uint8_t* const* data, const size_t* sizes
 int wg_decode_into(const uint8_t* data, size_t size, const wg_decoder_options* opt, uint8_t* out, size_t cap,
                    int stride) {
   if (!data || !out || !opt) return WG_STATUS_INVALID_PARAM;
+  if (opt->colorspace == 11 || opt->colorspace == 12) return WG_STATUS_INVALID_PARAM;  // wg_decode_yuv_into
   wg_features f{};
   int st = wg_get_features(data, size, &f);
   if (st != WG_STATUS_OK) return st;

@@ -48,6 +48,11 @@ hipError_t launch_alpha(const AlphaDesc* d_frames, int n_frames, hipStream_t str
 // K6: output colorspace / cropping window / flip, RGBA -> WEBP_CSP_MODE (0..10) bytes.
 hipError_t launch_emit(const EmitDesc* d_frames, int n_frames, int max_pixels, hipStream_t stream);
 
+// K8: MODE_YUV / MODE_YUVA output planes of every frame (YuvaDesc): lossy windows copied from the
+// reconstructed planes, lossless RGBA converted (ConvertToYUVA), A from the alpha plane / RGBA.
+// max_uw / max_uh: the largest chroma window.
+hipError_t launch_emit_yuva(const YuvaDesc* d_frames, int n_frames, int max_uw, int max_uh, hipStream_t stream);
+
 // K5: animation canvases (frames in display order, already decoded) -> n_frames canvases of
 // canvas_w x canvas_h RGBA.
 hipError_t launch_anim_compose(const AnimFrameDesc* d_frames, int n_frames, uint8_t* d_canvases, int canvas_w,

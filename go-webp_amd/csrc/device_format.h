@@ -141,6 +141,25 @@ struct AlphaDesc {
 };
 static_assert(sizeof(AlphaDesc) == 96, "AlphaDesc must be 96 bytes");
 
+// One frame's YUV output for K8 (emit_yuva.hip, MODE_YUV / MODE_YUVA): compact planes of the
+// output window -- Y (width x height), U and V ((width + 1) / 2 x (height + 1) / 2), A (width x
+// height, MODE_YUVA) -- from the lossy frame's reconstructed planes or the lossless frame's RGBA.
+struct YuvaDesc {
+  const uint8_t* y;      // lossy: the planes at the window origin (even x, y)
+  const uint8_t* u;
+  const uint8_t* v;
+  const uint8_t* rgba;   // lossless: the RGBA window origin
+  const uint8_t* a;      // lossy with ALPH: the unfiltered alpha plane at the window origin; else null (0xff)
+  uint8_t* oy;           // outputs, rows of width / (width + 1) / 2 bytes, row 0 at the top
+  uint8_t* ou;
+  uint8_t* ov;
+  uint8_t* oa;           // null: MODE_YUV
+  int32_t y_stride, uv_stride, rgba_stride, a_stride;
+  int32_t width, height, flip, lossless;
+  int32_t valid, pad0, pad1, pad2, pad3, pad4;
+};
+static_assert(sizeof(YuvaDesc) == 128, "YuvaDesc must be 128 bytes");
+
 // One frame's output conversion for K6 (emit.hip): RGBA window -> WEBP_CSP_MODE bytes.
 struct EmitDesc {
   const uint8_t* src;  // RGBA, first pixel of the window

@@ -108,8 +108,8 @@ void trim_ll(VP8LFrame& f) {
 }  // namespace
 
 int apply_output_options(const wg_decoder_options& opt, FrameParse* f) {
-  if (!output_bpp(opt.colorspace))
-    return (opt.colorspace == 11 || opt.colorspace == 12) ? WG_STATUS_UNSUPPORTED_FEATURE : WG_STATUS_INVALID_PARAM;
+  // the RGB family (0..10), or MODE_YUV / MODE_YUVA (11, 12: K8 writes the planes)
+  if (!output_bpp(opt.colorspace) && opt.colorspace != 11 && opt.colorspace != 12) return WG_STATUS_INVALID_PARAM;
   if (opt.use_scaling) return WG_STATUS_UNSUPPORTED_FEATURE;
   f->out_w = f->width;
   f->out_h = f->height;

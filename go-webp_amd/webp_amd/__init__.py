@@ -86,6 +86,28 @@ def options(colorspace=1, crop=None, flip=0, no_fancy=0, bypass=0, scale=None):
     return o
 
 
+class YUVABuffer(C.Structure):
+    """wg_yuva_buffer = WebPYUVABuffer (pkg/libwebp/webp/buffer.go:17-25): caller memory of the
+    MODE_YUV / MODE_YUVA planes."""
+    _fields_ = [("y", C.c_void_p), ("u", C.c_void_p), ("v", C.c_void_p), ("a", C.c_void_p),
+                ("y_stride", C.c_int32), ("u_stride", C.c_int32), ("v_stride", C.c_int32), ("a_stride", C.c_int32),
+                ("y_size", C.c_size_t), ("u_size", C.c_size_t), ("v_size", C.c_size_t), ("a_size", C.c_size_t)]
+
+
+def _yuva_arrays(w, h, alpha):
+    """Contiguous output planes of a w x h window and the YUVABuffer over them."""
+    uw, uh = (w + 1) // 2, (h + 1) // 2
+    out = {"y": np.empty((h, w), np.uint8), "u": np.empty((uh, uw), np.uint8), "v": np.empty((uh, uw), np.uint8)}
+    if alpha:
+        out["a"] = np.empty((h, w), np.uint8)
+    buf = YUVABuffer()
+    for k, arr in out.items():
+        setattr(buf, k, arr.ctypes.data)
+        setattr(buf, k + "_stride", arr.shape[1])
+        setattr(buf, k + "_size", arr.nbytes)
+    return out, buf
+
+
 class AnimInfo(C.Structure):
     """wg_anim_info = WebPAnimInfo."""
     _fields_ = [("canvas_width", C.c_uint32), ("canvas_height", C.c_uint32), ("loop_count", C.c_uint32),
@@ -220,6 +242,9 @@ _SIGS = {
     "wg_anim_batch_info": (C.c_int, [_P, _P, _P, _P]),
     "wg_anim_batch_download": (C.c_int, [_P, _P, C.c_size_t, _P]),
     "wg_debug_set_epoch": (C.c_uint32, [C.c_uint32]),
+    "wg_decode_yuv_into": (C.c_int, [_P, C.c_size_t, _P, _P]),
+    "wg_decode_yuv_batch": (C.c_int, [_P, _P, _P, C.c_int, _P, _P, _P]),
+    "wg_batch_download_yuva": (C.c_int, [_P, C.c_int, _P]),
 }
 EXPORTED = tuple(_SIGS)
 
@@ -298,6 +323,21 @@ def decode_into(data, opts):
     st = lib().wg_decode_into(b, len(b), C.byref(opts), out.ctypes.data, out.nbytes, out.shape[1])
     if st != Status.OK:
         raise WebPError(st, "wg_decode_into")
+    return out
+
+
+def decode_yuv(data, opts=None):
+    """Mirror of WebPDecodeYUV / WebPDecode in MODE_YUV (11) or MODE_YUVA (12) (opts.colorspace;
+    default MODE_YUV, no crop): one frame -> {"y", "u", "v"[, "a"]} planes of the output window."""
+    if opts is None:
+        opts = options(11)
+    b = _buf(data)
+    f = features(b)
+    w, h = (opts.crop_width, opts.crop_height) if opts.use_cropping else (f.width, f.height)
+    out, buf = _yuva_arrays(max(w, 1), max(h, 1), opts.colorspace == 12)
+    st = lib().wg_decode_yuv_into(b, len(b), C.byref(opts), C.byref(buf))
+    if st != Status.OK:
+        raise WebPError(st, "wg_decode_yuv_into")
     return out
 
 
@@ -513,6 +553,16 @@ class Batch:
             raise WebPError(st, "wg_batch_download_yuv")
         return y, u, v
 
+    def yuva(self, i):
+        """Frame i's MODE_YUV / MODE_YUVA planes of a batch created with colorspace 11 / 12
+        (wg_batch_download_yuva): {"y", "u", "v"[, "a"]}."""
+        w, h = self.dims(i)
+        out, buf = _yuva_arrays(w, h, self.opts is not None and self.opts.colorspace == 12)
+        st = lib().wg_batch_download_yuva(self._h, i, C.byref(buf))
+        if st != Status.OK:
+            raise WebPError(st, "wg_batch_download_yuva")
+        return out
+
     def close(self):
         if self._h:
             lib().wg_batch_destroy(self._h)
@@ -592,6 +642,26 @@ class Context:
         st = lib().wg_decode_batch(self._h, ptrs, sizes, n, C.byref(opts), optr, strides, caps, status.ctypes.data)
         if st != Status.OK:
             raise WebPError(st, "wg_decode_batch")
+        return [o if s == 0 else None for o, s in zip(outs, status)], status
+
+    def decode_yuv_batch(self, datas, opts):
+        """wg_decode_yuv_batch (opts.colorspace 11 / 12): frames -> ([{"y", "u", "v"[, "a"]} or None],
+        status)."""
+        bufs, ptrs, sizes = _ptr_arrays(datas)
+        n = len(bufs)
+        outs, yb = [], (YUVABuffer * n)()
+        for i, b in enumerate(bufs):
+            try:
+                f = features(b)
+                w, h = (opts.crop_width, opts.crop_height) if opts.use_cropping else (f.width, f.height)
+            except WebPError:
+                w = h = 1
+            o, yb[i] = _yuva_arrays(max(w, 1), max(h, 1), opts.colorspace == 12)
+            outs.append(o)
+        status = np.zeros(n, np.int32)
+        st = lib().wg_decode_yuv_batch(self._h, ptrs, sizes, n, C.byref(opts), yb, status.ctypes.data)
+        if st != Status.OK:
+            raise WebPError(st, "wg_decode_yuv_batch")
         return [o if s == 0 else None for o, s in zip(outs, status)], status
 
     def decode_anim(self, data, flags=0):

@@ -86,9 +86,11 @@ int wg_decode_rgba_into(const uint8_t* data, size_t size, uint8_t* rgba, size_t 
 int wg_set_default_device(int device);
 
 /* ---- output options (WebPDecoderConfig subset, pkg/libwebp/webp/decode.go:59-83) --------- */
-/* colorspace = WEBP_CSP_MODE of the RGB family: 0 RGB, 1 RGBA, 2 BGR, 3 BGRA, 4 ARGB,
- * 5 RGBA_4444, 6 RGB_565, 7 rgbA, 8 bgrA, 9 Argb, 10 rgbA_4444 (lower case = premultiplied);
- * the YUV modes 11/12 are UNSUPPORTED_FEATURE here (wg_batch_download_yuv gives the planes).
+/* colorspace = WEBP_CSP_MODE: the RGB family 0 RGB, 1 RGBA, 2 BGR, 3 BGRA, 4 ARGB, 5 RGBA_4444,
+ * 6 RGB_565, 7 rgbA, 8 bgrA, 9 Argb, 10 rgbA_4444 (lower case = premultiplied), or the YUV modes
+ * 11 MODE_YUV / 12 MODE_YUVA (planes: wg_decode_yuv_into / wg_decode_yuv_batch /
+ * wg_batch_download_yuva; the single-buffer entry points wg_decode_into / wg_decode_batch refuse
+ * them with INVALID_PARAM).
  * Cropping as WebPIoInitFromOptions: left/top snapped to even, the window must lie inside the
  * frame (else INVALID_PARAM).  Scaling is disabled in the reference (io_dec.c.go:540-541):
  * use_scaling -> UNSUPPORTED_FEATURE.  flip emits rows bottom-up. */
@@ -103,6 +105,27 @@ typedef struct {
 
 /* Bytes per pixel of a colorspace (3, 4 or 2); 0 if not an RGB-family mode. */
 int wg_output_bpp(int colorspace);
+
+/* ---- YUV output (MODE_YUV / MODE_YUVA) ---------------------------------------------------- */
+/* WebPYUVABuffer (pkg/libwebp/webp/buffer.go:17-25): caller memory for the Y plane (width x
+ * height), U and V ((width + 1) / 2 x (height + 1) / 2) and, MODE_YUVA, A (width x height) of the
+ * output window, rows of the given strides.  Checked as CheckDecBuffer checks external memory
+ * (buffer_dec.c.go): stride >= the plane's width, size >= stride * (rows - 1) + width, A present
+ * for MODE_YUVA (else INVALID_PARAM, nothing written). */
+typedef struct {
+  uint8_t *y, *u, *v, *a;
+  int32_t y_stride, u_stride, v_stride, a_stride;
+  size_t y_size, u_size, v_size, a_size;
+} wg_yuva_buffer;
+
+/* Replaces WebPDecodeYUVInto (webp.go:615-650) and WebPDecode with a MODE_YUV / MODE_YUVA
+ * config.output in external memory (webp.go:870-909): one frame on the GPU (default context) in
+ * opt->colorspace 11 or 12 with the options' crop window (lossy origins snapped to even) and flip.
+ * Lossy frames: the reconstructed planes' window (EmitYUV, io_dec.c.go:36-50) and the alpha plane
+ * or 0xff (EmitAlphaYUV :128-150); lossless frames: libwebp 1.6.0's per-row ConvertToYUVA
+ * (vp8l_dec.c.go:544-563).  Kernel K8 (device/emit_yuva.hip) writes the planes. */
+int wg_decode_yuv_into(const uint8_t* data, size_t size, const wg_decoder_options* opt,
+                       const wg_yuva_buffer* out);
 
 /* The status WebPDecode (webp.go:870-909) returns for this input and options (NULL = RGBA,
  * no crop), from the host stages alone: container, headers, options, then the entropy-coded
@@ -183,6 +206,11 @@ int wg_decode_batch(wg_ctx* ctx, const uint8_t* const* data, const size_t* sizes
                     const wg_decoder_options* opt, uint8_t* const* out, const int32_t* strides,
                     const size_t* caps, int32_t* status);
 
+/* wg_decode_yuv_into over n frames of one batch (opt->colorspace 11 or 12): outs[i] receives frame
+ * i's planes; per-frame status[i] (a frame whose buffer fails the check is INVALID_PARAM). */
+int wg_decode_yuv_batch(wg_ctx* ctx, const uint8_t* const* data, const size_t* sizes, int n,
+                        const wg_decoder_options* opt, const wg_yuva_buffer* outs, int32_t* status);
+
 /* ---- device-resident batch (benchmarks, tests) -------------------------------------- */
 typedef struct wg_batch wg_batch;
 
@@ -254,6 +282,10 @@ int64_t wg_batch_pixels(const wg_batch* b);
 int wg_batch_download_rgba(wg_batch* b, int i, uint8_t* rgba, int stride);
 int wg_batch_download(wg_batch* b, int i, uint8_t* out, int stride);
 int wg_batch_download_yuv(wg_batch* b, int i, uint8_t* y, uint8_t* u, uint8_t* v); /* lossy only */
+/* Frame i's MODE_YUV / MODE_YUVA planes of a batch created with colorspace 11 / 12 (K8's output of
+ * the last wg_batch_run; UNSUPPORTED_FEATURE for another batch; such a batch's wg_batch_download is
+ * UNSUPPORTED_FEATURE, its lossy frames have no RGBA). */
+int wg_batch_download_yuva(wg_batch* b, int i, const wg_yuva_buffer* out);
 
 /* ---- stage entry point: YUV420 -> RGBA on device pointers ---------------------------- */
 /* Fancy (fancy!=0, UpsampleRgbaLinePair, upsampling.c.go:43-107) or point-sampled

@@ -22,7 +22,7 @@ frames (SURVEY.md §8(d), Appendix B generators) are stored as ``.webp`` plus
 SHA-256 of their decodes in ``manifest.json``.  Every decode is also checked
 against libwebp's SIMD path (must be byte-identical) before it is written.
 
-Usage:  python tests/golden/make_golden.py [lossy|lossless|alpha|modes|anim|bench ...]
+Usage:  python tests/golden/make_golden.py [lossy|lossless|alpha|modes|yuv|anim|bench ...]
         (rewrites tests/golden/<section>/; default all sections)
 """
 import ctypes as C
@@ -460,6 +460,81 @@ def mode_cases(data, w, h, lossy):
     return out, statuses
 
 
+# ----------------------------------------------------------------------------- YUV output modes
+# MODE_YUV = 11, MODE_YUVA = 12 (WebPDecodeYUV / WebPDecodeYUVInto, webp.go:615-725; EmitYUV /
+# EmitAlphaYUV io_dec.c.go:36-60, 128-150 for lossy; libwebp 1.6.0 converts lossless rows with
+# ConvertToYUVA, vp8l_dec.c.go:544-563)
+def decode_yuva(data, mode, crop=None, flip=0, bypass=0):
+    """WebPDecode with config.output.colorspace = MODE_YUV / MODE_YUVA (+ crop / flip) -> (status,
+    {"y", "u", "v"[, "a"]} arrays)."""
+    cfg = (C.c_uint8 * 512)()
+    assert LIB.WebPInitDecoderConfigInternal(cfg, ABI)
+    ci = C.cast(cfg, C.POINTER(C.c_int32))
+    ci[40 // 4] = mode
+    ci[160 // 4] = bypass
+    if crop is not None:
+        ci[168 // 4] = 1
+        ci[172 // 4], ci[176 // 4], ci[180 // 4], ci[184 // 4] = crop
+    ci[208 // 4] = flip
+    st = LIB.WebPDecode(data, C.c_size_t(len(data)), cfg)
+    if st != 0:
+        return st, None
+    w, h = ci[44 // 4], ci[48 // 4]
+    cp = C.cast(cfg, C.POINTER(C.c_void_p))
+    # WebPYUVABuffer: y, u, v, a pointers at 56..80, strides y/u/v/a at 88..100
+    uw, uh = (w + 1) // 2, (h + 1) // 2
+
+    def plane(ptr, stride, pw, ph):  # (flip: DecodeInto restores pointer and stride, rows stored flipped)
+        return np.stack([np.frombuffer(C.string_at(ptr + r * stride, pw), np.uint8) for r in range(ph)])
+    out = {"y": plane(cp[56 // 8], ci[88 // 4], w, h), "u": plane(cp[64 // 8], ci[92 // 4], uw, uh),
+           "v": plane(cp[72 // 8], ci[96 // 4], uw, uh)}
+    if mode == 12:
+        out["a"] = plane(cp[80 // 8], ci[100 // 4], w, h)
+    LIB.WebPFreeDecBuffer(C.byref(cfg, 40))
+    return 0, out
+
+
+# sources: the output-mode ones (lossy with and without ALPH, lossless with alpha and palette) plus
+# lossless frames with odd sizes (the odd last column / row of ConvertToYUVA) and a
+# semi-transparent one with fully transparent and opaque regions (the A plane), and lossy ALPH
+# with level-quantized alpha
+YUV_SOURCES = MODE_SOURCES + [("lossless", "ll_corr_123x77"), ("alpha", "a_ll_q50_80x80"),
+                              ("yuv", "ll_alpha_odd_37x23")]
+YUV_CROPS = {"none": None, "c1": (3, 5, 20, 11), "c2": (0, 0, 9, 1), "c3": (6, 2, 1, 7), "c4": (5, 3, 12, 6),
+             "c5": (1, 1, 7, 5)}
+
+
+def yuv_extra_sources():
+    """Fixtures only the YUV section uses: written to tests/golden/yuv/."""
+    img = with_alpha(corr_luma(23, 37, 21), 21)
+    img[5:9, 20:30, 3] = 255  # an opaque patch among the semi-transparent and transparent ones
+    return {"ll_alpha_odd_37x23": encode(img, lossless=1, exact=1)}
+
+
+def yuv_cases(data, w, h):
+    """MODE_YUV / MODE_YUVA outputs per crop (flip on two crops); 'oob' records a status."""
+    out, statuses = {}, {}
+    crops = dict(YUV_CROPS)
+    crops["oob"] = (w - 4, 0, 8, 2)
+    for cname, crop in crops.items():
+        for mode in (11, 12):
+            for flip in (0, 1):
+                if flip and cname not in ("none", "c1"):
+                    continue
+                key = f"m{mode}_{cname}_f{flip}"
+                st, arrs = decode_yuva(data, mode, crop, flip)
+                _plain_c(False)
+                st2, arrs2 = decode_yuva(data, mode, crop, flip)
+                _plain_c(True)
+                assert st == st2, key
+                if arrs is not None:
+                    for k in arrs:
+                        assert np.array_equal(arrs[k], arrs2[k]), (key, k)
+                        out[f"{key}_{k}"] = arrs[k]
+                statuses[key] = st
+    return out, statuses
+
+
 # ----------------------------------------------------------------------------- animation
 DEMUX_ABI = 0x0107  # WEBP_DEMUX_ABI_VERSION of 1.6.0
 MUX_ABI = 0x0109    # WEBP_MUX_ABI_VERSION of 1.6.0
@@ -784,15 +859,15 @@ def sha(a):
 def main(argv):
     """argv: sections to (re)generate among lossy, lossy_extra, lossless, alpha, modes, anim, bench (default: all);
     the manifest entries of the other sections are kept."""
-    sections = set(argv) or {"lossy", "lossy_extra", "lossless", "alpha", "modes", "anim", "bench", "bench_c5x",
-                             "bench_c3s", "bench_c3a", "bench_anim", "bench_modes", "fuzz", "alpha_r5"}
+    sections = set(argv) or {"lossy", "lossy_extra", "lossless", "alpha", "modes", "yuv", "anim", "bench", "bench_c5x",
+                             "bench_c3s", "bench_c3a", "bench_anim", "bench_modes", "fuzz", "alpha_r5", "bench_yuva"}
     os.makedirs(os.path.join(HERE, "lossy"), exist_ok=True)
     os.makedirs(os.path.join(HERE, "lossless"), exist_ok=True)
     os.makedirs(os.path.join(HERE, "bench"), exist_ok=True)
     mpath = os.path.join(HERE, "manifest.json")
     manifest = json.load(open(mpath)) if os.path.exists(mpath) else {}
     manifest["libwebp"] = "1.6.0 (Pillow 12.2.0 bundle, plain-C DSP)"
-    for sec in sections - {"bench_c5x", "bench_c3s", "bench_c3a", "bench_modes", "alpha_r5"}:  # (these add)
+    for sec in sections - {"bench_c5x", "bench_c3s", "bench_c3a", "bench_modes", "alpha_r5", "bench_yuva"}:  # (these add)
         manifest[sec] = {}
     manifest.setdefault("alpha", {})
     manifest.setdefault("bench", {})
@@ -865,6 +940,20 @@ def main(argv):
                                                                                        "oob": [w - 4, 0, 8, 2]},
                                           status=statuses)
             print(src, len(arrs), "outputs", sum(1 for v in statuses.values() if v), "errors", flush=True)
+    if "yuv" in sections:
+        os.makedirs(os.path.join(HERE, "yuv"), exist_ok=True)
+        for name, data in yuv_extra_sources().items():
+            with open(os.path.join(HERE, "yuv", name + ".webp"), "wb") as f:
+                f.write(data)
+        for kind, src in YUV_SOURCES:
+            data = open(os.path.join(HERE, kind, src + ".webp"), "rb").read()
+            w, h = _decode_cfg(data, MODE_RGBA).shape[1::-1]
+            arrs, statuses = yuv_cases(data, w, h)
+            np.savez_compressed(os.path.join(HERE, "yuv", src + ".npz"), **arrs)
+            manifest["yuv"][src] = dict(source=f"{kind}/{src}.webp", width=w, height=h,
+                                        crops={k: v for k, v in YUV_CROPS.items()} | {"oob": [w - 4, 0, 8, 2]},
+                                        status=statuses)
+            print(src, len(arrs), "planes", sum(1 for v in statuses.values() if v), "errors", flush=True)
     if "anim" in sections:
         os.makedirs(os.path.join(HERE, "anim"), exist_ok=True)
         builders = list(ANIM_CASES) + [(k, (lambda v=v: v)) for k, v in _manual_anims().items()]
@@ -919,6 +1008,13 @@ def main(argv):
             assert st == 0 and st2 == 0 and np.array_equal(out, out2), fn
             manifest["bench"][fn]["sha256"][key] = sha(out)
             print(fn, key, flush=True)
+    if "bench_yuva" in sections:  # MODE_YUVA's A plane of the c3a frames (the Y / U / V are the planes')
+        for fn in sorted(k for k in manifest["bench"] if k.startswith("c3a_4k_s")):
+            data = open(os.path.join(HERE, "bench", fn), "rb").read()
+            st, out = decode_yuva(data, 12)
+            assert st == 0 and all(sha(out[k]) == manifest["bench"][fn]["sha256"][k] for k in "yuv"), fn
+            manifest["bench"][fn]["sha256"]["a"] = sha(out["a"])
+            print(fn, "yuva a", flush=True)
     if "bench_anim" in sections:
         manifest["bench_anim"] = {}
         for name, H, W, n, seed in BENCH_ANIM:

@@ -29,6 +29,8 @@ def oracle():
         L.oracle_vp8_reconstruct.argtypes = [P, P, P, P, P]
         L.oracle_yuv_to_rgba_fancy.argtypes = [P, C.c_int, P, P, C.c_int, P, C.c_int, C.c_int, C.c_int]
         L.oracle_yuv_to_rgba_point.argtypes = [P, C.c_int, P, P, C.c_int, P, C.c_int, C.c_int, C.c_int]
+        L.oracle_rgba_to_yuva.argtypes = [P, C.c_int, C.c_int, C.c_int, P, C.c_int, P, P, C.c_int, P, C.c_int,
+                                          C.c_int]
         L.oracle_transform_block.argtypes = [P, P, C.c_int]
         L.oracle_transform_block.restype = None
         L.oracle_vp8l_decode.argtypes = [P, P, P, P]
@@ -226,6 +228,78 @@ def load_anim(name):
 
 
 MODE_BPP = {0: 3, 1: 4, 2: 3, 3: 4, 4: 4, 5: 2, 6: 2, 7: 4, 8: 4, 9: 4, 10: 2}
+
+
+# ----------------------------------------------------------------------------- YUV output modes
+def yuv_sources():
+    return sorted(manifest().get("yuv", {}))
+
+
+def load_yuv(src):
+    ent = manifest()["yuv"][src]
+    data = open(os.path.join(GOLDEN, ent["source"]), "rb").read()
+    return data, dict(np.load(os.path.join(GOLDEN, "yuv", src + ".npz"))), ent
+
+
+def parse_yuv_key(key):
+    """'m{mode}_{crop}_f{flip}' -> (mode, crop name, flip)."""
+    m, crop, fl = key.split("_")
+    return int(m[1:]), crop, int(fl[1:])
+
+
+def yuv_window(data, crop):
+    """The output window WebPDecode uses for a crop (None = the frame): (x, y, w, h), or None when
+    libwebp reports INVALID_PARAM.  Lossy origins snap to even (WebPIoInitFromOptions with a YUV
+    source), lossless keep theirs; the buffer check uses the snapped origin either way."""
+    import webp_amd
+
+    f = webp_amd.features(data)
+    W, H = f.width, f.height
+    if crop is None:
+        return 0, 0, W, H
+    cw, ch = crop[2], crop[3]
+    x, y = (crop[0], crop[1]) if f.format == 2 else (crop[0] & ~1, crop[1] & ~1)
+    ok = lambda a, b: a >= 0 and b >= 0 and cw > 0 and ch > 0 and a + cw <= W and b + ch <= H  # noqa: E731
+    return (x, y, cw, ch) if ok(crop[0] & ~1, crop[1] & ~1) and ok(x, y) else None
+
+
+def oracle_yuva(data, mode, crop=None, flip=0):
+    """CPU WebPDecode in MODE_YUV (11) / MODE_YUVA (12) from the oracles -> {"y", "u", "v"[, "a"]},
+    or None for an invalid crop.  Lossy: the reconstructed planes' window (EmitYUV, io_dec.c.go:36-50),
+    A = the ALPH oracle's plane or 0xff (EmitAlphaYUV :128-150).  Lossless: the RGBA window through
+    oracle_rgba_to_yuva (WebPImportYUVAFromRGBA, dsp/yuv.go:304-385)."""
+    import webp_amd
+
+    win = yuv_window(data, crop)
+    if win is None:
+        return None
+    x, y, w, h = win
+    uw, uh = (w + 1) // 2, (h + 1) // 2
+    f = webp_amd.features(data)
+    if f.format == 2:
+        info, coded, tdata = webp_amd.vp8l_parse(data)
+        rgba = np.ascontiguousarray(oracle_vp8l_decode(info, coded, tdata)[y:y + h, x:x + w])
+        out = {"y": np.empty((h, w), np.uint8), "u": np.empty((uh, uw), np.uint8), "v": np.empty((uh, uw), np.uint8)}
+        a = np.empty((h, w), np.uint8) if mode == 12 else None
+        assert oracle().oracle_rgba_to_yuva(rgba.ctypes.data, w, h, 4 * w, out["y"].ctypes.data, w,
+                                            out["u"].ctypes.data, out["v"].ctypes.data, uw,
+                                            a.ctypes.data if a is not None else None, w, flip) == 0
+        if a is not None:
+            out["a"] = a
+        return out
+    info, mbs = webp_amd.vp8_parse(data)
+    planes = oracle_decode(info, mbs)
+    fl = (lambda p: p[::-1]) if flip else (lambda p: p)  # noqa: E731
+    out = {"y": fl(planes["y"][y:y + h, x:x + w]), "u": fl(planes["u"][y // 2:y // 2 + uh, x // 2:x // 2 + uw]),
+           "v": fl(planes["v"][y // 2:y // 2 + uh, x // 2:x // 2 + uw])}
+    if mode == 12:
+        try:
+            out["a"] = fl(oracle_alpha_plane(data)[1][y:y + h, x:x + w])
+        except webp_amd.WebPError as e:
+            if e.status != webp_amd.Status.UNSUPPORTED_FEATURE:
+                raise
+            out["a"] = np.full((h, w), 255, np.uint8)
+    return {k: np.ascontiguousarray(v) for k, v in out.items()}
 
 
 def oracle_output(data, mode=1, crop=None, flip=0, no_fancy=0, bypass=0):
