@@ -46,6 +46,12 @@ WORKLOADS = {
     "c3a": dict(prefix="c3a_4k", name="c3a_4k_alpha_x256", target="alpha_kernel",
                 desc="3840x2160 VP8-lossy + ALPH (lossless-compressed feathered cut-out alpha), deblock on, batch 256: "
                      "K1 + the alpha streams' K7 / K3 + K4 (SURVEY 8 f2)"),
+    "c3ag": dict(prefix="c3ag_4k", name="c3ag_4k_alpha_gradient_x256", target="alpha_kernel",
+                 desc="C3a's frames with the ALPH filter set to gradient (libwebp's GradientUnfilter: a 2-D "
+                      "wavefront), batch 256: K1 + the alpha streams' K7 / K3 + K4 (SURVEY 8 f2)"),
+    "c3av": dict(prefix="c3av_4k", name="c3av_4k_alpha_vertical_x256", target="alpha_kernel",
+                 desc="C3a's frames with the ALPH filter set to vertical (column running sums), batch 256: "
+                      "K1 + the alpha streams' K7 / K3 + K4 (SURVEY 8 f2)"),
     "c3rgb565": dict(prefix="c3_4k", name="c3_4k_rgb565_x256", target="vp8_recon_filter_kernel", colorspace=6,
                      desc="C3's frames decoded to MODE_RGB_565 (fancy upsampling), batch 256: K1, whose tail writes "
                           "the 565 pixels directly (no RGBA copy, no K6) (SURVEY 8 f4)"),

@@ -235,6 +235,7 @@ struct wg_batch {
   LLDesc* d_lldesc = nullptr;
   AlphaDesc* d_adesc = nullptr;
   int n_lossy = 0, n_lossless = 0, n_alpha = 0, n_k3 = 0, n_k6 = 0;  // n_k6: frames K6 converts
+  int n_alpha_2d = 0;  // alpha planes with filter vertical / gradient (K4's second instantiation)
   bool tail_modes = true, no_tail = false;  // no_tail: frames emitted directly in a mode K1's tail lacks
   int n_tok_w64 = 0;                         // K7 streams on its 64-mask-word instantiation (first in tokdesc)
   bool k2_modes = false;                     // K2 writes some frame in a non-RGBA colorspace (FrameDesc::emit)
@@ -762,6 +763,7 @@ void batch_layout(wg_batch* b, wg::StagingArena& arena, int32_t* status) {
       // K4 reads the filtered alpha (raw bytes, or K3's RGBA of the alpha stream) and
       // rewrites the RGBA A bytes (dword read-modify-write)
       b->n_alpha++;
+      if (f.ah.filter >= 2) b->n_alpha_2d++;
       if (f.ah.method == 1) {
         b->n_k3++;  // (K7 resolves every lossless stream)
         // libwebp's 8-bit alpha streams (a color map and nothing else, or no transform) under
@@ -1323,7 +1325,7 @@ int wg_batch_run(wg_batch* b, void* stream) {
         if (!b->lldesc.empty()) e = wg::launch_vp8l_transforms(b->d_lldesc, b->ll_groups, b->d_err, s);
         break;
       case kStageK4:  // after K3 (alpha streams) and K2 / K1's tail (A = 255), or alpha-first before them
-        if (b->n_alpha > 0) e = wg::launch_alpha(b->d_adesc, b->n_alpha, s);
+        if (b->n_alpha > 0) e = wg::launch_alpha(b->d_adesc, b->n_alpha, s, b->n_alpha_2d);
         break;
       case kStageK6:  // the output colorspace / flip over every frame's final RGBA (YUV output: K8)
         if (b->yuv) e = wg::launch_emit_yuva(b->d_ydesc, b->n, b->yuv_max_uw, b->yuv_max_uh, s);

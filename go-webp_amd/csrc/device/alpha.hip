@@ -14,18 +14,18 @@
 // After K2 / K1's tail (which wrote A = 255).  Filters none and horizontal -- what libwebp's
 // encoder picks for most planes -- go straight from the filtered bytes to the A bytes, rows in
 // parallel (alpha_rows_direct): out[y][x] = c[y-1] + sum_{i<=x} in[y][i] with c the column-0
-// prefix sums (one block scan), then a wave scan per row.  Vertical and gradient keep one
-// 1024-thread workgroup per plane and a scratch plane:
-//   1. gather the filtered bytes into `plane` (green extraction or a copy);
-//   2. unfilter in place:
-//        vertical    row 0 as horizontal, then out[y][x] = out[y-1][x] + in[y][x]
-//                    -> a running sum per column (threads across columns);
-//        gradient    row 0 as horizontal, then out = in + clip(L + T - TL): a wavefront
-//                    over 1024-row bands (thread = row, one column per step, T from the
-//                    thread above via DPP / LDS, the band's top row from LDS);
+// prefix sums (one block scan), then a wave scan per row.  Vertical and gradient run one
+// 1024-thread workgroup per plane, reading the filtered bytes straight from their source (K3's
+// green, the raw payload) and writing the unfiltered plane (round 6; no gather pass):
+//   1. row 0 as horizontal (one wave scan);
+//   2. vertical    out[y][x] = out[y-1][x] + in[y][x]: a running sum per column, four columns per
+//                  thread as one dword (bytewise adds without carries), rows loaded 8 ahead;
+//      gradient    out = in + clip(L + T - TL): a wavefront in 64-row bands, one band per wave at
+//                  a time (lane = row, one column per step, T from the lane above by DPP, the top
+//                  row of the band from the plane behind the band above's LDS progress counter --
+//                  no workgroup barrier per step), bands b = w, w + 16, ... on wave w;
 //   3. write the plane (its output window when cropping) into the A bytes (dword
-//      read-modify-write, coalesced).
-// The gradient wavefront is latency-bound (one barrier per column step) and is the slow case.
+//      read-modify-write, coalesced) -- or leave it there (alpha-first).
 //
 // Alpha-first batches (AlphaDesc::to_plane; capi.cpp decides): K4 runs before K1 and leaves the
 // unfiltered plane in `plane` (width-byte rows, the whole plane: no crop window) for the YUV -> RGBA
@@ -42,6 +42,7 @@
 namespace wg {
 namespace {
 
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 constexpr int kThreads = 1024;
 constexpr int kWaves = kThreads / 64;
 constexpr int kMaxDim = 16384;
@@ -75,20 +76,6 @@ __device__ __forceinline__ int block_excl_scan(int v, int* wsum, int* tot) {
   }
   __syncthreads();
   return wsum[wave] + inc - v;
-}
-
-// One row as HorizontalUnfilter_C with `pred` for its first byte, by wave `wave` (all
-// lanes of that wave call it): 64-byte chunks, wave scan + running carry.
-__device__ __forceinline__ void scan_row(uint8_t* row, int W, uint32_t pred) {
-  const int lane = threadIdx.x & 63;
-  uint32_t carry = pred;
-  for (int x0 = 0; x0 < W; x0 += 64) {
-    const int x = x0 + lane;
-    const int v = x < W ? row[x] : 0;
-    const int inc = wave_incl_scan(v);
-    if (x < W) row[x] = (uint8_t)(carry + (uint32_t)inc);
-    carry += (uint32_t)lane63(inc);
-  }
 }
 
 __device__ __forceinline__ uint32_t shr1(uint32_t old, uint32_t v) {  // lane i <- lane i-1; lane 0 <- old
@@ -251,127 +238,215 @@ __device__ void alpha_rows_direct(const AlphaDesc& F, int part, int parts, uint8
   }
 }
 
+// kWave = false: planes with filter none / horizontal (alpha_rows_direct, `parts` workgroups each);
+// true: vertical / gradient (one workgroup per plane).  Two instantiations, so the direct path keeps
+// its own registers and code, and only the second holds the gradient's LDS ring.
+template <bool kWave>
 __global__ void __launch_bounds__(kThreads) alpha_kernel(const AlphaDesc* __restrict__ frames) {
-  __shared__ uint8_t rowbuf[kMaxDim];  // horizontal: column-0 prefix; gradient: the band's top row
   __shared__ int wsum[kWaves];
   __shared__ int total;
-  __shared__ uint32_t edge[2][kWaves];  // gradient: each wave's lane-63 output of the last step
   __shared__ uint8_t palg[256];         // an 8-bit alpha stream's palette (green bytes)
   const AlphaDesc& F = frames[blockIdx.x];
-  if (!F.valid) return;
-  if (F.filter <= 1) {
+  if (!F.valid || (F.filter >= 2) != kWave) return;
+  if constexpr (!kWave) {
+    __shared__ uint8_t rowbuf[kMaxDim];  // horizontal: column-0 prefix
     alpha_rows_direct(F, blockIdx.y, gridDim.y, rowbuf, palg, wsum, &total);
     return;
-  }
-  if (blockIdx.y > 0) return;  // (vertical / gradient: the whole plane in one workgroup)
+  } else {
+  __shared__ uint32_t gprog[kWaves];    // gradient: each band's last row's columns done (tag: band << 16)
+  // gradient: per wave, its band's outputs (a 32-column ring per row) on their way to 16-byte stores
+  __shared__ __attribute__((aligned(16))) uint8_t ring[kWaves][64][32];
   const int W = F.width, H = F.height, tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
-  const size_t n = (size_t)W * H;
-  uint8_t* plane = F.plane;
+  const gptr<uint8_t> plane = as_global(F.plane);
+  if (F.coded && F.pal) {  // (an 8-bit stream's palette: only with filters none / horizontal in practice)
+    if (tid < (1 << (8 >> F.cbits))) palg[tid] = (uint8_t)(F.pal[tid] >> 8);
+  }
+  if (tid < kWaves) gprog[tid] = 0;
+  __syncthreads();
+  const bool gvec = F.green && (reinterpret_cast<uintptr_t>(F.green) & 15) == 0 && (W & 3) == 0;
 
-  // ---- 1. filtered bytes into the plane (4 px per thread step)
-  if (F.green) {
-    const uint32_t* g = reinterpret_cast<const uint32_t*>(F.green);
-    uint32_t* p4 = reinterpret_cast<uint32_t*>(plane);
-    const size_t n4 = n / 4;
-    for (size_t i = tid; i < n4; i += kThreads) {
-      const uint32_t a = g[4 * i], b = g[4 * i + 1], c = g[4 * i + 2], d = g[4 * i + 3];
-      p4[i] = ((a >> 8) & 0xff) | (b & 0xff00) | ((c << 8) & 0xff0000) | ((d << 16) & 0xff000000u);
+  // ---- 1. row 0: HorizontalUnfilter_C with no row above (filters.go:130-140)
+  if (wave == 0) {
+    uint32_t carry = 0;
+    for (int x0 = 0; x0 < W; x0 += 64) {
+      const int x = x0 + lane;
+      const int v = x < W ? (int)src_byte(F, palg, 0, x) : 0;
+      const int inc = wave_incl_scan(v);
+      if (x < W) plane[x] = (uint8_t)(carry + (uint32_t)inc);
+      carry += (uint32_t)lane63(inc);
     }
-    for (size_t i = n4 * 4 + tid; i < n; i += kThreads) plane[i] = (uint8_t)(g[i] >> 8);
-  } else {
-    const uint32_t* r4 = reinterpret_cast<const uint32_t*>(F.raw);
-    uint32_t* p4 = reinterpret_cast<uint32_t*>(plane);
-    const size_t n4 = (reinterpret_cast<uintptr_t>(F.raw) & 3) ? 0 : n / 4;
-    for (size_t i = tid; i < n4; i += kThreads) p4[i] = r4[i];
-    for (size_t i = n4 * 4 + tid; i < n; i += kThreads) plane[i] = F.raw[i];
   }
   __syncthreads();
 
-  // ---- 2. unfilter in place
-  if (F.filter == 1) {  // horizontal
-    // column-0 prefix sums c[y] (mod 256) into rowbuf
-    const int per = (H + kThreads - 1) / kThreads, y0 = tid * per, y1 = min(H, y0 + per);
-    int s = 0;
-    for (int y = y0; y < y1; ++y) s += plane[(size_t)y * W];
-    int run = block_excl_scan(s, wsum, &total);
-    for (int y = y0; y < y1; ++y) {
-      run += plane[(size_t)y * W];
-      rowbuf[y] = (uint8_t)run;
-    }
-    __syncthreads();
-    for (int y = wave; y < H; y += kWaves) scan_row(plane + (size_t)y * W, W, y == 0 ? 0u : rowbuf[y - 1]);
-  } else if (F.filter == 2) {  // vertical
-    if (wave == 0) scan_row(plane, W, 0u);
-    __syncthreads();
-    for (int x = tid; x < W; x += kThreads) {
-      uint32_t acc = plane[x];
-      int y = 1;
-      for (; y + 8 <= H; y += 8) {  // eight rows of loads in flight per step
-        uint8_t v[8];
+  // ---- 2. rows 1 .. H-1
+  if (F.filter == 2) {  // VerticalUnfilter_C (filters.go:146-155): a running sum per column
+    const bool dw = (W & 3) == 0;  // (dword rows: four columns per thread)
+    const int cols = dw ? W >> 2 : W;
+    for (int c = tid; c < cols; c += kThreads) {
+      if (dw) {
+        const int x = 4 * c;
+        uint32_t acc = *reinterpret_cast<gptr<const uint32_t>>(plane + x);
+        int y = 1;
+        // bytewise a + b mod 256 per byte (no carry between the four columns)
+        auto badd = [](uint32_t a, uint32_t b) {
+          return ((a & 0x7f7f7f7fu) + (b & 0x7f7f7f7fu)) ^ ((a ^ b) & 0x80808080u);
+        };
+        for (; y + 8 <= H; y += 8) {  // eight rows of loads in flight
+          uint32_t v[8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] = plane[(size_t)(y + k) * W + x];
+          for (int k = 0; k < 8; ++k) v[k] = src_quad(F, palg, y + k, x, gvec);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          acc += v[k];
-          plane[(size_t)(y + k) * W + x] = (uint8_t)acc;
+          for (int k = 0; k < 8; ++k) {
+            acc = badd(acc, v[k]);
+            *reinterpret_cast<gptr<uint32_t>>(plane + (size_t)(y + k) * W + x) = acc;
+          }
+        }
+        for (; y < H; ++y) {
+          acc = badd(acc, src_quad(F, palg, y, x, gvec));
+          *reinterpret_cast<gptr<uint32_t>>(plane + (size_t)y * W + x) = acc;
+        }
+      } else {
+        uint32_t acc = plane[c];
+        for (int y = 1; y < H; ++y) {
+          acc += src_byte(F, palg, y, c);
+          plane[(size_t)y * W + c] = (uint8_t)acc;
         }
       }
-      for (; y < H; ++y) {
-        acc += plane[(size_t)y * W + x];
-        plane[(size_t)y * W + x] = (uint8_t)acc;
-      }
     }
-  } else if (F.filter == 3) {  // gradient
-    if (wave == 0) scan_row(plane, W, 0u);
-    __syncthreads();
-    for (int x = tid; x < W; x += kThreads) rowbuf[x] = plane[x];
-    __syncthreads();
-    for (int yb = 1; yb < H; yb += kThreads) {
-      const int rows = min(kThreads, H - yb);
-      const int y = yb + tid;
-      const bool row_ok = tid < rows;
-      uint8_t* prow = plane + (size_t)min(y, H - 1) * W;
-      // inputs eight steps ahead (a shift register of loaded bytes)
-      constexpr int kAhead = 8;
-      uint32_t q[kAhead];
+  } else if (F.filter == 3) {  // GradientUnfilter_C (filters.go:157-171)
+    // Band b = rows [1 + 64 b, 1 + 64 b + 64): lane l owns row y = 1 + 64 b + l and at step s
+    // works on column x = s - l.  T = out[y-1][x] is what the lane above produced at step s - 1
+    // (DPP row shift); lane 0's comes from the band above's last row, read back from the plane in
+    // chunks of 64 columns (one per lane, then v_readlane per step) once that band's progress
+    // counter covers them; TL = the previous step's T; L = the lane's previous output.  The
+    // leftmost column predicts from above (L = TL = T).
+    // Memory: a lane's filtered bytes arrive 16 steps at a time (K3's green: four 16-byte loads of
+    // its row, a group ahead), and its outputs go into its row of the wave's LDS ring (32 columns),
+    // from which each group stores the one 16-column block of the row that has become complete --
+    // 16-byte stores instead of a byte store per lane and step (64 rows touched per instruction).
+    // Every 64 steps the band publishes how many columns of its last row are in the plane
+    // (gprog[b & 15], tag b << 16: a later band's value on the same slot implies this one is done).
+    const int nb = (H - 1 + 63) / 64;
+    const bool gq = F.green != nullptr;  // (else the raw payload: byte loads)
+    const __amdgpu_buffer_rsrc_t gsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t*>(gq ? F.green : F.raw), 0, gq ? 4 * W * H : W * H, 0x00020000);
+    const bool st16 = (W & 15) == 0 && (reinterpret_cast<uintptr_t>(F.plane) & 15) == 0;
+    uint8_t* myring = &ring[wave][lane][0];
+    for (int bnd = wave; bnd < nb; bnd += kWaves) {
+      const int y0 = 1 + 64 * bnd, rows = min(64, H - y0);
+      const int y = y0 + min(lane, rows - 1);
+      const bool row_ok = lane < rows;
+      // (global address space: flat accesses would make every LDS-ring access wait for them too)
+      const gptr<const uint8_t> above = plane + (size_t)(y0 - 1) * W;
+      const gptr<uint8_t> prow = as_global(plane) + (size_t)y * W;
+      uint32_t L = 0, T = 0, TL = 0;
+      uint32_t t0 = 0;  // lane j: column 64 c + j of the row above (the current chunk)
+      int stored = 0;   // columns [0, stored) of the lane's row are in the plane
+      // the 16 filtered bytes of steps sg .. sg + 15 (columns sg - lane ..): K3's 16 pixels as loaded
+      // (green = byte 1; unpacked where used, so the loads stay in flight a group ahead), or the raw
+      // payload's bytes in the .y lanes
+      auto load_group = [&](int sg, u32x4 q[4]) {
+        // (columns before the row's start, x0 < 0 -- possible only for W < 64 -- and rows past the
+        // band read 0 through the buffer range: their values are never used)
+        const int e = y * W + (sg - lane);
+        const uint32_t off = row_ok && e >= 0 ? (uint32_t)e : 0x20000000u;
+        if (gq) {
 #pragma unroll
-      for (int k = 0; k < kAhead; ++k) {
-        const int x = k - tid;
-        q[k] = (row_ok && x >= 0 && x < W) ? prow[x] : 0u;
-      }
-      uint32_t L = 0, TL = 0;
+          for (int j = 0; j < 4; ++j) q[j] = __builtin_amdgcn_raw_buffer_load_b128(gsrc, (int)(4 * off + 16 * j), 0, 0);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) q[j][k] = __builtin_amdgcn_raw_buffer_load_b8(gsrc, (int)(off + 4 * j + k), 0, 0) << 8;
+        }
+      };
+      // store the lane's complete 16-column blocks below `upto` (exclusive) from the ring: during
+      // the band at most one per group (the lane's columns advance 16 per group), a fixed number of
+      // vector-memory operations -- a store loop of varying trip count would make the compiler wait
+      // for vmcnt(0), i.e. for the group loads just issued, at the next group
+      auto flush_one = [&](int upto) {
+        if (row_ok && stored + 16 <= upto) {
+          const uint4 v = *reinterpret_cast<const uint4*>(myring + (stored & 31));
+          if (st16) {
+            *reinterpret_cast<gptr<u32x4>>(prow + stored) = u32x4{v.x, v.y, v.z, v.w};
+          } else {
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int k = 0; k < 16; ++k) prow[stored + k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+          }
+          stored += 16;
+        }
+      };
+      auto flush_rest = [&] {  // (the row's remaining columns, after the band's last group)
+        for (int m = stored; row_ok && m < W; ++m) prow[m] = myring[m & 31];
+        stored = W;
+      };
+      u32x4 qa[4], qb[4];
       const int steps = W + rows - 1;
-      for (int s = 0; s < steps; ++s) {
-        const int x = s - tid;
-        const bool ok = row_ok && x >= 0 && x < W;
-        // T = out[y-1][x]: the thread above's output of step s-1 (DPP within the wave;
-        // across waves through `edge`; the band's top row from rowbuf)
-        uint32_t up = 0;
-        if (wave > 0) up = edge[(s + 1) & 1][wave - 1];
-        else if (s < W) up = rowbuf[s];
-        uint32_t T = shr1(up, L) & 0xff;
-        const uint32_t v = q[0];
+      load_group(0, qa);
+      for (int s0 = 0; s0 < steps; s0 += 64) {
+        if (s0 < W) {  // the next 64 columns of the row above: wait for the band above, load
+          if (bnd > 0) {
+            const uint32_t need = ((uint32_t)(bnd - 1) << 16) | (uint32_t)min(W, s0 + 64);
+            uint32_t* pg = gprog + ((bnd - 1) & (kWaves - 1));
+            if (__hip_atomic_load(pg, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
+              const uint64_t t_0 = __builtin_amdgcn_s_memrealtime();
+              while (__hip_atomic_load(pg, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
+                __builtin_amdgcn_s_sleep(2);
+                if (__builtin_amdgcn_s_memrealtime() - t_0 > 200000000ull) break;  // (2 s: never reached)
+              }
+            }
+          }
+          t0 = above[min(s0 + lane, W - 1)];  // (unconditional: see run_group)
+        }
+        const int s1 = min(steps, s0 + 64);
+        // (straight-line code: no break at the band's end and no test on s < W -- steps past the
+        // band's end have x >= W on every row (no output) and lane 0's T past the row's end feeds
+        // nothing; a branch around each v_readlane of t0 made the waitcnt pass wait vmcnt(0) before
+        // every one of them, i.e. for the group loads in flight)
+        auto run_group = [&](int sg, const u32x4 q[4]) {
 #pragma unroll
-        for (int k = 0; k + 1 < kAhead; ++k) q[k] = q[k + 1];
-        {
-          const int xa = x + kAhead;
-          q[kAhead - 1] = (row_ok && xa >= 0 && xa < W) ? prow[xa] : 0u;
+          for (int k = 0; k < 16; ++k) {
+            const int s = sg + k;
+            const int x = s - lane;
+            const bool ok = row_ok && x >= 0 && x < W;
+            const uint32_t up = (uint32_t)__builtin_amdgcn_readlane((int)t0, (s - s0) & 63);
+            T = shr1(up, L) & 0xffu;
+            const uint32_t l = x == 0 ? T : L, tl = x == 0 ? T : TL;
+            const int g = (int)l + (int)T - (int)tl;
+            const uint32_t o = (((q[k >> 2][k & 3] >> 8) & 0xffu) + (uint32_t)min(max(g, 0), 255)) & 0xffu;
+            if (ok) {
+              myring[x & 31] = (uint8_t)o;
+              L = o;
+            }
+            TL = T;
+          }
+        };
+        for (int sg = s0; sg < s1; sg += 32) {
+          load_group(sg + 16, qb);
+          run_group(sg, qa);
+          flush_one(min(W, max(0, sg + 16 - lane)));
+          if (sg + 16 >= s1) {
+            for (int j = 0; j < 4; ++j) qa[j] = qb[j];
+            break;
+          }
+          load_group(sg + 32, qa);
+          run_group(sg + 16, qb);
+          flush_one(min(W, max(0, sg + 32 - lane)));
         }
-        uint32_t l = L, tl = TL;
-        if (x == 0) l = tl = T;  // leftmost: predicted from above
-        const int g = (int)l + (int)T - (int)tl;
-        const uint32_t o = (v + (uint32_t)min(max(g, 0), 255)) & 0xff;
-        if (ok) {
-          prow[x] = (uint8_t)o;
-          L = o;
-          if (tid == rows - 1) rowbuf[x] = (uint8_t)o;  // the next band's top row
-        }
-        TL = T;
-        if (lane == 63) edge[s & 1][wave] = L;
-        __syncthreads();
+        // the band's last row: columns [0, stored) are in the plane (release: the stores before the
+        // counter); lane rows - 1 has the fewest
+        const uint32_t done = (uint32_t)__builtin_amdgcn_readlane(stored, rows - 1);
+        if (lane == 0)
+          __hip_atomic_store(gprog + (bnd & (kWaves - 1)), ((uint32_t)bnd << 16) | done, __ATOMIC_RELEASE,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
       }
-      __syncthreads();
+      flush_rest();
+      const uint32_t done = (uint32_t)__builtin_amdgcn_readlane(stored, rows - 1);
+      if (lane == 0)
+        __hip_atomic_store(gprog + (bnd & (kWaves - 1)), ((uint32_t)bnd << 16) | done, __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_WORKGROUP);
     }
   }
   __syncthreads();
@@ -380,19 +455,26 @@ __global__ void __launch_bounds__(kThreads) alpha_kernel(const AlphaDesc* __rest
   if (F.to_plane) return;  // (alpha-first: the strips read the plane)
   for (int y = wave; y < F.win_h; y += kWaves) {
     uint32_t* dst = reinterpret_cast<uint32_t*>(F.rgba + (size_t)y * F.rgba_stride);
-    const uint8_t* src = plane + (size_t)(y + F.win_y) * W + F.win_x;
+    const gptr<const uint8_t> src = plane + (size_t)(y + F.win_y) * W + F.win_x;
     for (int x = lane; x < F.win_w; x += 64) dst[x] = (dst[x] & 0x00ffffffu) | ((uint32_t)src[x] << 24);
   }
+  }  // (kWave)
 }
 
 }  // namespace
 
-hipError_t launch_alpha(const AlphaDesc* d_frames, int n_frames, hipStream_t stream) {
+hipError_t launch_alpha(const AlphaDesc* d_frames, int n_frames, hipStream_t stream, int n_wave) {
   if (n_frames <= 0) return hipSuccess;
   // filters none / horizontal run rows on `parts` workgroups per plane (the chip holds two
-  // 1024-thread workgroups per CU); vertical / gradient planes use the first only
-  const int parts = std::max(1, std::min(8, 512 / n_frames));
-  hipLaunchKernelGGL(alpha_kernel, dim3(n_frames, parts), dim3(kThreads), 0, stream, d_frames);
+  // 1024-thread workgroups per CU); vertical / gradient planes one workgroup each, in a second
+  // launch over the same descriptors (each instantiation skips the other's planes)
+  if (n_wave < n_frames) {
+    const int parts = std::max(1, std::min(8, 512 / n_frames));
+    hipLaunchKernelGGL(alpha_kernel<false>, dim3(n_frames, parts), dim3(kThreads), 0, stream, d_frames);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  if (n_wave > 0) hipLaunchKernelGGL(alpha_kernel<true>, dim3(n_frames, 1), dim3(kThreads), 0, stream, d_frames);
   return hipGetLastError();
 }
 

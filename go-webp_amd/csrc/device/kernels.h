@@ -43,7 +43,8 @@ hipError_t launch_vp8l_resolve(const LLTokDesc* d_descs, const LLTokDesc* single
 
 // K4: ALPH planes (unfilter) -> A bytes of the RGBA output, one 1024-thread workgroup per
 // plane; runs after K2 and K3.
-hipError_t launch_alpha(const AlphaDesc* d_frames, int n_frames, hipStream_t stream);
+// n_wave: planes with filter vertical / gradient (a second kernel instantiation, one workgroup each).
+hipError_t launch_alpha(const AlphaDesc* d_frames, int n_frames, hipStream_t stream, int n_wave);
 
 // K6: output colorspace / cropping window / flip, RGBA -> WEBP_CSP_MODE (0..10) bytes.
 hipError_t launch_emit(const EmitDesc* d_frames, int n_frames, int max_pixels, hipStream_t stream);

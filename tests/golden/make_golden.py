@@ -860,14 +860,14 @@ def main(argv):
     """argv: sections to (re)generate among lossy, lossy_extra, lossless, alpha, modes, anim, bench (default: all);
     the manifest entries of the other sections are kept."""
     sections = set(argv) or {"lossy", "lossy_extra", "lossless", "alpha", "modes", "yuv", "anim", "bench", "bench_c5x",
-                             "bench_c3s", "bench_c3a", "bench_anim", "bench_modes", "fuzz", "alpha_r5", "bench_yuva"}
+                             "bench_c3s", "bench_c3a", "bench_anim", "bench_modes", "fuzz", "alpha_r5", "bench_yuva", "bench_c3ag"}
     os.makedirs(os.path.join(HERE, "lossy"), exist_ok=True)
     os.makedirs(os.path.join(HERE, "lossless"), exist_ok=True)
     os.makedirs(os.path.join(HERE, "bench"), exist_ok=True)
     mpath = os.path.join(HERE, "manifest.json")
     manifest = json.load(open(mpath)) if os.path.exists(mpath) else {}
     manifest["libwebp"] = "1.6.0 (Pillow 12.2.0 bundle, plain-C DSP)"
-    for sec in sections - {"bench_c5x", "bench_c3s", "bench_c3a", "bench_modes", "alpha_r5", "bench_yuva"}:  # (these add)
+    for sec in sections - {"bench_c5x", "bench_c3s", "bench_c3a", "bench_modes", "alpha_r5", "bench_yuva", "bench_c3ag"}:  # (these add)
         manifest[sec] = {}
     manifest.setdefault("alpha", {})
     manifest.setdefault("bench", {})
@@ -1008,6 +1008,22 @@ def main(argv):
             assert st == 0 and st2 == 0 and np.array_equal(out, out2), fn
             manifest["bench"][fn]["sha256"][key] = sha(out)
             print(fn, key, flush=True)
+    if "bench_c3ag" in sections:  # c3a's frames with the ALPH filter bits set to gradient / vertical
+        # (libwebp's encoder picks none / horizontal for every alpha plane we tried at 4K, even with
+        # alpha_filtering = best on linear ramps: K4's wavefront unfilters get their workload this way;
+        # libwebp's decode of the edited file is the expected output, as for the a_*_g / _v fixtures)
+        for fn in sorted(k for k in manifest["bench"] if k.startswith("c3a_4k_s")):
+            src = open(os.path.join(HERE, "bench", fn), "rb").read()
+            for tag, filt in (("c3ag", 3), ("c3av", 2)):
+                data = set_alpha_filter(src, filt)
+                r = decode_all(data, lossy=True)
+                out = fn.replace("c3a_", tag + "_")
+                with open(os.path.join(HERE, "bench", out), "wb") as f:
+                    f.write(data)
+                ent = dict(manifest["bench"][fn])
+                ent.update(bytes=len(data), sha256={k: sha(v) for k, v in r.items()}, alph=alpha_header(data))
+                manifest["bench"][out] = ent
+                print(out, ent["alph"], flush=True)
     if "bench_yuva" in sections:  # MODE_YUVA's A plane of the c3a frames (the Y / U / V are the planes')
         for fn in sorted(k for k in manifest["bench"] if k.startswith("c3a_4k_s")):
             data = open(os.path.join(HERE, "bench", fn), "rb").read()

@@ -2,7 +2,8 @@
 1.6.0 (manifest "bench" / "bench_anim", made by tests/golden/make_golden.py):
 
 * c3a (f2, K4): 8 x 4K lossy + lossless-compressed ALPH frames, the bench's 256-frame layout
-  (frames cycled), RGBA SHA-256 with K1's tail and with a separate K2, and point sampling;
+  (frames cycled), RGBA SHA-256 with K1's tail and with a separate K2, and point sampling; the same
+  frames with the ALPH filter set to gradient (c3ag) and vertical (c3av);
 * c3rgb565 (f4): C3's frames decoded to MODE_RGB_565 as a resident batch -- K1's tail emits the
   565 pixels itself (no RGBA copy, no K6) -- SHA-256 of WebPDecode's bytes;
 * anim (f3, K5): the 64-frame 1920x1080 animation as a resident animation batch, every
@@ -55,6 +56,31 @@ def test_c3a_alpha_frames(ctx, mode):
         for i in range(n):
             want = m[os.path.basename(paths[i % 8])]["sha256"][key]
             assert _sha(b.rgba(i)) == want, (mode, i)
+    finally:
+        b.close()
+
+
+@pytest.mark.parametrize("prefix", ["c3ag_4k", "c3av_4k"])
+@pytest.mark.parametrize("mode", ["fused", "separate"])
+def test_c3ag_c3av_gradient_vertical_alpha(ctx, prefix, mode):
+    """c3a's frames with the ALPH filter set to gradient (c3ag) / vertical (c3av): K3 (the streams
+    now need their green), K4's wavefront / column-sum unfilters -- 16 frames (every seed twice),
+    alpha-first (K4 before K1's tail) and with a separate K2; RGBA SHA-256 = libwebp's."""
+    paths = bench_files(prefix)
+    assert len(paths) == 8
+    m = manifest()["bench"]
+    datas = [open(p, "rb").read() for p in paths]
+    n = 16
+    b = ctx.batch([datas[i % 8] for i in range(n)])
+    try:
+        assert (b.status == 0).all(), b.status
+        b.set_emit(mode == "separate")
+        for _ in range(2):
+            b.run()
+        ms = b.kernel_ms()
+        assert ms[0] > 0 and ms[2] > 0 and ms[3] > 0, ms
+        for i in range(n):
+            assert _sha(b.rgba(i)) == m[os.path.basename(paths[i % 8])]["sha256"]["rgba"], (prefix, mode, i)
     finally:
         b.close()
 
