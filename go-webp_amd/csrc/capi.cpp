@@ -181,6 +181,35 @@ struct wg_ctx {
   std::mutex side_mu;
   int chunk_frames = 0;  // frames per pipeline chunk, 0 = automatic (wg_ctx_set_chunk_frames)
   wg_pipeline_stats stats{};  // of the last pipelined decode
+  // HIP events kept for reuse (batches' stage timings, pipeline chunks): creating ~14 events per
+  // call was a fixed cost of every single-frame decode.  [0] default (spin-wait), [1] blocking-sync.
+  std::mutex ev_mu;
+  std::vector<hipEvent_t> spare_ev[2];
+  // pinned words the pipeline's chunks copy their error word into (no synchronous D2H per chunk)
+  int32_t* err_words = nullptr;
+  int n_err_words = 0;
+  hipEvent_t take_event(int blocking) {
+    {
+      std::lock_guard<std::mutex> lock(ev_mu);
+      auto& v = spare_ev[blocking ? 1 : 0];
+      if (!v.empty()) {
+        hipEvent_t e = v.back();
+        v.pop_back();
+        return e;
+      }
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreateWithFlags(&e, blocking ? hipEventBlockingSync : hipEventDefault) != hipSuccess) {
+      (void)hipGetLastError();
+      return nullptr;
+    }
+    return e;
+  }
+  void give_event(hipEvent_t e, int blocking) {
+    if (!e) return;
+    std::lock_guard<std::mutex> lock(ev_mu);
+    spare_ev[blocking ? 1 : 0].push_back(e);
+  }
   wg::WorkerPool* workers() {
     if (!pool) pool.reset(new wg::WorkerPool(host_threads));
     return pool.get();
@@ -205,18 +234,17 @@ struct Timing {
   int8_t order[kStages] = {0, 1, 2, 3, 4, 5, 6};  // launch order: ev[i] .. ev[i + 1] bracket stage order[i]
 };
 
-hipError_t timing_create(Timing& t) {
+// (events from the context's spare list, back to it when the batch goes)
+hipError_t timing_create(wg_ctx* c, Timing& t) {
   for (auto& e : t.ev)
-    if (hipError_t r = hipEventCreate(&e); r != hipSuccess) return r;
+    if (!(e = c->take_event(0))) return hipErrorOutOfMemory;
   for (auto& e : t.side)
-    if (hipError_t r = hipEventCreate(&e); r != hipSuccess) return r;
+    if (!(e = c->take_event(0))) return hipErrorOutOfMemory;
   return hipSuccess;
 }
-void timing_destroy(Timing& t) {
-  for (auto& e : t.ev)
-    if (e) hipEventDestroy(e);
-  for (auto& e : t.side)
-    if (e) hipEventDestroy(e);
+void timing_destroy(wg_ctx* c, Timing& t) {
+  for (auto& e : t.ev) c->give_event(e, 0), e = nullptr;
+  for (auto& e : t.side) c->give_event(e, 0), e = nullptr;
 }
 
 }  // namespace
@@ -511,6 +539,9 @@ void wg_ctx_destroy(wg_ctx* c) {
   c->arena.reset();
   for (auto& a : c->arena_ring) a.reset();
   c->cache.trim(0);
+  for (auto& v : c->spare_ev)
+    for (hipEvent_t e : v) hipEventDestroy(e);
+  if (c->err_words) pinned_free(c->err_words);
   if (c->stream) hipStreamDestroy(c->stream);
   for (hipStream_t w : c->work)
     if (w) hipStreamDestroy(w);
@@ -534,7 +565,7 @@ int wg_set_default_device(int device) {
 void wg_batch_destroy(wg_batch* b) {
   if (!b) return;
   if (set_device(b->ctx->device)) batch_wait(b);  // nothing may still use the buffers handed back to the cache
-  for (auto& t : b->timings) timing_destroy(t);
+  for (auto& t : b->timings) timing_destroy(b->ctx, t);
   for (auto& d : b->done) hipEventDestroy(d.second);
   DeviceCache& c = b->ctx->cache;
   c.put(b->d_desc);
@@ -768,7 +799,9 @@ void batch_layout(wg_batch* b, wg::StagingArena& arena, int32_t* status) {
         b->n_k3++;  // (K7 resolves every lossless stream)
         // libwebp's 8-bit alpha streams (a color map and nothing else, or no transform) under
         // filter none / horizontal: K4 expands the palette itself, straight from K7's output
-        f.alpha_direct = f.ah.filter <= 1 && (f.al.n_transforms == 0 ||
+        // (any filter: K4 reads the coded image itself -- rows in parallel for none / horizontal, a
+        // gather into its plane for vertical / gradient)
+        f.alpha_direct = (f.al.n_transforms == 0 ||
                                               (f.al.n_transforms == 1 && f.al.type[0] == wg::kVP8LColorIndexing));
         if (f.al.two_pass() && !f.alpha_direct) {
           f.off_ascratch = pl_b;
@@ -925,7 +958,7 @@ bool set_alpha_first(wg_batch* b) {
     const FrameParse& f = b->fp[(size_t)i];
     if (f.status != WG_STATUS_OK || f.lossless || !f.alpha) continue;
     AlphaDesc& a = b->adesc[j++];
-    a.plane = af || !f.alpha_direct ? b->d_planes + f.off_aplane : nullptr;
+    a.plane = af || !f.alpha_direct || f.ah.filter >= 2 ? b->d_planes + f.off_aplane : nullptr;
     a.to_plane = af ? 1 : 0;
     b->desc[(size_t)i].alpha_off16 = af ? (int32_t)((f.off_aplane - f.off_y) / 16) : 0;
   }
@@ -1026,7 +1059,7 @@ int batch_upload(wg_batch* b, const wg::StagingArena& arena) {
       } else {
         a.raw = b->d_in + arena.dev_offset(f.araw);
       }
-      a.plane = f.alpha_direct ? nullptr : b->d_planes + f.off_aplane;
+      a.plane = f.alpha_direct && f.ah.filter <= 1 ? nullptr : b->d_planes + f.off_aplane;
       a.rgba = d.rgba;
       a.width = f.width;
       a.height = f.height;
@@ -1236,8 +1269,8 @@ int wg_batch_run(wg_batch* b, void* stream) {
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : b->home;
   if (b->n_runs_pending >= b->timings.size()) {
     Timing t;
-    if (timing_create(t) != hipSuccess) {
-      timing_destroy(t);
+    if (timing_create(b->ctx, t) != hipSuccess) {
+      timing_destroy(b->ctx, t);
       return WG_STATUS_OUT_OF_MEMORY;
     }
     b->timings.push_back(t);
@@ -1353,9 +1386,11 @@ int wg_batch_run(wg_batch* b, void* stream) {
   return batch_mark_done(b, s) == hipSuccess ? WG_STATUS_OK : WG_STATUS_OUT_OF_MEMORY;
 }
 
-int wg_batch_kernel_ms(const wg_batch* bc, float* ms, int n_ms) {
-  wg_batch* b = const_cast<wg_batch*>(bc);
-  if (!b || !ms || n_ms < 1) return WG_STATUS_INVALID_PARAM;
+}  // extern "C"
+
+namespace {
+// wg_batch_kernel_ms; the pipeline's chunks read their error word asynchronously (err_word given)
+int batch_kernel_ms(wg_batch* b, float* ms, int n_ms, const int32_t* err_word) {
   for (int k = 0; k < n_ms; ++k) ms[k] = 0.f;
   if (b->n_runs_pending == 0) return WG_STATUS_OK;
   double acc[kStages] = {};
@@ -1376,13 +1411,24 @@ int wg_batch_kernel_ms(const wg_batch* bc, float* ms, int n_ms) {
     }
   }
   int err = 0;
-  if (hipMemcpy(&err, b->d_err, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess || err) return WG_STATUS_USER_ABORT;
+  if (err_word) err = *err_word;
+  else if (hipMemcpy(&err, b->d_err, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) err = 1;
+  if (err) return WG_STATUS_USER_ABORT;
   for (int k = 0; k < kStages; ++k) {
     const int pub = kPublicOfStage[k];
     if (pub < n_ms) ms[pub] = cnt[k] ? (float)(acc[k] / cnt[k]) : 0.f;
   }
   b->n_runs_pending = 0;
   return WG_STATUS_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int wg_batch_kernel_ms(const wg_batch* bc, float* ms, int n_ms) {
+  wg_batch* b = const_cast<wg_batch*>(bc);
+  if (!b || !ms || n_ms < 1) return WG_STATUS_INVALID_PARAM;
+  return batch_kernel_ms(b, ms, n_ms, nullptr);
 }
 
 int wg_batch_kernel_bytes(const wg_batch* b, double* bytes, int n_bytes) {
@@ -1452,8 +1498,8 @@ int wg_batch_run_emit(wg_batch* b, void* stream) {
   hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : b->home;
   if (b->n_runs_pending >= b->timings.size()) {
     Timing t;
-    if (timing_create(t) != hipSuccess) {
-      timing_destroy(t);
+    if (timing_create(b->ctx, t) != hipSuccess) {
+      timing_destroy(b->ctx, t);
       return WG_STATUS_OUT_OF_MEMORY;
     }
     b->timings.push_back(t);
@@ -1546,6 +1592,7 @@ double now_s() {
 // 2/3 around the download (3 = everything of the chunk is complete).
 struct PipeChunk {
   int a = 0, n = 0, arena = 0;
+  int32_t* err_word = nullptr;  // pinned: the chunk's error word, copied behind its download
   hipStream_t s = nullptr;
   BatchPtr b;
   hipEvent_t ev[4] = {};
@@ -1583,6 +1630,10 @@ void pipe_download(PipeChunk& c, uint8_t* const* out, const int32_t* strides, co
     }
     *bytes += 4.0 * f.out_w * f.out_h;
   }
+  if (c.err_word && hipMemcpyAsync(c.err_word, b->d_err, sizeof(int32_t), hipMemcpyDeviceToHost, c.s) != hipSuccess) {
+    (void)hipGetLastError();
+    *c.err_word = 1;  // (reported as the chunk's failure)
+  }
   hipEventRecord(c.ev[3], c.s);
 }
 
@@ -1591,7 +1642,7 @@ void pipe_finish(PipeChunk& c, int32_t* status, wg_pipeline_stats* ps) {
   if (c.ran) {
     hipEventSynchronize(c.ev[3]);
     float ms[5] = {};
-    const int st = wg_batch_kernel_ms(c.b.get(), ms, 5);  // (reads the error word)
+    const int st = batch_kernel_ms(c.b.get(), ms, 5, c.err_word);  // (checks the error word)
     for (float m : ms) ps->kernel_ms += m;
     float a = 0;
     if (hipEventElapsedTime(&a, c.ev[0], c.ev[1]) == hipSuccess) ps->h2d_ms += a;
@@ -1682,26 +1733,40 @@ int decode_pipelined(wg_ctx* ctx, const uint8_t* const* data, const size_t* size
   hipStream_t streams[2] = {K > 1 ? ctx->work[0] : ctx->stream, K > 1 ? ctx->work[1] : ctx->stream};
   std::vector<PipeChunk> ch((size_t)K);
   // the chunks' events go on every exit path, once no thread can still wait on them
+  // (blocking-sync events when a device thread waits on them beside the entropy stage's 16 threads:
+  // it sleeps instead of spinning on their CPUs; one chunk: the calling thread waits, spinning --
+  // no wake-up latency on the single-frame path)
+  const int blocking = K > 1 ? 1 : 0;
   struct EventsGuard {
     std::vector<PipeChunk>& ch;
+    wg_ctx* ctx;
+    int blocking;
     ~EventsGuard() {
       for (PipeChunk& c : ch)
-        for (hipEvent_t& e : c.ev)
-          if (e) hipEventDestroy(e), e = nullptr;
+        for (hipEvent_t& e : c.ev) ctx->give_event(e, blocking), e = nullptr;
     }
-  } events_guard{ch};
+  } events_guard{ch, ctx, blocking};
+  // one pinned error word per chunk
+  if (ctx->n_err_words < K) {
+    if (ctx->err_words) pinned_free(ctx->err_words);
+    ctx->n_err_words = 0;
+    ctx->err_words = static_cast<int32_t*>(pinned_alloc(sizeof(int32_t) * (size_t)std::max(K, 64)));
+    if (!ctx->err_words) {
+      fail_frames(status, 0, n, WG_STATUS_OUT_OF_MEMORY);
+      return WG_STATUS_OUT_OF_MEMORY;
+    }
+    ctx->n_err_words = std::max(K, 64);
+  }
   for (int k = 0; k < K; ++k) {
     PipeChunk& c = ch[(size_t)k];
     c.a = bounds[(size_t)k];
     c.n = bounds[(size_t)k + 1] - c.a;
     c.arena = k % kRing;
     c.s = streams[k & 1];
-    // (blocking-sync events: the device thread's waits sleep instead of spinning on a CPU the
-    // entropy stage's 16 threads are using)
+    c.err_word = ctx->err_words + k;
+    *c.err_word = 0;
     for (hipEvent_t& e : c.ev)
-      if (hipEventCreateWithFlags(&e, hipEventBlockingSync) != hipSuccess) {
-        (void)hipGetLastError();
-        e = nullptr;
+      if (!(e = ctx->take_event(blocking))) {
         fail_frames(status, 0, n, WG_STATUS_OUT_OF_MEMORY);
         return WG_STATUS_OUT_OF_MEMORY;
       }

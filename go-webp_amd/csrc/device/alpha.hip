@@ -266,12 +266,28 @@ __global__ void __launch_bounds__(kThreads) alpha_kernel(const AlphaDesc* __rest
   __syncthreads();
   const bool gvec = F.green && (reinterpret_cast<uintptr_t>(F.green) & 15) == 0 && (W & 3) == 0;
 
-  // ---- 1. row 0: HorizontalUnfilter_C with no row above (filters.go:130-140)
+  // ---- 1. the filtered bytes into the plane (coalesced: four per thread and step; K7's coded
+  //         image through the palette, K3's green, or the raw payload), then row 0 as
+  //         HorizontalUnfilter_C with no row above (filters.go:130-140)
+  {
+    const bool dw = (W & 3) == 0;
+    const size_t n4 = dw ? (size_t)W * H / 4 : 0;
+    const int q4 = W >> 2;
+    for (size_t i = tid; i < n4; i += kThreads) {
+      const int y = (int)(i / (size_t)q4), x = 4 * (int)(i - (size_t)y * q4);
+      *reinterpret_cast<gptr<uint32_t>>(plane + 4 * i) = src_quad(F, palg, y, x, gvec);
+    }
+    for (size_t i = n4 * 4 + tid; i < (size_t)W * H; i += kThreads) {
+      const int y = (int)(i / (size_t)W), x = (int)(i - (size_t)y * W);
+      plane[i] = (uint8_t)src_byte(F, palg, y, x);
+    }
+  }
+  __syncthreads();
   if (wave == 0) {
     uint32_t carry = 0;
     for (int x0 = 0; x0 < W; x0 += 64) {
       const int x = x0 + lane;
-      const int v = x < W ? (int)src_byte(F, palg, 0, x) : 0;
+      const int v = x < W ? (int)plane[x] : 0;
       const int inc = wave_incl_scan(v);
       if (x < W) plane[x] = (uint8_t)(carry + (uint32_t)inc);
       carry += (uint32_t)lane63(inc);
@@ -295,7 +311,7 @@ __global__ void __launch_bounds__(kThreads) alpha_kernel(const AlphaDesc* __rest
         for (; y + 8 <= H; y += 8) {  // eight rows of loads in flight
           uint32_t v[8];
 #pragma unroll
-          for (int k = 0; k < 8; ++k) v[k] = src_quad(F, palg, y + k, x, gvec);
+          for (int k = 0; k < 8; ++k) v[k] = *reinterpret_cast<gptr<const uint32_t>>(plane + (size_t)(y + k) * W + x);
 #pragma unroll
           for (int k = 0; k < 8; ++k) {
             acc = badd(acc, v[k]);
@@ -303,13 +319,13 @@ __global__ void __launch_bounds__(kThreads) alpha_kernel(const AlphaDesc* __rest
           }
         }
         for (; y < H; ++y) {
-          acc = badd(acc, src_quad(F, palg, y, x, gvec));
+          acc = badd(acc, *reinterpret_cast<gptr<const uint32_t>>(plane + (size_t)y * W + x));
           *reinterpret_cast<gptr<uint32_t>>(plane + (size_t)y * W + x) = acc;
         }
       } else {
         uint32_t acc = plane[c];
         for (int y = 1; y < H; ++y) {
-          acc += src_byte(F, palg, y, c);
+          acc += plane[(size_t)y * W + c];
           plane[(size_t)y * W + c] = (uint8_t)acc;
         }
       }
@@ -328,12 +344,15 @@ __global__ void __launch_bounds__(kThreads) alpha_kernel(const AlphaDesc* __rest
     // Every 64 steps the band publishes how many columns of its last row are in the plane
     // (gprog[b & 15], tag b << 16: a later band's value on the same slot implies this one is done).
     const int nb = (H - 1 + 63) / 64;
-    const bool gq = F.green != nullptr;  // (else the raw payload: byte loads)
-    const __amdgpu_buffer_rsrc_t gsrc = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint8_t*>(gq ? F.green : F.raw), 0, gq ? 4 * W * H : W * H, 0x00020000);
+    // (the filtered bytes are in the plane since step 1: read in place, ahead of the outputs)
+    const __amdgpu_buffer_rsrc_t psrc = __builtin_amdgcn_make_buffer_rsrc(F.plane, 0, W * H, 0x00020000);
     const bool st16 = (W & 15) == 0 && (reinterpret_cast<uintptr_t>(F.plane) & 15) == 0;
     uint8_t* myring = &ring[wave][lane][0];
+#ifdef WG_ABL_GRAD_1BAND  // (measurement only: one band per wave, output wrong)
+    for (int bnd = wave; bnd < min(nb, kWaves); bnd += kWaves) {
+#else
     for (int bnd = wave; bnd < nb; bnd += kWaves) {
+#endif
       const int y0 = 1 + 64 * bnd, rows = min(64, H - y0);
       const int y = y0 + min(lane, rows - 1);
       const bool row_ok = lane < rows;
@@ -341,25 +360,22 @@ __global__ void __launch_bounds__(kThreads) alpha_kernel(const AlphaDesc* __rest
       const gptr<const uint8_t> above = plane + (size_t)(y0 - 1) * W;
       const gptr<uint8_t> prow = as_global(plane) + (size_t)y * W;
       uint32_t L = 0, T = 0, TL = 0;
-      uint32_t t0 = 0;  // lane j: column 64 c + j of the row above (the current chunk)
       int stored = 0;   // columns [0, stored) of the lane's row are in the plane
-      // the 16 filtered bytes of steps sg .. sg + 15 (columns sg - lane ..): K3's 16 pixels as loaded
-      // (green = byte 1; unpacked where used, so the loads stay in flight a group ahead), or the raw
-      // payload's bytes in the .y lanes
-      auto load_group = [&](int sg, u32x4 q[4]) {
+      // the 16 filtered bytes of steps sg .. sg + 15 (columns sg - lane ..): the five aligned dwords
+      // around them as loaded, shifted into place (v_alignbyte) where used, so the loads stay in
+      // flight a group ahead
+      struct Grp {
+        u32x4 w;
+        uint32_t w4, sh;
+      };
+      auto load_group = [&](int sg, Grp& q) {
         // (columns before the row's start, x0 < 0 -- possible only for W < 64 -- and rows past the
         // band read 0 through the buffer range: their values are never used)
         const int e = y * W + (sg - lane);
         const uint32_t off = row_ok && e >= 0 ? (uint32_t)e : 0x20000000u;
-        if (gq) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) q[j] = __builtin_amdgcn_raw_buffer_load_b128(gsrc, (int)(4 * off + 16 * j), 0, 0);
-        } else {
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int k = 0; k < 4; ++k) q[j][k] = __builtin_amdgcn_raw_buffer_load_b8(gsrc, (int)(off + 4 * j + k), 0, 0) << 8;
-        }
+        q.w = __builtin_amdgcn_raw_buffer_load_b128(psrc, (int)(off & ~3u), 0, 0);
+        q.w4 = __builtin_amdgcn_raw_buffer_load_b32(psrc, (int)((off & ~3u) + 16), 0, 0);
+        q.sh = off & 3u;
       };
       // store the lane's complete 16-column blocks below `upto` (exclusive) from the ring: during
       // the band at most one per group (the lane's columns advance 16 per group), a fixed number of
@@ -382,65 +398,80 @@ __global__ void __launch_bounds__(kThreads) alpha_kernel(const AlphaDesc* __rest
         for (int m = stored; row_ok && m < W; ++m) prow[m] = myring[m & 31];
         stored = W;
       };
-      u32x4 qa[4], qb[4];
+      Grp qa, qb;
       const int steps = W + rows - 1;
       load_group(0, qa);
-      for (int s0 = 0; s0 < steps; s0 += 64) {
-        if (s0 < W) {  // the next 64 columns of the row above: wait for the band above, load
-          if (bnd > 0) {
-            const uint32_t need = ((uint32_t)(bnd - 1) << 16) | (uint32_t)min(W, s0 + 64);
-            uint32_t* pg = gprog + ((bnd - 1) & (kWaves - 1));
-            if (__hip_atomic_load(pg, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
-              const uint64_t t_0 = __builtin_amdgcn_s_memrealtime();
-              while (__hip_atomic_load(pg, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
-                __builtin_amdgcn_s_sleep(2);
-                if (__builtin_amdgcn_s_memrealtime() - t_0 > 200000000ull) break;  // (2 s: never reached)
-              }
-            }
+      // Groups of 16 steps.  Lane j < 16 holds column 16 g + j of the row above for group g (t0),
+      // loaded one group ahead (tn) once the band above's last row has stored 16 g + 32 columns;
+      // the band publishes its own last row's stored columns after every group.
+      auto wait_above = [&](int cols) {
+#ifdef WG_ABL_GRAD_NOWAIT  // (measurement only: output wrong)
+        return;
+#endif
+        if (bnd == 0) return;  // (row 0 is complete)
+        const uint32_t need = ((uint32_t)(bnd - 1) << 16) | (uint32_t)min(W, cols);
+        uint32_t* pg = gprog + ((bnd - 1) & (kWaves - 1));
+        if (__hip_atomic_load(pg, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
+          const uint64_t t_0 = __builtin_amdgcn_s_memrealtime();
+          while (__hip_atomic_load(pg, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
+            __builtin_amdgcn_s_sleep(1);
+            if (__builtin_amdgcn_s_memrealtime() - t_0 > 200000000ull) break;  // (2 s: never reached)
           }
-          t0 = above[min(s0 + lane, W - 1)];  // (unconditional: see run_group)
         }
-        const int s1 = min(steps, s0 + 64);
-        // (straight-line code: no break at the band's end and no test on s < W -- steps past the
-        // band's end have x >= W on every row (no output) and lane 0's T past the row's end feeds
-        // nothing; a branch around each v_readlane of t0 made the waitcnt pass wait vmcnt(0) before
-        // every one of them, i.e. for the group loads in flight)
-        auto run_group = [&](int sg, const u32x4 q[4]) {
+      };
+      // (straight-line steps: no break at the band's end and no test on s < W -- steps past the
+      // band's end have x >= W on every row (no output) and lane 0's T past the row's end feeds
+      // nothing; a branch around each v_readlane of t0 made the waitcnt pass wait vmcnt(0) before
+      // every one of them, i.e. for the group loads in flight)
+      auto run_group = [&](int sg, const Grp& q, uint32_t t0) {
+        const uint32_t b[4] = {__builtin_amdgcn_alignbyte(q.w.y, q.w.x, q.sh), __builtin_amdgcn_alignbyte(q.w.z, q.w.y, q.sh),
+                               __builtin_amdgcn_alignbyte(q.w.w, q.w.z, q.sh), __builtin_amdgcn_alignbyte(q.w4, q.w.w, q.sh)};
 #pragma unroll
-          for (int k = 0; k < 16; ++k) {
-            const int s = sg + k;
-            const int x = s - lane;
-            const bool ok = row_ok && x >= 0 && x < W;
-            const uint32_t up = (uint32_t)__builtin_amdgcn_readlane((int)t0, (s - s0) & 63);
-            T = shr1(up, L) & 0xffu;
-            const uint32_t l = x == 0 ? T : L, tl = x == 0 ? T : TL;
-            const int g = (int)l + (int)T - (int)tl;
-            const uint32_t o = (((q[k >> 2][k & 3] >> 8) & 0xffu) + (uint32_t)min(max(g, 0), 255)) & 0xffu;
-            if (ok) {
-              myring[x & 31] = (uint8_t)o;
-              L = o;
-            }
-            TL = T;
+        for (int k = 0; k < 16; ++k) {
+          const int s = sg + k;
+          const int x = s - lane;
+          const bool ok = row_ok && x >= 0 && x < W;
+          const uint32_t up = (uint32_t)__builtin_amdgcn_readlane((int)t0, k);
+          T = shr1(up, L) & 0xffu;
+          const uint32_t l = x == 0 ? T : L, tl = x == 0 ? T : TL;
+          const int g = (int)l + (int)T - (int)tl;
+          const uint32_t o = (((b[k >> 2] >> (8 * (k & 3))) & 0xffu) + (uint32_t)min(max(g, 0), 255)) & 0xffu;
+          if (ok) {
+#ifndef WG_ABL_GRAD_NOLDS  // (measurement only: output wrong)
+            myring[x & 31] = (uint8_t)o;
+#endif
+            L = o;
           }
-        };
-        for (int sg = s0; sg < s1; sg += 32) {
-          load_group(sg + 16, qb);
-          run_group(sg, qa);
-          flush_one(min(W, max(0, sg + 16 - lane)));
-          if (sg + 16 >= s1) {
-            for (int j = 0; j < 4; ++j) qa[j] = qb[j];
-            break;
-          }
-          load_group(sg + 32, qa);
-          run_group(sg + 16, qb);
-          flush_one(min(W, max(0, sg + 32 - lane)));
+          TL = T;
         }
-        // the band's last row: columns [0, stored) are in the plane (release: the stores before the
-        // counter); lane rows - 1 has the fewest
+      };
+      auto publish = [&] {  // (release: the row's plane stores before the counter; lane rows - 1 has the fewest)
         const uint32_t done = (uint32_t)__builtin_amdgcn_readlane(stored, rows - 1);
         if (lane == 0)
           __hip_atomic_store(gprog + (bnd & (kWaves - 1)), ((uint32_t)bnd << 16) | done, __ATOMIC_RELEASE,
                              __HIP_MEMORY_SCOPE_WORKGROUP);
+      };
+      wait_above(16);
+      uint32_t ta = above[min(lane & 15, W - 1)], tb = 0;
+      for (int sg = 0; sg < steps; sg += 32) {
+        // group sg (qa, ta), then group sg + 16 (qb, tb)
+        load_group(sg + 16, qb);
+        if (sg + 16 < W) {
+          wait_above(sg + 32);
+          tb = above[min(sg + 16 + (lane & 15), W - 1)];
+        }
+        run_group(sg, qa, ta);
+        flush_one(min(W, max(0, sg + 16 - lane)));
+        publish();
+        if (sg + 16 >= steps) break;
+        load_group(sg + 32, qa);
+        if (sg + 32 < W) {
+          wait_above(sg + 48);
+          ta = above[min(sg + 32 + (lane & 15), W - 1)];
+        }
+        run_group(sg + 16, qb, tb);
+        flush_one(min(W, max(0, sg + 32 - lane)));
+        publish();
       }
       flush_rest();
       const uint32_t done = (uint32_t)__builtin_amdgcn_readlane(stored, rows - 1);

@@ -63,9 +63,10 @@ def test_c3a_alpha_frames(ctx, mode):
 @pytest.mark.parametrize("prefix", ["c3ag_4k", "c3av_4k"])
 @pytest.mark.parametrize("mode", ["fused", "separate"])
 def test_c3ag_c3av_gradient_vertical_alpha(ctx, prefix, mode):
-    """c3a's frames with the ALPH filter set to gradient (c3ag) / vertical (c3av): K3 (the streams
-    now need their green), K4's wavefront / column-sum unfilters -- 16 frames (every seed twice),
-    alpha-first (K4 before K1's tail) and with a separate K2; RGBA SHA-256 = libwebp's."""
+    """c3a's frames with the ALPH filter set to gradient (c3ag) / vertical (c3av): K4 gathers the
+    8-bit streams' bytes from K7's coded image through their colour map (no K3), then its wavefront /
+    column-sum unfilters -- 16 frames (every seed twice), alpha-first (K4 before K1's tail) and with
+    a separate K2; RGBA SHA-256 = libwebp's."""
     paths = bench_files(prefix)
     assert len(paths) == 8
     m = manifest()["bench"]
@@ -78,7 +79,7 @@ def test_c3ag_c3av_gradient_vertical_alpha(ctx, prefix, mode):
         for _ in range(2):
             b.run()
         ms = b.kernel_ms()
-        assert ms[0] > 0 and ms[2] > 0 and ms[3] > 0, ms
+        assert ms[0] > 0 and ms[3] > 0 and ms[4] > 0 and ms[2] == 0, ms  # K1, K4, K7; no K3
         for i in range(n):
             assert _sha(b.rgba(i)) == m[os.path.basename(paths[i % 8])]["sha256"]["rgba"], (prefix, mode, i)
     finally:
