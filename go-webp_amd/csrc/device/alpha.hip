@@ -78,6 +78,43 @@ __device__ __forceinline__ int block_excl_scan(int v, int* wsum, int* tot) {
   return wsum[wave] + inc - v;
 }
 
+typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+// LDS byte address of a __shared__ object (M0 / ds address form)
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+// The gradient's LDS-DMA loads: 16 bytes per lane from buffer `rs` (bounds-checked: out-of-range
+// offsets read 0) at `off` into LDS at `lds` + 16 lane.  Invisible to the compiler's vmcnt
+// bookkeeping: the consumer waits with its own counted s_waitcnt.  M0 is written and restored in
+// the same statement (compiler-reserved); s_nop 4 covers a descriptor fresh from v_readfirstlane,
+// s_nop 0 the M0 write before the load.
+__device__ __forceinline__ void dma_load_b128(i32x4 rs, uint32_t off, uint32_t lds) {
+  uint32_t keep;
+  asm volatile(
+      "s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %3, 0 offen lds\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(off), "s"(lds), "s"(rs)
+      : "memory");
+}
+
+// Bytes [4 q + r, 4 q + r + 16) of the 32 in d0..d7 (zeros past them), q in 0..4, r in 0..3,
+// per-lane values: a binary mux on q's bits (18 v_cndmask), then v_alignbyte.  (Scalars, no
+// array: a select chain over an array becomes an indexed access, i.e. a private array in scratch.)
+__device__ __forceinline__ void window16(uint32_t d0, uint32_t d1, uint32_t d2, uint32_t d3, uint32_t d4, uint32_t d5,
+                                         uint32_t d6, uint32_t d7, int q, int r, uint32_t o[4]) {
+  const bool b1 = (q & 1) != 0, b2 = (q & 2) != 0, b4 = (q & 4) != 0;
+  const uint32_t e0 = b1 ? d1 : d0, e1 = b1 ? d2 : d1, e2 = b1 ? d3 : d2, e3 = b1 ? d4 : d3, e4 = b1 ? d5 : d4,
+                 e5 = b1 ? d6 : d5, e6 = b1 ? d7 : d6, e7 = b1 ? 0u : d7;
+  const uint32_t f0 = b2 ? e2 : e0, f1 = b2 ? e3 : e1, f2 = b2 ? e4 : e2, f3 = b2 ? e5 : e3, f4 = b2 ? e6 : e4;
+  (void)e7;
+  const uint32_t g0 = b4 ? d4 : f0, g1 = b4 ? d5 : f1, g2 = b4 ? d6 : f2, g3 = b4 ? d7 : f3, g4 = b4 ? 0u : f4;
+  o[0] = __builtin_amdgcn_alignbyte(g1, g0, r);
+  o[1] = __builtin_amdgcn_alignbyte(g2, g1, r);
+  o[2] = __builtin_amdgcn_alignbyte(g3, g2, r);
+  o[3] = __builtin_amdgcn_alignbyte(g4, g3, r);
+}
+
 __device__ __forceinline__ uint32_t shr1(uint32_t old, uint32_t v) {  // lane i <- lane i-1; lane 0 <- old
   return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x138, 0xF, 0xF, false);
 }
@@ -254,10 +291,8 @@ __global__ void __launch_bounds__(kThreads) alpha_kernel(const AlphaDesc* __rest
     return;
   } else {
   __shared__ uint32_t gprog[kWaves];    // gradient: each band's last row's columns done (tag: band << 16)
-  // gradient: per wave, its band's outputs (a 32-column ring per row) on their way to 16-byte stores
-  __shared__ __attribute__((aligned(16))) uint8_t ring[kWaves][64][32];
   const int W = F.width, H = F.height, tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
+  const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // (uniform: the band loop and its exits stay scalar)
   const gptr<uint8_t> plane = as_global(F.plane);
   if (F.coded && F.pal) {  // (an 8-bit stream's palette: only with filters none / horizontal in practice)
     if (tid < (1 << (8 >> F.cbits))) palg[tid] = (uint8_t)(F.pal[tid] >> 8);
@@ -269,17 +304,32 @@ __global__ void __launch_bounds__(kThreads) alpha_kernel(const AlphaDesc* __rest
   // ---- 1. the filtered bytes into the plane (coalesced: four per thread and step; K7's coded
   //         image through the palette, K3's green, or the raw payload), then row 0 as
   //         HorizontalUnfilter_C with no row above (filters.go:130-140)
+  //         (a wave per row, a lane per four columns; maps of at most 16 colours by v_perm)
   {
     const bool dw = (W & 3) == 0;
-    const size_t n4 = dw ? (size_t)W * H / 4 : 0;
-    const int q4 = W >> 2;
-    for (size_t i = tid; i < n4; i += kThreads) {
-      const int y = (int)(i / (size_t)q4), x = 4 * (int)(i - (size_t)y * q4);
-      *reinterpret_cast<gptr<uint32_t>>(plane + 4 * i) = src_quad(F, palg, y, x, gvec);
+    const bool ppal = F.coded && F.pal && F.cbits >= 1;
+    uint32_t pg[4] = {0u, 0u, 0u, 0u};
+    if (ppal) {
+      const int ne = 1 << (8 >> F.cbits);
+#pragma unroll
+      for (int e = 0; e < 16; ++e)
+        if (e < ne) pg[e >> 2] |= ((F.pal[e] >> 8) & 0xffu) << (8 * (e & 3));
     }
-    for (size_t i = n4 * 4 + tid; i < (size_t)W * H; i += kThreads) {
-      const int y = (int)(i / (size_t)W), x = (int)(i - (size_t)y * W);
-      plane[i] = (uint8_t)src_byte(F, palg, y, x);
+    for (int y = wave; y < H; y += kWaves) {
+      const gptr<uint8_t> prow = plane + (size_t)y * W;
+      for (int x = 4 * lane; x < W; x += 256) {
+        if (x + 3 < W) {
+          const uint32_t q = ppal ? pal_quad(F, pg, y, x) : src_quad(F, palg, y, x, gvec);
+          if (dw) {
+            *reinterpret_cast<gptr<uint32_t>>(prow + x) = q;
+          } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) prow[x + k] = (uint8_t)(q >> (8 * k));
+          }
+        } else {
+          for (int k = 0; x + k < W; ++k) prow[x + k] = (uint8_t)src_byte(F, palg, y, x + k);
+        }
+      }
     }
   }
   __syncthreads();
@@ -331,24 +381,61 @@ __global__ void __launch_bounds__(kThreads) alpha_kernel(const AlphaDesc* __rest
       }
     }
   } else if (F.filter == 3) {  // GradientUnfilter_C (filters.go:157-171)
+#ifdef WG_ABL_GRAD_SKIP  // (measurement only: output wrong)
+    if (F.width != 12345) goto grad_done;
+#endif
     // Band b = rows [1 + 64 b, 1 + 64 b + 64): lane l owns row y = 1 + 64 b + l and at step s
     // works on column x = s - l.  T = out[y-1][x] is what the lane above produced at step s - 1
-    // (DPP row shift); lane 0's comes from the band above's last row, read back from the plane in
-    // chunks of 64 columns (one per lane, then v_readlane per step) once that band's progress
-    // counter covers them; TL = the previous step's T; L = the lane's previous output.  The
-    // leftmost column predicts from above (L = TL = T).
-    // Memory: a lane's filtered bytes arrive 16 steps at a time (K3's green: four 16-byte loads of
-    // its row, a group ahead), and its outputs go into its row of the wave's LDS ring (32 columns),
-    // from which each group stores the one 16-column block of the row that has become complete --
-    // 16-byte stores instead of a byte store per lane and step (64 rows touched per instruction).
-    // Every 64 steps the band publishes how many columns of its last row are in the plane
-    // (gprog[b & 15], tag b << 16: a later band's value on the same slot implies this one is done).
+    // (DPP wave shift); TL = the previous step's T; L = the lane's previous output; the leftmost
+    // column predicts from above (L = TL = T).  Lane 0's T is the band above's last row: that band
+    // writes the row's outputs into an LDS ring (`tring`, one per band slot b & 15, 512 columns)
+    // as it stores them, and publishes how many columns are there (gprog[b & 15], tag b << 16: a
+    // later band's value on the slot implies this one is done); band 0's T is row 0 (`row0`).  The
+    // band below reports the columns it has read (cprog) so the ring is not overwritten early.
+    // Steps go in groups of 16 (column x0 = 16 g - lane .. x0 + 15 for the lane in group g).
+    // Inputs: a group's 16 filtered bytes span two aligned 16-byte blocks of the row, the second
+    // being the first of the next group: each group loads ONE aligned block -- A lane is a row, so
+    // every load or store touches 64 lines, and that line rate bounds the wavefront (an unaligned
+    // 16 + 4-byte pair per group, plus a global T load, cost 0.6 ms more on c3ag).  The blocks go
+    // by LDS-DMA (buffer_load ... lds: no VGPR destination, so nothing the compiler could copy
+    // before the data lands) into the wave's four 1 KiB slots, three groups ahead; the wave waits
+    // for them with a counted vmcnt (hidden from the compiler: its own count fell back to waiting
+    // for nearly every load at the loop's back edge).  Blocks start at or after x0: none holds an
+    // output yet; a neighbouring row's bytes in a block feed only columns outside the row.
+    // Outputs: a group's 16 outputs sit in `cur` (static byte positions); after the group the lane
+    // stores the aligned 16-column block of its row that has just become complete, shifted out of
+    // prv|cur (the shift is the same for every group of the lane).
     const int nb = (H - 1 + 63) / 64;
-    // (the filtered bytes are in the plane since step 1: read in place, ahead of the outputs)
+    constexpr int kRing = 512;
+    __shared__ __attribute__((aligned(16))) uint8_t tring[kWaves][kRing];
+    __shared__ __attribute__((aligned(16))) uint8_t row0[kMaxDim];
+    __shared__ __attribute__((aligned(16))) uint32_t dma[kWaves][4][256];  // (1 KiB per slot: 16 B per lane)
+    __shared__ uint32_t cprog[kWaves];
+    if (tid < kWaves) cprog[tid] = 0;
+    for (int x = tid; x < W; x += kThreads) row0[x] = plane[x];
+    __syncthreads();
     const __amdgpu_buffer_rsrc_t psrc = __builtin_amdgcn_make_buffer_rsrc(F.plane, 0, W * H, 0x00020000);
+    const uint64_t pa = reinterpret_cast<uintptr_t>(F.plane);
+    const i32x4 prs = {__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)pa),
+                       __builtin_amdgcn_readfirstlane((int32_t)(uint32_t)(pa >> 32) & 0xffff),
+                       __builtin_amdgcn_readfirstlane(W * H), 0x00020000};
     const bool st16 = (W & 15) == 0 && (reinterpret_cast<uintptr_t>(F.plane) & 15) == 0;
-    uint8_t* myring = &ring[wave][lane][0];
-#ifdef WG_ABL_GRAD_1BAND  // (measurement only: one band per wave, output wrong)
+    uint32_t dslot[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) dslot[k] = lds_addr(&dma[wave][k][0]);
+    auto spin = [&](const uint32_t* ctr, uint32_t need) {  // (acquire; 2 s bound: never reached)
+#ifdef WG_ABL_GRAD_NOWAIT  // (measurement only: output wrong)
+      return;
+#endif
+      if (__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
+        const uint64_t t_0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
+          __builtin_amdgcn_s_sleep(1);
+          if (__builtin_amdgcn_s_memrealtime() - t_0 > 200000000ull) break;
+        }
+      }
+    };
+#ifdef WG_ABL_GRAD_1BAND  // (measurement only: output wrong)
     for (int bnd = wave; bnd < min(nb, kWaves); bnd += kWaves) {
 #else
     for (int bnd = wave; bnd < nb; bnd += kWaves) {
@@ -356,76 +443,78 @@ __global__ void __launch_bounds__(kThreads) alpha_kernel(const AlphaDesc* __rest
       const int y0 = 1 + 64 * bnd, rows = min(64, H - y0);
       const int y = y0 + min(lane, rows - 1);
       const bool row_ok = lane < rows;
-      // (global address space: flat accesses would make every LDS-ring access wait for them too)
-      const gptr<const uint8_t> above = plane + (size_t)(y0 - 1) * W;
+#ifdef WG_ABL_GRAD_1BAND
+      const bool produce = bnd + 1 < min(nb, kWaves);
+#else
+      const bool produce = bnd + 1 < nb;
+#endif  // (a band below reads this one's last row, lane 63)
+      const int slot = bnd & (kWaves - 1), aslot = (bnd - 1) & (kWaves - 1);
+      // (global address space: flat accesses would make every LDS access wait for them too)
       const gptr<uint8_t> prow = as_global(plane) + (size_t)y * W;
       uint32_t L = 0, T = 0, TL = 0;
       int stored = 0;   // columns [0, stored) of the lane's row are in the plane
-      // the 16 filtered bytes of steps sg .. sg + 15 (columns sg - lane ..): the five aligned dwords
-      // around them as loaded, shifted into place (v_alignbyte) where used, so the loads stay in
-      // flight a group ahead
-      struct Grp {
-        u32x4 w;
-        uint32_t w4, sh;
-      };
-      auto load_group = [&](int sg, Grp& q) {
-        // (columns before the row's start, x0 < 0 -- possible only for W < 64 -- and rows past the
-        // band read 0 through the buffer range: their values are never used)
-        const int e = y * W + (sg - lane);
-        const uint32_t off = row_ok && e >= 0 ? (uint32_t)e : 0x20000000u;
-        q.w = __builtin_amdgcn_raw_buffer_load_b128(psrc, (int)(off & ~3u), 0, 0);
-        q.w4 = __builtin_amdgcn_raw_buffer_load_b32(psrc, (int)((off & ~3u) + 16), 0, 0);
-        q.sh = off & 3u;
-      };
-      // store the lane's complete 16-column blocks below `upto` (exclusive) from the ring: during
-      // the band at most one per group (the lane's columns advance 16 per group), a fixed number of
-      // vector-memory operations -- a store loop of varying trip count would make the compiler wait
-      // for vmcnt(0), i.e. for the group loads just issued, at the next group
-      auto flush_one = [&](int upto) {
-        if (row_ok && stored + 16 <= upto) {
-          const uint4 v = *reinterpret_cast<const uint4*>(myring + (stored & 31));
-          if (st16) {
-            *reinterpret_cast<gptr<u32x4>>(prow + stored) = u32x4{v.x, v.y, v.z, v.w};
-          } else {
-            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-            for (int k = 0; k < 16; ++k) prow[stored + k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
-          }
-          stored += 16;
-        }
-      };
-      auto flush_rest = [&] {  // (the row's remaining columns, after the band's last group)
-        for (int m = stored; row_ok && m < W; ++m) prow[m] = myring[m & 31];
-        stored = W;
-      };
-      Grp qa, qb;
-      const int steps = W + rows - 1;
-      load_group(0, qa);
-      // Groups of 16 steps.  Lane j < 16 holds column 16 g + j of the row above for group g (t0),
-      // loaded one group ahead (tn) once the band above's last row has stored 16 g + 32 columns;
-      // the band publishes its own last row's stored columns after every group.
-      auto wait_above = [&](int cols) {
-#ifdef WG_ABL_GRAD_NOWAIT  // (measurement only: output wrong)
-        return;
+      const int A0 = y * W - lane;  // plane offset of the lane's group-0 column
+      const int ls = 16 - ((-A0) & 15), lq = ls >> 2, lr = ls & 3;
+      const uint32_t blk0 = row_ok ? (uint32_t)(A0 + ((-A0) & 15)) : 0x40000000u;
+      // (group 0's first block -- group g's previous one is group g - 1's -- a plain counted load)
+      u32x4 prevw = __builtin_amdgcn_raw_buffer_load_b128(psrc, (int)(blk0 - 16u), 0, 0);
+#ifdef WG_ABL_GRAD_NOLOAD  // (measurement only: output wrong)
+      auto load_group = [&](int sg, int k) { if (F.width == 12345) dma_load_b128(prs, blk0 + (uint32_t)sg, dslot[k]); };
+#else
+      auto load_group = [&](int sg, int k) { dma_load_b128(prs, blk0 + (uint32_t)sg, dslot[k]); };
 #endif
-        if (bnd == 0) return;  // (row 0 is complete)
-        const uint32_t need = ((uint32_t)(bnd - 1) << 16) | (uint32_t)min(W, cols);
-        uint32_t* pg = gprog + ((bnd - 1) & (kWaves - 1));
-        if (__hip_atomic_load(pg, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
-          const uint64_t t_0 = __builtin_amdgcn_s_memrealtime();
-          while (__hip_atomic_load(pg, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
-            __builtin_amdgcn_s_sleep(1);
-            if (__builtin_amdgcn_s_memrealtime() - t_0 > 200000000ull) break;  // (2 s: never reached)
+      const int sh = 16 - ((-lane) & 15), sq = sh >> 2, sr = sh & 3;
+      uint32_t prv[4] = {0u, 0u, 0u, 0u}, cur[4] = {0u, 0u, 0u, 0u};
+      auto emit = [&](int sg) {
+        const int x0 = sg - lane, B = x0 - (x0 & 15);
+        uint32_t o[4];
+        window16(prv[0], prv[1], prv[2], prv[3], cur[0], cur[1], cur[2], cur[3], sq, sr, o);
+#ifdef WG_ABL_GRAD_NOSTORE  // (measurement only: output wrong)
+        if (row_ok && B >= 0 && B < W && F.width == 12345) {
+#else
+        if (row_ok && B >= 0 && B < W) {
+#endif
+          if (B + 16 <= W && st16) {
+            *reinterpret_cast<gptr<u32x4>>(prow + B) = u32x4{o[0], o[1], o[2], o[3]};
+          } else {
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+              if (B + k < W) prow[B + k] = (uint8_t)(o[k >> 2] >> (8 * (k & 3)));
           }
         }
+        stored = row_ok ? max(0, min(W, B + 16)) : W;
+        // the last row's block into the ring, once the band below has read what it replaces
+        const int Bl = sg - 63 - ((sg - 63) & 15);  // (lane 63's B)
+        if (produce && Bl >= 0 && Bl < W) {
+          const uint32_t need = Bl < kRing ? (((uint32_t)(bnd - 15) << 16) | 0xffffu)
+                                           : (((uint32_t)(bnd + 1) << 16) | (uint32_t)(Bl - kRing + 16));
+          // (the slot's previous reader, band b - 15, exists from b = 16 on: band 0 reads row0)
+          if (bnd >= 16 || Bl >= kRing) spin(cprog + slot, need);
+          if (lane == 63) *reinterpret_cast<u32x4*>(&tring[slot][Bl & (kRing - 1)]) = u32x4{o[0], o[1], o[2], o[3]};
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) prv[j] = cur[j];
       };
-      // (straight-line steps: no break at the band's end and no test on s < W -- steps past the
-      // band's end have x >= W on every row (no output) and lane 0's T past the row's end feeds
-      // nothing; a branch around each v_readlane of t0 made the waitcnt pass wait vmcnt(0) before
-      // every one of them, i.e. for the group loads in flight)
-      auto run_group = [&](int sg, const Grp& q, uint32_t t0) {
-        const uint32_t b[4] = {__builtin_amdgcn_alignbyte(q.w.y, q.w.x, q.sh), __builtin_amdgcn_alignbyte(q.w.z, q.w.y, q.sh),
-                               __builtin_amdgcn_alignbyte(q.w.w, q.w.z, q.sh), __builtin_amdgcn_alignbyte(q.w4, q.w.w, q.sh)};
+      // lane 0's T for group sg (lanes j < 16: column sg + j of the row above; past the row's end
+      // a clamped column, unused), once the band above has it in its ring
+      auto read_t = [&](int sg) -> uint32_t {
+        const int c = min(sg + (lane & 15), W - 1);
+        if (bnd == 0) return row0[c];
+        if (sg < W) spin(gprog + aslot, ((uint32_t)(bnd - 1) << 16) | (uint32_t)min(W, sg + 16));
+        const uint32_t t = tring[aslot][c & (kRing - 1)];
+        // (the read stays before the report in program order -- LDS serves a wave's accesses in
+        // order, so the producer's overwrite, issued after it sees the report, comes after it)
+        asm volatile("" ::: "memory");
+        if (lane == 0) __hip_atomic_store(cprog + aslot, ((uint32_t)bnd << 16) | (uint32_t)min(W, sg + 16),
+                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return t;
+      };
+      auto run_group = [&](int sg, const u32x4& q, uint32_t t0) {
+        uint32_t b[4];
+        {
+          window16(prevw.x, prevw.y, prevw.z, prevw.w, q.x, q.y, q.z, q.w, lq, lr, b);
+          prevw = q;
+        }
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
           const int s = sg + k;
@@ -436,50 +525,55 @@ __global__ void __launch_bounds__(kThreads) alpha_kernel(const AlphaDesc* __rest
           const uint32_t l = x == 0 ? T : L, tl = x == 0 ? T : TL;
           const int g = (int)l + (int)T - (int)tl;
           const uint32_t o = (((b[k >> 2] >> (8 * (k & 3))) & 0xffu) + (uint32_t)min(max(g, 0), 255)) & 0xffu;
-          if (ok) {
-#ifndef WG_ABL_GRAD_NOLDS  // (measurement only: output wrong)
-            myring[x & 31] = (uint8_t)o;
-#endif
-            L = o;
-          }
+          cur[k >> 2] = (k & 3) == 0 ? o : cur[k >> 2] | (o << (8 * (k & 3)));
+          L = ok ? o : L;
           TL = T;
         }
       };
-      auto publish = [&] {  // (release: the row's plane stores before the counter; lane rows - 1 has the fewest)
+      auto publish = [&] {  // (release: the ring and the row's plane stores before the counter)
         const uint32_t done = (uint32_t)__builtin_amdgcn_readlane(stored, rows - 1);
         if (lane == 0)
-          __hip_atomic_store(gprog + (bnd & (kWaves - 1)), ((uint32_t)bnd << 16) | done, __ATOMIC_RELEASE,
-                             __HIP_MEMORY_SCOPE_WORKGROUP);
+          __hip_atomic_store(gprog + slot, ((uint32_t)bnd << 16) | done, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       };
-      wait_above(16);
-      uint32_t ta = above[min(lane & 15, W - 1)], tb = 0;
-      for (int sg = 0; sg < steps; sg += 32) {
-        // group sg (qa, ta), then group sg + 16 (qb, tb)
-        load_group(sg + 16, qb);
-        if (sg + 16 < W) {
-          wait_above(sg + 32);
-          tb = above[min(sg + 16 + (lane & 15), W - 1)];
-        }
-        run_group(sg, qa, ta);
-        flush_one(min(W, max(0, sg + 16 - lane)));
+      const int steps = W + rows - 1;
+      load_group(0, 0);
+      load_group(16, 1);
+      load_group(32, 2);
+      int last = 0;  // the last group's first step
+      // stage: issue group sg + 48's block, read T, wait for group sg's block (issued three
+      // stages ago: the two stages' blocks since and this one's -- vmcnt(3) leaves only those and
+      // younger stores in flight), the 16 steps, the stores
+      auto stage = [&](int sg, int k) -> bool {
+        load_group(sg + 48, (k + 3) & 3);
+        const uint32_t t = read_t(sg);
+        asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+        const u32x4 q = *reinterpret_cast<const u32x4*>(&dma[wave][k][4 * lane]);
+        run_group(sg, q, t);
+        emit(sg);
         publish();
-        if (sg + 16 >= steps) break;
-        load_group(sg + 32, qa);
-        if (sg + 32 < W) {
-          wait_above(sg + 48);
-          ta = above[min(sg + 32 + (lane & 15), W - 1)];
-        }
-        run_group(sg + 16, qb, tb);
-        flush_one(min(W, max(0, sg + 32 - lane)));
-        publish();
+        last = sg;
+        return sg + 16 >= steps;
+      };
+      for (int sg = 0;; sg += 64) {
+        if (stage(sg, 0)) break;
+        if (stage(sg + 16, 1)) break;
+        if (stage(sg + 32, 2)) break;
+        if (stage(sg + 48, 3)) break;
       }
-      flush_rest();
+      emit(last + 16);  // (the row's columns after its last full block: bytes of the last group)
       const uint32_t done = (uint32_t)__builtin_amdgcn_readlane(stored, rows - 1);
-      if (lane == 0)
-        __hip_atomic_store(gprog + (bnd & (kWaves - 1)), ((uint32_t)bnd << 16) | done, __ATOMIC_RELEASE,
-                           __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (lane == 0) {
+        __hip_atomic_store(gprog + slot, ((uint32_t)bnd << 16) | done, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (bnd > 0)  // (this band has read all of the band above's ring)
+          __hip_atomic_store(cprog + aslot, ((uint32_t)bnd << 16) | 0xffffu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      // (the blocks loaded past the end land before their slots are reused)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
   }
+#ifdef WG_ABL_GRAD_SKIP
+grad_done:
+#endif
   __syncthreads();
 
   // ---- 3. plane window -> A bytes (the RGBA holds the window: the whole plane unless cropping)
