@@ -266,6 +266,7 @@ struct wg_batch {
   int n_alpha_2d = 0;  // alpha planes with filter vertical / gradient (K4's second instantiation)
   bool tail_modes = true, no_tail = false;  // no_tail: frames emitted directly in a mode K1's tail lacks
   int n_tok_w64 = 0;                         // K7 streams on its 64-mask-word instantiation (first in tokdesc)
+  int n_tok_alpha = 0;                       // of those, the alpha streams whose bytes K7 writes (first)
   bool k2_modes = false;                     // K2 writes some frame in a non-RGBA colorspace (FrameDesc::emit)
   wg_decoder_options opt{};          // output colorspace, cropping, flip (f4)
   bool any_crop = false;             // K2 reads compact cropped planes through desc2
@@ -810,7 +811,17 @@ void batch_layout(wg_batch* b, wg::StagingArena& arena, int32_t* status) {
         f.al.off_coded = pl_b;
         pl_b = align_up(pl_b + f.al.n_px() * 4);
         k7 += k7_bytes(f.al);
-        if (f.alpha_direct) {
+        // 8-bit streams whose map fits K7's registers (<= 16 entries: bundled indices) or that
+        // have none, under filters none / vertical / gradient: K7 writes the filtered bytes itself,
+        // into the plane (K4 then works in place: no gather; none: nothing left to do alpha-first).
+        // Not horizontal: K4 reads the coded image there as fast as the bytes (c3a, same call:
+        // K4 1.40 vs 1.53 ms) and K7's extra stores cost ~1 ms per 256 4K planes
+        f.alpha_k7 = f.alpha_direct && f.ah.filter != 1 && (f.al.n_transforms == 0 || f.al.bits[0] >= 1) &&
+                     wg::vp8l_resolve_w64(f.al.cache_bits);
+        if (f.alpha_k7) {
+          k7 += px;  // (its filtered bytes)
+          k4 += px;  // (K4 reads them back)
+        } else if (f.alpha_direct) {
           k4 += 4.0 * f.al.n_px() + (f.al.n_transforms ? (double)f.al.tdata[0].bytes : 0.0);
         } else {
           k3 += ll_bytes(f.al);
@@ -1046,7 +1057,27 @@ int batch_upload(wg_batch* b, const wg::StagingArena& arena) {
       AlphaDesc a{};
       if (f.ah.method == 1) {
         b->tokdesc.push_back(make_tok(f.al, arena, b->d_in, b->d_planes));
-        if (f.alpha_direct) {
+        if (f.alpha_k7) {  // (K7 writes the filtered bytes: K4 reads them as it reads a raw plane)
+          wg::LLTokDesc& t = b->tokdesc.back();
+          uint8_t* dst = b->d_planes + f.off_aplane;
+          t.afilt = dst;
+          t.a_cw = f.al.coded_width;
+          t.a_width = f.width;
+          t.a_height = f.height;
+          t.a_cbits = f.al.n_transforms ? f.al.bits[0] : 0;
+          t.a_pal = f.al.n_transforms ? 1 : 0;
+          // p / cw by multiply-shift for p < 2^28 (n_px): l = ceil(log2 cw), m = 2^(28+l) / cw + 1
+          int l = 0;
+          while ((1 << l) < t.a_cw) ++l;
+          t.a_cw_s = l;
+          t.a_cw_m = (uint32_t)((uint64_t(1) << (28 + l)) / (uint64_t)t.a_cw + 1);
+          if (t.a_pal) {  // ExpandColorMap's padded map: 1 << (8 >> cbits) <= 16 ARGB entries
+            const uint32_t* pal = reinterpret_cast<const uint32_t*>(arena.host_ptr(f.al.tdata[0]));
+            const int ne = 1 << (8 >> t.a_cbits);
+            for (int e = 0; e < ne; ++e) t.a_pg[e >> 2] |= ((pal[e] >> 8) & 0xffu) << (8 * (e & 3));
+          }
+          a.raw = dst;
+        } else if (f.alpha_direct) {
           a.coded = reinterpret_cast<const uint32_t*>(b->d_planes + f.al.off_coded);
           a.coded_width = f.al.coded_width;
           a.cbits = f.al.n_transforms ? f.al.bits[0] : 0;
@@ -1199,11 +1230,16 @@ int batch_upload(wg_batch* b, const wg::StagingArena& arena) {
   if (e == hipSuccess && !b->lldesc.empty())
     e = hipMemcpyAsync(b->d_lldesc, b->lldesc.data(), sizeof(LLDesc) * b->lldesc.size(), hipMemcpyHostToDevice,
                        home);
-  // K7 launches the streams of its 64-mask-word instantiation first (one kernel each)
+  // K7 launches the streams of its 64-mask-word instantiation first (one kernel each), the alpha
+  // streams whose bytes it writes (a 64-word instantiation of their own) before them
   std::stable_partition(b->tokdesc.begin(), b->tokdesc.end(),
                         [](const wg::LLTokDesc& t) { return wg::vp8l_resolve_w64(t.cache_bits); });
   b->n_tok_w64 = (int)std::count_if(b->tokdesc.begin(), b->tokdesc.end(),
                                     [](const wg::LLTokDesc& t) { return wg::vp8l_resolve_w64(t.cache_bits); });
+  std::stable_partition(b->tokdesc.begin(), b->tokdesc.begin() + b->n_tok_w64,
+                        [](const wg::LLTokDesc& t) { return t.afilt != nullptr; });
+  b->n_tok_alpha = (int)std::count_if(b->tokdesc.begin(), b->tokdesc.end(),
+                                      [](const wg::LLTokDesc& t) { return t.afilt != nullptr; });
   if (e == hipSuccess && !b->tokdesc.empty())
     e = hipMemcpyAsync(b->d_tokdesc, b->tokdesc.data(), sizeof(wg::LLTokDesc) * b->tokdesc.size(),
                        hipMemcpyHostToDevice, home);
@@ -1302,7 +1338,8 @@ int wg_batch_run(wg_batch* b, void* stream) {
   if (side) {
     hipError_t e = hipStreamWaitEvent(side, t.ev[0], 0);
     if (e == hipSuccess) e = hipEventRecord(t.side[0], side);
-    if (e == hipSuccess) e = wg::launch_vp8l_resolve(b->d_tokdesc, nullptr, (int)b->tokdesc.size(), b->d_err, side, b->n_tok_w64);
+    if (e == hipSuccess) e = wg::launch_vp8l_resolve(b->d_tokdesc, nullptr, (int)b->tokdesc.size(), b->d_err, side, b->n_tok_w64,
+                                                   b->n_tok_alpha);
     if (e == hipSuccess) e = hipEventRecord(t.side[1], side);
     if (e != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
   }
@@ -1352,7 +1389,7 @@ int wg_batch_run(wg_batch* b, void* stream) {
       case kStageK7:  // the lossless streams' color cache and back-references
         if (t.forked) e = hipStreamWaitEvent(s, t.side[1], 0);
         else if (b->n_k3 > 0)
-          e = wg::launch_vp8l_resolve(b->d_tokdesc, nullptr, (int)b->tokdesc.size(), b->d_err, s, b->n_tok_w64);
+          e = wg::launch_vp8l_resolve(b->d_tokdesc, nullptr, (int)b->tokdesc.size(), b->d_err, s, b->n_tok_w64, b->n_tok_alpha);
         break;
       case kStageK3:
         if (!b->lldesc.empty()) e = wg::launch_vp8l_transforms(b->d_lldesc, b->ll_groups, b->d_err, s);

@@ -155,6 +155,8 @@ __device__ __forceinline__ uint32_t src_quad(const AlphaDesc& F, const uint8_t* 
            coded_green(F, palg, v3, x + 3) << 24;
   }
   const size_t i = (size_t)y * F.width + x;
+  if (F.raw && ((reinterpret_cast<uintptr_t>(F.raw) | (uintptr_t)F.width) & 3) == 0)
+    return *reinterpret_cast<const uint32_t*>(F.raw + i);
   if (F.green && vec) {
     const uint4 g = *reinterpret_cast<const uint4*>(F.green + 4 * i);
     return __builtin_amdgcn_perm(__builtin_amdgcn_perm(g.w, g.z, 0x0c0c0501u), __builtin_amdgcn_perm(g.y, g.x, 0x0c0c0501u),
@@ -199,6 +201,8 @@ __device__ void alpha_rows_direct(const AlphaDesc& F, int part, int parts, uint8
   const int W = F.width, H = F.height, tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const bool horiz = F.filter == 1;
+  // (filter none, alpha-first, K7 wrote the bytes into the plane: they are the output already)
+  if (!horiz && F.to_plane && F.raw == F.plane) return;
   if (F.coded && F.pal) {
     if (tid < (1 << (8 >> F.cbits))) palg[tid] = (uint8_t)(F.pal[tid] >> 8);
     __syncthreads();
@@ -305,7 +309,8 @@ __global__ void __launch_bounds__(kThreads) alpha_kernel(const AlphaDesc* __rest
   //         image through the palette, K3's green, or the raw payload), then row 0 as
   //         HorizontalUnfilter_C with no row above (filters.go:130-140)
   //         (a wave per row, a lane per four columns; maps of at most 16 colours by v_perm)
-  {
+  //         (K7 wrote an 8-bit stream's filtered bytes into the plane itself: nothing to gather)
+  if (F.raw != F.plane) {
     const bool dw = (W & 3) == 0;
     const bool ppal = F.coded && F.pal && F.cbits >= 1;
     uint32_t pg[4] = {0u, 0u, 0u, 0u};

@@ -97,9 +97,18 @@ struct LLTokDesc {
   uint32_t* coded;         // n_px resolved pixels
   int32_t n_px, n_lits, cache_bits, valid;
   int32_t trusted;  // tokens from the host entropy stage, which keeps them in bounds (no device check)
-  int32_t pad;
+  int32_t a_cw;     // afilt: the coded image's width (coded pixels per row)
+  // An 8-bit alpha stream (libwebp's ALPH: a colour map of at most 16 entries, bundled, or no
+  // transform): K7 also writes its FILTERED alpha bytes -- green through the map -- into `afilt`
+  // (a_width-byte rows, a_height rows), so K4 reads 1 B/px instead of the coded image (and, for
+  // filter none or vertical / gradient, finds them already in its plane).  Null: not written.
+  uint8_t* afilt;
+  int32_t a_width, a_height, a_cbits, a_pal;  // a_pal: the map's green bytes in a_pg (else the green itself)
+  uint32_t a_pg[4];                           // entry 4j + i in byte i of a_pg[j]
+  uint32_t a_cw_m;                            // p / a_cw = (p * a_cw_m) >> (28 + a_cw_s) for p < 2^28
+  int32_t a_cw_s;
 };
-static_assert(sizeof(LLTokDesc) == 48, "LLTokDesc must be 48 bytes");
+static_assert(sizeof(LLTokDesc) == 96, "LLTokDesc must be 96 bytes");
 
 // One lossless (VP8L) frame for K3.  `coded` is the entropy-coded ARGB image from the host
 // stage; `stages` are its transforms in APPLICATION order (the reverse of bitstream order).

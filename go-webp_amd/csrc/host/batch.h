@@ -46,6 +46,7 @@ struct FrameParse {
   LLMeta al;
   Region araw;
   bool alpha_direct = false;  // capi.cpp: K4 reads the alpha stream's coded image itself (no K3)
+  bool alpha_k7 = false;      // capi.cpp: K7 writes the stream's filtered bytes (LLTokDesc::afilt)
   bool emit_direct = false;   // capi.cpp: K1's tail / K2 write the output colorspace itself (no K6)
   // output (cropping, f4): out_w x out_h, taken at (win_x, win_y) of the frame's RGBA buffer
   // (rgba_w x rgba_h: the window itself for lossy frames, the whole frame for lossless)
