@@ -267,6 +267,7 @@ struct wg_batch {
   bool tail_modes = true, no_tail = false;  // no_tail: frames emitted directly in a mode K1's tail lacks
   int n_tok_w64 = 0;                         // K7 streams on its 64-mask-word instantiation (first in tokdesc)
   int n_tok_alpha = 0;                       // of those, the alpha streams whose bytes K7 writes (first)
+  int n_tok_tiled = 0;                       // of those, the ones into band tiles (first)
   bool k2_modes = false;                     // K2 writes some frame in a non-RGBA colorspace (FrameDesc::emit)
   wg_decoder_options opt{};          // output colorspace, cropping, flip (f4)
   bool any_crop = false;             // K2 reads compact cropped planes through desc2
@@ -818,6 +819,10 @@ void batch_layout(wg_batch* b, wg::StagingArena& arena, int32_t* status) {
         // K4 1.40 vs 1.53 ms) and K7's extra stores cost ~1 ms per 256 4K planes
         f.alpha_k7 = f.alpha_direct && f.ah.filter != 1 && (f.al.n_transforms == 0 || f.al.bits[0] >= 1) &&
                      wg::vp8l_resolve_w64(f.al.cache_bits);
+        if (f.alpha_k7 && f.ah.filter == 3) {  // (gradient: rows 1.. in K4's band tiles)
+          f.off_atile = pl_b;
+          pl_b = align_up(pl_b + (size_t)((f.height - 1 + 63) / 64) * ((f.width + 15) / 16) * 1024);
+        }
         if (f.alpha_k7) {
           k7 += px;  // (its filtered bytes)
           k4 += px;  // (K4 reads them back)
@@ -1076,7 +1081,9 @@ int batch_upload(wg_batch* b, const wg::StagingArena& arena) {
             const int ne = 1 << (8 >> t.a_cbits);
             for (int e = 0; e < ne; ++e) t.a_pg[e >> 2] |= ((pal[e] >> 8) & 0xffu) << (8 * (e & 3));
           }
+          if (f.ah.filter == 3) t.atile = b->d_planes + f.off_atile;
           a.raw = dst;
+          a.tiles = t.atile;
         } else if (f.alpha_direct) {
           a.coded = reinterpret_cast<const uint32_t*>(b->d_planes + f.al.off_coded);
           a.coded_width = f.al.coded_width;
@@ -1240,6 +1247,10 @@ int batch_upload(wg_batch* b, const wg::StagingArena& arena) {
                         [](const wg::LLTokDesc& t) { return t.afilt != nullptr; });
   b->n_tok_alpha = (int)std::count_if(b->tokdesc.begin(), b->tokdesc.end(),
                                       [](const wg::LLTokDesc& t) { return t.afilt != nullptr; });
+  std::stable_partition(b->tokdesc.begin(), b->tokdesc.begin() + b->n_tok_alpha,
+                        [](const wg::LLTokDesc& t) { return t.atile != nullptr; });
+  b->n_tok_tiled = (int)std::count_if(b->tokdesc.begin(), b->tokdesc.end(),
+                                      [](const wg::LLTokDesc& t) { return t.atile != nullptr; });
   if (e == hipSuccess && !b->tokdesc.empty())
     e = hipMemcpyAsync(b->d_tokdesc, b->tokdesc.data(), sizeof(wg::LLTokDesc) * b->tokdesc.size(),
                        hipMemcpyHostToDevice, home);
@@ -1339,7 +1350,7 @@ int wg_batch_run(wg_batch* b, void* stream) {
     hipError_t e = hipStreamWaitEvent(side, t.ev[0], 0);
     if (e == hipSuccess) e = hipEventRecord(t.side[0], side);
     if (e == hipSuccess) e = wg::launch_vp8l_resolve(b->d_tokdesc, nullptr, (int)b->tokdesc.size(), b->d_err, side, b->n_tok_w64,
-                                                   b->n_tok_alpha);
+                                                   b->n_tok_alpha, b->n_tok_tiled);
     if (e == hipSuccess) e = hipEventRecord(t.side[1], side);
     if (e != hipSuccess) return WG_STATUS_UNSUPPORTED_FEATURE;
   }
@@ -1389,7 +1400,8 @@ int wg_batch_run(wg_batch* b, void* stream) {
       case kStageK7:  // the lossless streams' color cache and back-references
         if (t.forked) e = hipStreamWaitEvent(s, t.side[1], 0);
         else if (b->n_k3 > 0)
-          e = wg::launch_vp8l_resolve(b->d_tokdesc, nullptr, (int)b->tokdesc.size(), b->d_err, s, b->n_tok_w64, b->n_tok_alpha);
+          e = wg::launch_vp8l_resolve(b->d_tokdesc, nullptr, (int)b->tokdesc.size(), b->d_err, s, b->n_tok_w64, b->n_tok_alpha,
+                                      b->n_tok_tiled);
         break;
       case kStageK3:
         if (!b->lldesc.empty()) e = wg::launch_vp8l_transforms(b->d_lldesc, b->ll_groups, b->d_err, s);

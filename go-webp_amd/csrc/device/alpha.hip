@@ -15,15 +15,18 @@
 // encoder picks for most planes -- go straight from the filtered bytes to the A bytes, rows in
 // parallel (alpha_rows_direct): out[y][x] = c[y-1] + sum_{i<=x} in[y][i] with c the column-0
 // prefix sums (one block scan), then a wave scan per row.  Vertical and gradient run one
-// 1024-thread workgroup per plane, reading the filtered bytes straight from their source (K3's
-// green, the raw payload) and writing the unfiltered plane (round 6; no gather pass):
-//   1. row 0 as horizontal (one wave scan);
+// 1024-thread workgroup per plane on a scratch plane (width-byte rows):
+//   1. the filtered bytes into it (a wave per row: K3's green, the raw payload, K7's coded image
+//      through its map) -- unless K7 wrote them there itself (8-bit streams, LLTokDesc::afilt) --
+//      then row 0 as horizontal (one wave scan);
 //   2. vertical    out[y][x] = out[y-1][x] + in[y][x]: a running sum per column, four columns per
 //                  thread as one dword (bytewise adds without carries), rows loaded 8 ahead;
 //      gradient    out = in + clip(L + T - TL): a wavefront in 64-row bands, one band per wave at
 //                  a time (lane = row, one column per step, T from the lane above by DPP, the top
-//                  row of the band from the plane behind the band above's LDS progress counter --
-//                  no workgroup barrier per step), bands b = w, w + 16, ... on wave w;
+//                  row of the band through an LDS ring written by the band above, behind its LDS
+//                  progress counter -- no workgroup barrier per step), bands b = w, w + 16, ... on
+//                  wave w; the filtered bytes arrive 16 columns per lane by LDS-DMA three groups
+//                  ahead, from K7's band tiles (64 rows x 16 columns per KiB) when K7 wrote them;
 //   3. write the plane (its output window when cropping) into the A bytes (dword
 //      read-modify-write, coalesced) -- or leave it there (alpha-first).
 //
@@ -420,10 +423,15 @@ __global__ void __launch_bounds__(kThreads) alpha_kernel(const AlphaDesc* __rest
     for (int x = tid; x < W; x += kThreads) row0[x] = plane[x];
     __syncthreads();
     const __amdgpu_buffer_rsrc_t psrc = __builtin_amdgcn_make_buffer_rsrc(F.plane, 0, W * H, 0x00020000);
-    const uint64_t pa = reinterpret_cast<uintptr_t>(F.plane);
+    // the group loads' source: K7's band tiles (rows 1..: tile (b, c) = 64 rows x 16 columns, 1 KiB,
+    // LLTokDesc::atile) -- a group's loads then read four 256-byte runs instead of 64 rows -- or the
+    // plane itself (width-byte rows)
+    const bool tl = F.tiles != nullptr;
+    const int ncb = (W + 15) >> 4;
+    const uint64_t pa = reinterpret_cast<uintptr_t>(tl ? F.tiles : F.plane);
     const i32x4 prs = {__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)pa),
                        __builtin_amdgcn_readfirstlane((int32_t)(uint32_t)(pa >> 32) & 0xffff),
-                       __builtin_amdgcn_readfirstlane(W * H), 0x00020000};
+                       __builtin_amdgcn_readfirstlane(tl ? nb * ncb * 1024 : W * H), 0x00020000};
     const bool st16 = (W & 15) == 0 && (reinterpret_cast<uintptr_t>(F.plane) & 15) == 0;
     uint32_t dslot[4];
 #pragma unroll
@@ -458,15 +466,22 @@ __global__ void __launch_bounds__(kThreads) alpha_kernel(const AlphaDesc* __rest
       const gptr<uint8_t> prow = as_global(plane) + (size_t)y * W;
       uint32_t L = 0, T = 0, TL = 0;
       int stored = 0;   // columns [0, stored) of the lane's row are in the plane
-      const int A0 = y * W - lane;  // plane offset of the lane's group-0 column
+      // Group g's new block: the plane's aligned block c = ceil(A / 16) at A = y W + x0, taken from
+      // (previous | new) at ls = 16 - (-A mod 16); or, in tiles, the row's block g - lane / 16 of
+      // the band (x0 = 16 g - lane: ls = 16 - lane mod 16), one tile (1 KiB) further per group.
+      // Group 0's previous block: tiles -- only columns x < 0, unused; plane -- a plain counted load.
+      const int A0 = tl ? -lane : y * W - lane;
       const int ls = 16 - ((-A0) & 15), lq = ls >> 2, lr = ls & 3;
-      const uint32_t blk0 = row_ok ? (uint32_t)(A0 + ((-A0) & 15)) : 0x40000000u;
-      // (group 0's first block -- group g's previous one is group g - 1's -- a plain counted load)
-      u32x4 prevw = __builtin_amdgcn_raw_buffer_load_b128(psrc, (int)(blk0 - 16u), 0, 0);
+      const uint32_t blk0 = !row_ok ? 0x80000000u
+                            : tl    ? (uint32_t)(((bnd * ncb - (lane >> 4)) << 10) + (lane << 4))
+                                    : (uint32_t)(A0 + ((-A0) & 15));
+      const uint32_t gstep = tl ? 64u : 1u;  // (offset per step: a tile per 16 steps)
+      u32x4 prevw = {0u, 0u, 0u, 0u};
+      if (!tl) prevw = __builtin_amdgcn_raw_buffer_load_b128(psrc, (int)(blk0 - 16u), 0, 0);
 #ifdef WG_ABL_GRAD_NOLOAD  // (measurement only: output wrong)
-      auto load_group = [&](int sg, int k) { if (F.width == 12345) dma_load_b128(prs, blk0 + (uint32_t)sg, dslot[k]); };
+      auto load_group = [&](int sg, int k) { if (F.width == 12345) dma_load_b128(prs, blk0 + gstep * (uint32_t)sg, dslot[k]); };
 #else
-      auto load_group = [&](int sg, int k) { dma_load_b128(prs, blk0 + (uint32_t)sg, dslot[k]); };
+      auto load_group = [&](int sg, int k) { dma_load_b128(prs, blk0 + gstep * (uint32_t)sg, dslot[k]); };
 #endif
       const int sh = 16 - ((-lane) & 15), sq = sh >> 2, sr = sh & 3;
       uint32_t prv[4] = {0u, 0u, 0u, 0u}, cur[4] = {0u, 0u, 0u, 0u};

@@ -38,9 +38,10 @@ hipError_t launch_vp8l_transforms(const LLDesc* d_frames, const int* group_count
 // 64-mask-word instantiation (vp8l_resolve_w64(cache_bits): one window per block), the rest the
 // 32-word one.
 bool vp8l_resolve_w64(int cache_bits);
-// The first n_alpha of the 64-word streams write their alpha bytes too (LLTokDesc::afilt).
+// The first n_alpha of the 64-word streams write their alpha bytes too (LLTokDesc::afilt), the
+// first n_tiled of those into band tiles (LLTokDesc::atile).
 hipError_t launch_vp8l_resolve(const LLTokDesc* d_descs, const LLTokDesc* single, int n, int* d_err,
-                               hipStream_t stream, int n_w64 = 0, int n_alpha = 0);
+                               hipStream_t stream, int n_w64 = 0, int n_alpha = 0, int n_tiled = 0);
 
 // K4: ALPH planes (unfilter) -> A bytes of the RGBA output, one 1024-thread workgroup per
 // plane; runs after K2 and K3.

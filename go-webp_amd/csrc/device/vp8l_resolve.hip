@@ -125,10 +125,11 @@ __device__ unsigned long long g_k7_wave[kWaves][16];  // per wave (lane 0): the 
 // be null there: bad tokens then only resolve to 0, the serial path's rule); else stream
 // blockIdx.x of `descs`.  (Two instantiations: a descriptor chosen at run time between the two
 // loses its uniformity and the pointers' address space -- flat loads and spills.)
-// kAlpha: the 8-bit alpha streams whose filtered bytes K7 writes too (LLTokDesc::afilt; its own
-// instantiation, so the other streams' code is unchanged: measured, its mere presence cost c3a's
-// K7 1.7 %).
-template <bool kSingle, bool kW64, bool kAlpha>
+// kAlpha: the 8-bit alpha streams whose filtered bytes K7 writes too (LLTokDesc::afilt): 1 in
+// width-byte rows, 2 rows 1.. in band tiles (LLTokDesc::atile).  Instantiations of their own, so the
+// other streams' code is unchanged (measured: the alpha code's mere presence cost c3a's K7 1.7 %,
+// the tiles' c3av's 3 %).
+template <bool kSingle, bool kW64, int kAlpha>
 __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __restrict__ descs, LLTokDesc single,
                                                             int* err) {
   __shared__ uint64_t mask[kMaskWords];          // per key k: words k*W .. k*W+W-1, bit = rank in window
@@ -267,31 +268,43 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
     const uint32_t m = ((i4 >> 3) & 0x01010101u) * 0xffu;
     return (hi & m) | (lo & ~m);
   };
+  const int a_ncb = (D.a_width + 15) >> 4;
+  const __amdgpu_buffer_rsrc_t at_rs = __builtin_amdgcn_make_buffer_rsrc(
+      D.atile, 0, kAlpha == 2 ? ((D.a_height - 1 + 63) >> 6) * a_ncb * 1024 : 0, 0x00020000);
   auto store_alpha = [&](int pos0, const uint32_t* ov) {
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
     const int cw = D.a_cw, W = D.a_width, cb = D.a_cbits;
+    // byte (y, x): row-major in afilt, or (atile, rows >= 1) in its band tile
+    auto tile_off = [&](int y, int x) {
+      const int r = y - 1;
+      return (uint32_t)((((r >> 6) * a_ncb + (x >> 4)) << 10) + ((r & 63) << 4) + (x & 15));
+    };
     auto div_cw = [&](int p) {  // (a multiply-shift: the host's magic number, p < 2^28)
       return (int)(((uint64_t)(uint32_t)p * D.a_cw_m) >> (28 + D.a_cw_s));
     };
     const int yc = div_cw(pos0), xc = pos0 - yc * cw;
     const uint32_t g0 = (ov[0] >> 8) & 0xffu, g1 = (ov[1] >> 8) & 0xffu, g2 = (ov[2] >> 8) & 0xffu, g3 = (ov[3] >> 8) & 0xffu;
     const int x0 = xc << cb, nbytes = kPer << cb;
-    const uint32_t base = (uint32_t)(yc * W + x0);
+    const bool tiled = kAlpha == 2 && yc >= 1;
+    const __amdgpu_buffer_rsrc_t rs = tiled ? at_rs : af_rs;
+    // (tiles: the bytes of four coded pixels lie in one tile row, 16 for cbits 3 in each of two)
+    const uint32_t base = tiled ? tile_off(yc, x0) : (uint32_t)(yc * W + x0);
     const bool whole = xc + kPer <= cw && pos0 + kPer <= n && x0 + nbytes <= W;
     if (whole && cb == 0 && !D.a_pal && (base & 3) == 0) {
-      __builtin_amdgcn_raw_buffer_store_b32(g0 | g1 << 8 | g2 << 16 | g3 << 24, af_rs, base, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(g0 | g1 << 8 | g2 << 16 | g3 << 24, rs, base, 0, 0);
     } else if (whole && cb == 1 && (base & 7) == 0) {
       const uint32_t a = palq((g0 & 15) | (g0 >> 4) << 8 | (g1 & 15) << 16 | (g1 >> 4) << 24);
       const uint32_t b = palq((g2 & 15) | (g2 >> 4) << 8 | (g3 & 15) << 16 | (g3 >> 4) << 24);
-      __builtin_amdgcn_raw_buffer_store_b64(u32x2{a, b}, af_rs, base, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b64(u32x2{a, b}, rs, base, 0, 0);
     } else if (whole && cb == 2 && (base & 15) == 0) {
       auto q2 = [&](uint32_t g) { return palq((g & 3) | ((g >> 2) & 3) << 8 | ((g >> 4) & 3) << 16 | (g >> 6) << 24); };
-      __builtin_amdgcn_raw_buffer_store_b128(u32x4{q2(g0), q2(g1), q2(g2), q2(g3)}, af_rs, base, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4{q2(g0), q2(g1), q2(g2), q2(g3)}, rs, base, 0, 0);
     } else if (whole && cb == 3 && (base & 15) == 0) {
       auto q3 = [&](uint32_t t) { return palq((t & 1) | ((t >> 1) & 1) << 8 | ((t >> 2) & 1) << 16 | ((t >> 3) & 1) << 24); };
-      __builtin_amdgcn_raw_buffer_store_b128(u32x4{q3(g0), q3(g0 >> 4), q3(g1), q3(g1 >> 4)}, af_rs, base, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b128(u32x4{q3(g2), q3(g2 >> 4), q3(g3), q3(g3 >> 4)}, af_rs, base + 16u, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4{q3(g0), q3(g0 >> 4), q3(g1), q3(g1 >> 4)}, rs, base, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4{q3(g2), q3(g2 >> 4), q3(g3), q3(g3 >> 4)}, rs,
+                                             tiled ? tile_off(yc, x0 + 16) : base + 16u, 0, 0);
     } else {  // row ends, the stream's end, unaligned rows: byte by byte
       const int per = 1 << cb, bpp = 8 >> cb;
 #pragma unroll 1
@@ -306,7 +319,10 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
           if (x >= W) break;
           const uint32_t idx = (g >> (k * bpp)) & ((1u << bpp) - 1u);
           const uint32_t v = D.a_pal ? palq(idx) & 0xffu : g;
-          __builtin_amdgcn_raw_buffer_store_b8(v, af_rs, (uint32_t)(y * W + x), 0, 0);
+          if (kAlpha == 2 && y >= 1)
+            __builtin_amdgcn_raw_buffer_store_b8(v, at_rs, tile_off(y, x), 0, 0);
+          else
+            __builtin_amdgcn_raw_buffer_store_b8(v, af_rs, (uint32_t)(y * W + x), 0, 0);
         }
       }
     }
@@ -323,7 +339,7 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
       for (int j = 0; j < kPer; ++j)
         __builtin_amdgcn_raw_buffer_store_b32(ov[j], out_rs, pos0 + j < n ? 4u * (uint32_t)(pos0 + j) : kDropOff, 0, 0);
     }
-    if constexpr (kAlpha) {
+    if constexpr (kAlpha != 0) {
       if (pos0 < n) {
         const uint32_t ov[kPer] = {o.x, o.y, o.z, o.w};
         store_alpha(pos0, ov);
@@ -1059,26 +1075,29 @@ extern "C" int wg_debug_k7_stats(unsigned long long* out, int reset) {
 bool vp8l_resolve_w64(int cache_bits) { return cache_bits <= kW64Bits; }
 
 hipError_t launch_vp8l_resolve(const LLTokDesc* d_descs, const LLTokDesc* single, int n, int* d_err,
-                               hipStream_t stream, int n_w64, int n_alpha) {
+                               hipStream_t stream, int n_w64, int n_alpha, int n_tiled) {
   if (n <= 0) return hipSuccess;
   if (single) {
     if (vp8l_resolve_w64(single->cache_bits))
-      hipLaunchKernelGGL((vp8l_resolve_kernel<true, true, false>), dim3(1), dim3(kThreads), 0, stream, nullptr, *single, d_err);
+      hipLaunchKernelGGL((vp8l_resolve_kernel<true, true, 0>), dim3(1), dim3(kThreads), 0, stream, nullptr, *single, d_err);
     else
-      hipLaunchKernelGGL((vp8l_resolve_kernel<true, false, false>), dim3(1), dim3(kThreads), 0, stream, nullptr, *single,
+      hipLaunchKernelGGL((vp8l_resolve_kernel<true, false, 0>), dim3(1), dim3(kThreads), 0, stream, nullptr, *single,
                          d_err);
     return hipGetLastError();
   }
-  // the first n_alpha streams (64-word, with their alpha bytes), then the other n_w64 - n_alpha on
-  // the 64-word instantiation, the rest on the 32-word one
-  if (n_alpha > 0)
-    hipLaunchKernelGGL((vp8l_resolve_kernel<false, true, true>), dim3(n_alpha), dim3(kThreads), 0, stream, d_descs,
+  // the first n_alpha streams (64-word, with their alpha bytes: the first n_tiled of them into band
+  // tiles), then the other n_w64 - n_alpha on the 64-word instantiation, the rest on the 32-word one
+  if (n_tiled > 0)
+    hipLaunchKernelGGL((vp8l_resolve_kernel<false, true, 2>), dim3(n_tiled), dim3(kThreads), 0, stream, d_descs,
                        LLTokDesc{}, d_err);
+  if (n_alpha > n_tiled)
+    hipLaunchKernelGGL((vp8l_resolve_kernel<false, true, 1>), dim3(n_alpha - n_tiled), dim3(kThreads), 0, stream,
+                       d_descs + n_tiled, LLTokDesc{}, d_err);
   if (n_w64 > n_alpha)
-    hipLaunchKernelGGL((vp8l_resolve_kernel<false, true, false>), dim3(n_w64 - n_alpha), dim3(kThreads), 0, stream,
+    hipLaunchKernelGGL((vp8l_resolve_kernel<false, true, 0>), dim3(n_w64 - n_alpha), dim3(kThreads), 0, stream,
                        d_descs + n_alpha, LLTokDesc{}, d_err);
   if (n > n_w64)
-    hipLaunchKernelGGL((vp8l_resolve_kernel<false, false, false>), dim3(n - n_w64), dim3(kThreads), 0, stream,
+    hipLaunchKernelGGL((vp8l_resolve_kernel<false, false, 0>), dim3(n - n_w64), dim3(kThreads), 0, stream,
                        d_descs + n_w64, LLTokDesc{}, d_err);
   return hipGetLastError();
 }

@@ -107,8 +107,13 @@ struct LLTokDesc {
   uint32_t a_pg[4];                           // entry 4j + i in byte i of a_pg[j]
   uint32_t a_cw_m;                            // p / a_cw = (p * a_cw_m) >> (28 + a_cw_s) for p < 2^28
   int32_t a_cw_s;
+  // gradient-filtered planes: rows 1.. go to `atile` instead, as K4's wavefront reads them -- per
+  // 64-row band b (rows 1 + 64 b ..) and 16-column block c, a 1 KiB tile of 64 rows x 16 bytes,
+  // tile (b, c) at ((b * ceil(a_width / 16) + c) << 10), row r at r << 4.  Row 0 stays in afilt.
+  uint8_t* atile;
+  uint64_t pad2;
 };
-static_assert(sizeof(LLTokDesc) == 96, "LLTokDesc must be 96 bytes");
+static_assert(sizeof(LLTokDesc) == 112, "LLTokDesc must be 112 bytes");
 
 // One lossless (VP8L) frame for K3.  `coded` is the entropy-coded ARGB image from the host
 // stage; `stages` are its transforms in APPLICATION order (the reverse of bitstream order).
@@ -147,8 +152,12 @@ struct AlphaDesc {
   // pixel x in coded[x >> cbits]], or of the coded pixel itself when pal is null
   const uint32_t* coded;
   const uint32_t* pal;   // 1 << (8 >> cbits) ARGB entries (ExpandColorMap's padded map)
+  // gradient: the filtered rows 1.. in K7's band tiles (LLTokDesc::atile), or null (in `raw` /
+  // the plane, width-byte rows)
+  const uint8_t* tiles;
+  uint64_t pad0;
 };
-static_assert(sizeof(AlphaDesc) == 96, "AlphaDesc must be 96 bytes");
+static_assert(sizeof(AlphaDesc) == 112, "AlphaDesc must be 112 bytes");
 
 // One frame's YUV output for K8 (emit_yuva.hip, MODE_YUV / MODE_YUVA): compact planes of the
 // output window -- Y (width x height), U and V ((width + 1) / 2 x (height + 1) / 2), A (width x

@@ -54,7 +54,7 @@ struct FrameParse {
   bool cropped = false;
   // device layout (capi.cpp): offsets within the batch's plane and RGBA buffers
   size_t off_y = 0, off_u = 0, off_v = 0, off_cols = 0, off_gprog = 0, off_scratch = 0, off_rgba = 0;
-  size_t off_ascratch = 0, off_argba = 0, off_aplane = 0;
+  size_t off_ascratch = 0, off_argba = 0, off_aplane = 0, off_atile = 0;
   size_t off_yc = 0, off_uc = 0, off_vc = 0;
   int yc_stride = 0, uvc_stride = 0;
   bool wide = false;

@@ -123,7 +123,7 @@ def k7_isa(tmp_path_factory):
     if not (os.path.exists(HIPCC) and os.path.exists(os.path.join(LLVM, "llvm-objdump"))):
         pytest.skip("hipcc / llvm-objdump not available")
     funcs = _disassemble(str(tmp_path_factory.mktemp("k7isa")))
-    assert len(funcs) == 5, sorted(funcs)  # stage entry / batch, 32 / 64 mask words per key, + alpha bytes
+    assert len(funcs) == 6, sorted(funcs)  # stage entry / batch, 32 / 64 mask words per key, + alpha bytes (rows / tiles)
     return funcs
 
 
