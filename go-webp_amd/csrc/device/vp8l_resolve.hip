@@ -259,7 +259,10 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
   // itself without a map (ColorIndexInverseTransform, lossless.go:428-459; ExtractAlphaRows,
   // vp8l_dec.c.go:1462-1489 keeps the green).  The map's <= 16 green bytes sit in a_pg: v_perm
   // on four indices at once.  Rows of the coded image map to rows of the plane, so the bytes of
-  // four coded pixels within a row are contiguous: one 4- / 8- / 16- / 32-byte store when aligned.
+  // four coded pixels within a row are contiguous: one 4-byte (no map) or 8-byte (5..16 colours:
+  // two indices per coded pixel, libwebp's usual alpha map) store when aligned; maps of 2..4
+  // colours, row ends and unaligned rows byte by byte (kept small: the kernel's code size shows
+  // in its time).
   const __amdgpu_buffer_rsrc_t af_rs =
       __builtin_amdgcn_make_buffer_rsrc(D.afilt, 0, D.afilt ? D.a_width * D.a_height : 0, 0x00020000);
   auto palq = [&](uint32_t i4) {  // four map indices (bytes of i4) -> their green bytes
@@ -297,33 +300,20 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
       const uint32_t a = palq((g0 & 15) | (g0 >> 4) << 8 | (g1 & 15) << 16 | (g1 >> 4) << 24);
       const uint32_t b = palq((g2 & 15) | (g2 >> 4) << 8 | (g3 & 15) << 16 | (g3 >> 4) << 24);
       __builtin_amdgcn_raw_buffer_store_b64(u32x2{a, b}, rs, base, 0, 0);
-    } else if (whole && cb == 2 && (base & 15) == 0) {
-      auto q2 = [&](uint32_t g) { return palq((g & 3) | ((g >> 2) & 3) << 8 | ((g >> 4) & 3) << 16 | (g >> 6) << 24); };
-      __builtin_amdgcn_raw_buffer_store_b128(u32x4{q2(g0), q2(g1), q2(g2), q2(g3)}, rs, base, 0, 0);
-    } else if (whole && cb == 3 && (base & 15) == 0) {
-      auto q3 = [&](uint32_t t) { return palq((t & 1) | ((t >> 1) & 1) << 8 | ((t >> 2) & 1) << 16 | ((t >> 3) & 1) << 24); };
-      __builtin_amdgcn_raw_buffer_store_b128(u32x4{q3(g0), q3(g0 >> 4), q3(g1), q3(g1 >> 4)}, rs, base, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b128(u32x4{q3(g2), q3(g2 >> 4), q3(g3), q3(g3 >> 4)}, rs,
-                                             tiled ? tile_off(yc, x0 + 16) : base + 16u, 0, 0);
-    } else {  // row ends, the stream's end, unaligned rows: byte by byte
+    } else {  // row ends, the stream's end, unaligned rows: byte by byte (one flat loop: small code)
       const int per = 1 << cb, bpp = 8 >> cb;
 #pragma unroll 1
-      for (int j = 0; j < kPer; ++j) {
-        const int p = pos0 + j;
-        if (p >= n) break;
-        const int y = div_cw(p), xq = p - y * cw;
-        const uint32_t g = ((j == 0 ? ov[0] : j == 1 ? ov[1] : j == 2 ? ov[2] : ov[3]) >> 8) & 0xffu;
-#pragma unroll 1
-        for (int k = 0; k < per; ++k) {
-          const int x = (xq << cb) + k;
-          if (x >= W) break;
-          const uint32_t idx = (g >> (k * bpp)) & ((1u << bpp) - 1u);
-          const uint32_t v = D.a_pal ? palq(idx) & 0xffu : g;
-          if (kAlpha == 2 && y >= 1)
-            __builtin_amdgcn_raw_buffer_store_b8(v, at_rs, tile_off(y, x), 0, 0);
-          else
-            __builtin_amdgcn_raw_buffer_store_b8(v, af_rs, (uint32_t)(y * W + x), 0, 0);
-        }
+      for (int i = 0; i < nbytes; ++i) {
+        const int j = i >> cb, k = i & (per - 1), p = pos0 + j;
+        const int y = div_cw(p), x = ((p - y * cw) << cb) + k;
+        const uint32_t w = j == 0 ? ov[0] : j == 1 ? ov[1] : j == 2 ? ov[2] : ov[3];
+        const uint32_t g = (w >> 8) & 0xffu;
+        const uint32_t idx = (g >> (k * bpp)) & ((1u << bpp) - 1u);
+        const uint32_t v = D.a_pal ? palq(idx) & 0xffu : g;
+        const bool t = kAlpha == 2 && y >= 1;
+        // (past the stream or the row: an offset past the buffer, dropped)
+        const uint32_t off = p >= n || x >= W ? 0x80000000u : t ? tile_off(y, x) : (uint32_t)(y * W + x);
+        __builtin_amdgcn_raw_buffer_store_b8(v, t ? at_rs : af_rs, off, 0, 0);
       }
     }
   };
