@@ -321,6 +321,8 @@ def alpha_pattern(H, W, seed, kind):
         a = rng.integers(0, 40, (H, W)) * 6
     elif kind == "many":  # 61 levels: a palette of more than 16 colours, one pixel per coded pixel
         a = ((xx * 2 + yy) % 61) * 4
+    elif kind == "l12":  # 12 levels: a palette of 5..16 colours, two pixels per coded pixel
+        a = ((xx // 5 + yy // 3) % 12) * 20
     else:
         a = rng.integers(0, 256, (H, W))
     return np.concatenate([img, (a % 256).astype(np.uint8)[..., None]], -1)
@@ -828,6 +830,19 @@ ALPHA_CASES_R5 = [
     ("a_ll_rl_none_61x29", lambda: alpha_pattern(29, 61, 49, "rl"), {"alpha_filtering": 0}, (1, 0)),
     ("a_ll_rl_h_64x33", lambda: alpha_pattern(33, 64, 50, "rl"), {"alpha_filtering": 0, "set_filter": 1}, (1, 1)),
 ]
+# section alpha_r6 (added to "alpha"): 8-bit streams under vertical / gradient, whose filtered bytes
+# K7 writes itself (into the plane; gradient rows into band tiles) -- maps of 2, 4 and 12 colours
+# (8, 4, 2 pixels per coded pixel) and none, widths off the 8- and 16-byte grid, several bands
+ALPHA_CASES_R6 = [
+    ("a_ll_bin_g_70x150", lambda: alpha_pattern(150, 70, 51, "bin"), {"alpha_filtering": 0, "set_filter": 3}, (1, 3)),
+    ("a_ll_lv_g_90x130", lambda: alpha_pattern(130, 90, 52, "lv"), {"alpha_filtering": 0, "set_filter": 3}, (1, 3)),
+    ("a_ll_l12_g_88x140", lambda: alpha_pattern(140, 88, 53, "l12"), {"alpha_filtering": 0, "set_filter": 3}, (1, 3)),
+    ("a_ll_l12_g_256x70", lambda: alpha_pattern(70, 256, 54, "l12"), {"alpha_filtering": 0, "set_filter": 3}, (1, 3)),
+    ("a_ll_rl_g_61x100", lambda: alpha_pattern(100, 61, 55, "rl"), {"alpha_filtering": 0, "set_filter": 3}, (1, 3)),
+    ("a_ll_l12_v_88x50", lambda: alpha_pattern(50, 88, 56, "l12"), {"alpha_filtering": 0, "set_filter": 2}, (1, 2)),
+    ("a_ll_rl_v_61x40", lambda: alpha_pattern(40, 61, 57, "rl"), {"alpha_filtering": 0, "set_filter": 2}, (1, 2)),
+    ("a_ll_l12_none_72x30", lambda: alpha_pattern(30, 72, 58, "l12"), {"alpha_filtering": 0}, (1, 0)),
+]
 
 BENCH_CASES = [
     # name, H, W, seeds, kwargs, generator  
@@ -860,14 +875,16 @@ def main(argv):
     """argv: sections to (re)generate among lossy, lossy_extra, lossless, alpha, modes, anim, bench (default: all);
     the manifest entries of the other sections are kept."""
     sections = set(argv) or {"lossy", "lossy_extra", "lossless", "alpha", "modes", "yuv", "anim", "bench", "bench_c5x",
-                             "bench_c3s", "bench_c3a", "bench_anim", "bench_modes", "fuzz", "alpha_r5", "bench_yuva", "bench_c3ag"}
+                             "bench_c3s", "bench_c3a", "bench_anim", "bench_modes", "fuzz", "alpha_r5", "alpha_r6", "bench_yuva",
+                             "bench_c3ag"}
     os.makedirs(os.path.join(HERE, "lossy"), exist_ok=True)
     os.makedirs(os.path.join(HERE, "lossless"), exist_ok=True)
     os.makedirs(os.path.join(HERE, "bench"), exist_ok=True)
     mpath = os.path.join(HERE, "manifest.json")
     manifest = json.load(open(mpath)) if os.path.exists(mpath) else {}
     manifest["libwebp"] = "1.6.0 (Pillow 12.2.0 bundle, plain-C DSP)"
-    for sec in sections - {"bench_c5x", "bench_c3s", "bench_c3a", "bench_modes", "alpha_r5", "bench_yuva", "bench_c3ag"}:  # (these add)
+    for sec in sections - {"bench_c5x", "bench_c3s", "bench_c3a", "bench_modes", "alpha_r5", "alpha_r6", "bench_yuva",
+                           "bench_c3ag"}:  # (these add)
         manifest[sec] = {}
     manifest.setdefault("alpha", {})
     manifest.setdefault("bench", {})
@@ -898,7 +915,8 @@ def main(argv):
         print(name, len(data), flush=True)
     os.makedirs(os.path.join(HERE, "alpha"), exist_ok=True)
     for name, fn, kw, want in (ALPHA_CASES if "alpha" in sections else []) + \
-            (ALPHA_CASES_R5 if sections & {"alpha", "alpha_r5"} else []):
+            (ALPHA_CASES_R5 if sections & {"alpha", "alpha_r5"} else []) + \
+            (ALPHA_CASES_R6 if sections & {"alpha", "alpha_r6"} else []):
         img = fn()
         kw = dict(kw)
         filt = kw.pop("set_filter", None)
