@@ -6,7 +6,7 @@ TAG=${TAG:-r01}
 WL=${WL:-c3}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
-BENCH="python3 bench.py --workload $WL --steps ${STEPS:-3} --warmup 1 --no-cpu-baseline --no-e2e"
+BENCH="python3 bench.py --workload $WL --steps ${STEPS:-3} --warmup ${WARMUP:-1} --no-cpu-baseline --no-e2e"
 run() {  # run <name> <timeout> <rocprofv3 args...>
   local name=$1 to=$2; shift 2
   echo "=== $name"
@@ -15,7 +15,7 @@ run() {  # run <name> <timeout> <rocprofv3 args...>
   echo "=== $name rc=$rc"; tail -n 3 $OUT/$name.log
   if [ $rc -ne 0 ]; then exit $rc; fi
 }
-run trace 240 --kernel-trace --stats
+[ -z "$PMC_ONLY" ] && run trace 240 --kernel-trace --stats
 if [ -n "$PMC1" ]; then run pmc1 240 --pmc $PMC1; fi
 if [ -n "$PMC2" ]; then run pmc2 240 --pmc $PMC2; fi
 if [ -n "$PMC3" ]; then run pmc3 240 --pmc $PMC3; fi
