@@ -112,6 +112,65 @@ func Decode(r io.Reader) (image.Image, error) {
 	return img, nil
 }
 
+// YUVA holds the planes of a MODE_YUV / MODE_YUVA decode (WebPYUVABuffer, buffer.go:17-25): Y
+// (W x H), U and V ((W+1)/2 x (H+1)/2) and, with alpha requested, A (W x H; 0xff for frames
+// without ALPH).  The samples are VP8's (studio-swing BT.601), not image.YCbCr's JFIF ones, so
+// they are returned as planes rather than as an image.YCbCr whose At() would convert them with
+// the wrong matrix.
+type YUVA struct {
+	W, H                           int
+	Y, U, V, A                     []byte
+	YStride, UVStride, AStride     int
+}
+
+// DecodeYUVA decodes one frame to its Y / U / V (/ A) planes on the GPU (wg_decode_yuv_into:
+// WebPDecode with config.output.colorspace MODE_YUV = 11 or MODE_YUVA = 12, webp.go:870-909).
+// Lossy frames give their reconstructed planes; lossless ones libwebp 1.6.0's ARGB -> YUV(A)
+// conversion.
+func DecodeYUVA(r io.Reader, withAlpha bool) (*YUVA, error) {
+	data, err := io.ReadAll(r)
+	if err != nil {
+		return nil, err
+	}
+	cfg, err := decodeConfig(data)
+	if err != nil {
+		return nil, err
+	}
+	w, h := cfg.Width, cfg.Height
+	uw, uh := (w+1)/2, (h+1)/2
+	out := &YUVA{W: w, H: h, Y: make([]byte, w*h), U: make([]byte, uw*uh), V: make([]byte, uw*uh),
+		YStride: w, UVStride: uw}
+	var opt C.wg_decoder_options
+	opt.colorspace = 11
+	var buf C.wg_yuva_buffer
+	// (Go memory for the duration of the call: pinned, the struct holding its pointers is C's)
+	var pin runtime.Pinner
+	defer pin.Unpin()
+	pin.Pin(&out.Y[0])
+	pin.Pin(&out.U[0])
+	pin.Pin(&out.V[0])
+	buf.y, buf.u, buf.v = (*C.uint8_t)(&out.Y[0]), (*C.uint8_t)(&out.U[0]), (*C.uint8_t)(&out.V[0])
+	buf.y_stride, buf.u_stride, buf.v_stride = C.int32_t(w), C.int32_t(uw), C.int32_t(uw)
+	buf.y_size, buf.u_size, buf.v_size = C.size_t(len(out.Y)), C.size_t(len(out.U)), C.size_t(len(out.V))
+	if withAlpha {
+		opt.colorspace = 12
+		out.A, out.AStride = make([]byte, w*h), w
+		pin.Pin(&out.A[0])
+		buf.a, buf.a_stride, buf.a_size = (*C.uint8_t)(&out.A[0]), C.int32_t(w), C.size_t(len(out.A))
+	}
+	cbuf := (*C.wg_yuva_buffer)(C.malloc(C.size_t(unsafe.Sizeof(buf))))
+	defer C.free(unsafe.Pointer(cbuf))
+	*cbuf = buf
+	copt := (*C.wg_decoder_options)(C.malloc(C.size_t(unsafe.Sizeof(opt))))
+	defer C.free(unsafe.Pointer(copt))
+	*copt = opt
+	p, n := cBytes(data)
+	if err := statusErr(C.wg_decode_yuv_into(p, n, copt, cbuf), "DecodeYUVA"); err != nil {
+		return nil, err
+	}
+	return out, nil
+}
+
 // SetDevice selects the HIP device behind Decode (wg_set_default_device).
 func SetDevice(device int) error {
 	return statusErr(C.wg_set_default_device(C.int(device)), "SetDevice")
