@@ -118,9 +118,9 @@ func Decode(r io.Reader) (image.Image, error) {
 // they are returned as planes rather than as an image.YCbCr whose At() would convert them with
 // the wrong matrix.
 type YUVA struct {
-	W, H                           int
-	Y, U, V, A                     []byte
-	YStride, UVStride, AStride     int
+	W, H                       int
+	Y, U, V, A                 []byte
+	YStride, UVStride, AStride int
 }
 
 // DecodeYUVA decodes one frame to its Y / U / V (/ A) planes on the GPU (wg_decode_yuv_into:
@@ -149,14 +149,16 @@ func DecodeYUVA(r io.Reader, withAlpha bool) (*YUVA, error) {
 	pin.Pin(&out.Y[0])
 	pin.Pin(&out.U[0])
 	pin.Pin(&out.V[0])
-	buf.y, buf.u, buf.v = (*C.uint8_t)(&out.Y[0]), (*C.uint8_t)(&out.U[0]), (*C.uint8_t)(&out.V[0])
+	buf.y = (*C.uint8_t)(unsafe.Pointer(&out.Y[0]))
+	buf.u = (*C.uint8_t)(unsafe.Pointer(&out.U[0]))
+	buf.v = (*C.uint8_t)(unsafe.Pointer(&out.V[0]))
 	buf.y_stride, buf.u_stride, buf.v_stride = C.int32_t(w), C.int32_t(uw), C.int32_t(uw)
 	buf.y_size, buf.u_size, buf.v_size = C.size_t(len(out.Y)), C.size_t(len(out.U)), C.size_t(len(out.V))
 	if withAlpha {
 		opt.colorspace = 12
 		out.A, out.AStride = make([]byte, w*h), w
 		pin.Pin(&out.A[0])
-		buf.a, buf.a_stride, buf.a_size = (*C.uint8_t)(&out.A[0]), C.int32_t(w), C.size_t(len(out.A))
+		buf.a, buf.a_stride, buf.a_size = (*C.uint8_t)(unsafe.Pointer(&out.A[0])), C.int32_t(w), C.size_t(len(out.A))
 	}
 	cbuf := (*C.wg_yuva_buffer)(C.malloc(C.size_t(unsafe.Sizeof(buf))))
 	defer C.free(unsafe.Pointer(cbuf))
