@@ -485,22 +485,42 @@ __global__ void __launch_bounds__(kThreads) alpha_kernel(const AlphaDesc* __rest
 #endif
       const int sh = 16 - ((-lane) & 15), sq = sh >> 2, sr = sh & 3;
       uint32_t prv[4] = {0u, 0u, 0u, 0u}, cur[4] = {0u, 0u, 0u, 0u};
-      auto emit = [&](int sg) {
-        const int x0 = sg - lane, B = x0 - (x0 & 15);
-        uint32_t o[4];
-        window16(prv[0], prv[1], prv[2], prv[3], cur[0], cur[1], cur[2], cur[3], sq, sr, o);
-#ifdef WG_ABL_GRAD_NOSTORE  // (measurement only: output wrong)
-        if (row_ok && B >= 0 && B < W && F.width == 12345) {
-#else
-        if (row_ok && B >= 0 && B < W) {
-#endif
-          if (B + 16 <= W && st16) {
-            *reinterpret_cast<gptr<u32x4>>(prow + B) = u32x4{o[0], o[1], o[2], o[3]};
-          } else {
+      // A group's 16 outputs as the aligned block [B, B + 16) of the lane's row (B = x0 rounded down
+      // to 16, x0 = 16 g - lane), kept in slot g mod 4 (static: the loop's four stages); when B is
+      // 48 mod 64 the 64-byte segment [B - 48, B + 16) is complete and leaves as four 16-byte stores
+      // back to back -- whole 64-byte pieces of lines, 16 lanes a group -- instead of one 16-byte
+      // piece per row and group (c3ag: the L2 wrote the part-written lines back at 2.9x the bytes).
+      // Every lane issues the four stores (lanes without a due, whole block store past the buffer:
+      // dropped), so each stage has a fixed count of vector-memory operations for the counted vmcnt.
+      // Blocks after a lane's last segment go out after the loop (flush); row ends byte by byte.
+      uint32_t os[4][4];
+      const int cl = (lane + 15) >> 4;  // B(g) = 16 (g - cl)
+      auto block_whole = [&](int Bb) { return row_ok && Bb >= 0 && Bb + 16 <= W && st16; };
+      auto block_bytes = [&](int Bb, const uint32_t* o) {  // (a block not stored whole: its bytes in the row)
+        if (row_ok && Bb >= 0 && Bb < W && !block_whole(Bb)) {
 #pragma unroll
-            for (int k = 0; k < 16; ++k)
-              if (B + k < W) prow[B + k] = (uint8_t)(o[k >> 2] >> (8 * (k & 3)));
-          }
+          for (int i = 0; i < 16; ++i)
+            if (Bb + i < W) prow[Bb + i] = (uint8_t)(o[i >> 2] >> (8 * (i & 3)));
+        }
+      };
+      auto emit = [&](int sg, int k) {
+        const int x0 = sg - lane, B = x0 - (x0 & 15);
+        window16(prv[0], prv[1], prv[2], prv[3], cur[0], cur[1], cur[2], cur[3], sq, sr, os[k]);
+        const bool due = (B & 63) == 48;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int Bi = B - 48 + 16 * i;
+          const uint32_t* o = os[(k + 1 + i) & 3];
+#ifdef WG_ABL_GRAD_NOSTORE  // (measurement only: output wrong)
+          const uint32_t voff = 0x80000000u;
+#else
+          const uint32_t voff = due && block_whole(Bi) ? (uint32_t)(y * W + Bi) : 0x80000000u;
+#endif
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4{o[0], o[1], o[2], o[3]}, psrc, voff, 0, 0);
+        }
+        if (due) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) block_bytes(B - 48 + 16 * i, os[(k + 1 + i) & 3]);
         }
         stored = row_ok ? max(0, min(W, B + 16)) : W;
         // the last row's block into the ring, once the band below has read what it replaces
@@ -510,10 +530,28 @@ __global__ void __launch_bounds__(kThreads) alpha_kernel(const AlphaDesc* __rest
                                            : (((uint32_t)(bnd + 1) << 16) | (uint32_t)(Bl - kRing + 16));
           // (the slot's previous reader, band b - 15, exists from b = 16 on: band 0 reads row0)
           if (bnd >= 16 || Bl >= kRing) spin(cprog + slot, need);
-          if (lane == 63) *reinterpret_cast<u32x4*>(&tring[slot][Bl & (kRing - 1)]) = u32x4{o[0], o[1], o[2], o[3]};
+          if (lane == 63)
+            *reinterpret_cast<u32x4*>(&tring[slot][Bl & (kRing - 1)]) = u32x4{os[k][0], os[k][1], os[k][2], os[k][3]};
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) prv[j] = cur[j];
+      };
+      // after the loop (gf = the last group emitted): slot j holds group g_j, the latest g <= gf with
+      // g = j mod 4; its block went out with a segment iff a due group (g - cl = 3 mod 4) lies in
+      // [g_j, g_j + 3] at or before gf -- else it goes out now
+      auto flush = [&](int gf) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int gj = gf - ((gf - j) & 3);
+          const int tj = gj + ((cl + 3 - gj) & 3);
+          if (gj >= 0 && tj > gf) {
+            const int Bj = 16 * (gj - cl);
+            if (block_whole(Bj))
+              __builtin_amdgcn_raw_buffer_store_b128(u32x4{os[j][0], os[j][1], os[j][2], os[j][3]}, psrc,
+                                                     (uint32_t)(y * W + Bj), 0, 0);
+            block_bytes(Bj, os[j]);
+          }
+        }
       };
       // lane 0's T for group sg (lanes j < 16: column sg + j of the row above; past the row's end
       // a clamped column, unused), once the band above has it in its ring
@@ -560,19 +598,28 @@ __global__ void __launch_bounds__(kThreads) alpha_kernel(const AlphaDesc* __rest
       load_group(16, 1);
       load_group(32, 2);
       int last = 0;  // the last group's first step
-      // stage: issue group sg + 48's block, read T, wait for group sg's block (issued three
-      // stages ago: the two stages' blocks since and this one's -- vmcnt(3) leaves only those and
-      // younger stores in flight), the 16 steps, the stores
+      // stage: issue group sg + 48's block, read T, wait for group sg's block, the 16 steps, the
+      // stores.  Issued after group sg's block: its stage's four stores, then a block and four stores
+      // per stage since, and this stage's block -- vmcnt(15) (the first three stages: 3, fewer
+      // stores behind them) leaves exactly those in flight.  (Byte stores at row ends only add
+      // younger operations: the wait then covers a few more, never fewer.)  The stage past the last
+      // group emits the row's tail only (its last group's bytes) and ends the loop.
       auto stage = [&](int sg, int k) -> bool {
-        load_group(sg + 48, (k + 3) & 3);
-        const uint32_t t = read_t(sg);
-        asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-        const u32x4 q = *reinterpret_cast<const u32x4*>(&dma[wave][k][4 * lane]);
-        run_group(sg, q, t);
-        emit(sg);
-        publish();
+        const bool work = sg < steps;
+        if (work) {
+          load_group(sg + 48, (k + 3) & 3);
+          const uint32_t t = read_t(sg);
+          if (sg < 48)
+            asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+          else
+            asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
+          const u32x4 q = *reinterpret_cast<const u32x4*>(&dma[wave][k][4 * lane]);
+          run_group(sg, q, t);
+        }
+        emit(sg, k);
+        if (work) publish();
         last = sg;
-        return sg + 16 >= steps;
+        return !work;
       };
       for (int sg = 0;; sg += 64) {
         if (stage(sg, 0)) break;
@@ -580,7 +627,7 @@ __global__ void __launch_bounds__(kThreads) alpha_kernel(const AlphaDesc* __rest
         if (stage(sg + 32, 2)) break;
         if (stage(sg + 48, 3)) break;
       }
-      emit(last + 16);  // (the row's columns after its last full block: bytes of the last group)
+      flush(last >> 4);
       const uint32_t done = (uint32_t)__builtin_amdgcn_readlane(stored, rows - 1);
       if (lane == 0) {
         __hip_atomic_store(gprog + slot, ((uint32_t)bnd << 16) | done, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
