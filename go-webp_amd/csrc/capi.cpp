@@ -174,7 +174,7 @@ struct wg_ctx {
   // the pipelined decode (wg_decode_rgba_batch): a second staging arena, and two work streams
   // (kernels + download of alternate chunks) next to `stream`, which carries every chunk's
   // upload -- so an upload never queues behind an earlier chunk's download
-  std::unique_ptr<wg::StagingArena> arena_ring[2];  // with `arena`, a ring of three
+  std::unique_ptr<wg::StagingArena> arena_ring[3];  // with `arena`, a ring of four
   hipStream_t work[2] = {nullptr, nullptr};
   // K7 beside K1 / K2 (wg_batch_run: small batches whose grids fit on the chip together)
   hipStream_t side = nullptr;
@@ -1773,11 +1773,15 @@ int decode_pipelined(wg_ctx* ctx, const uint8_t* const* data, const size_t* size
         return WG_STATUS_OUT_OF_MEMORY;
       }
   }
-  // staging arenas in a ring of three: chunk k parses into arena k % 3 once chunk k - 3's upload
-  // from it has completed
-  constexpr int kRing = 3;
+  // staging arenas in a ring of four: chunk k parses into arena k % 4 once chunk k - 4's upload
+  // from it has completed (three left the host stage waiting 5-11 ms per 256-frame c3 call for the
+  // device thread, which queues a chunk's upload only after retiring the chunk two before it; with
+  // four the waits are gone and the drain grows by less: 7.97k -> 8.10k MPix/s, same call; a fourth
+  // halving of the last chunks measured no better)
+  constexpr int kRing = 4;
   wg::StagingArena* arenas[kRing] = {ctx->arena.get(), K > 1 ? ctx->arena_ring[0].get() : nullptr,
-                                     K > 1 ? ctx->arena_ring[1].get() : nullptr};
+                                     K > 1 ? ctx->arena_ring[1].get() : nullptr,
+                                     K > 1 ? ctx->arena_ring[2].get() : nullptr};
   // one chunk: everything on the context stream; else uploads on it, the rest on a work stream
   hipStream_t streams[2] = {K > 1 ? ctx->work[0] : ctx->stream, K > 1 ? ctx->work[1] : ctx->stream};
   std::vector<PipeChunk> ch((size_t)K);
