@@ -67,6 +67,7 @@ constexpr int kSlots = 2048;              // 1 << MAX_CACHE_BITS (format_constan
 constexpr int kMaskWords = 8192;          // 64 KB of 64-bit rank masks, split over the keys
 constexpr int kMaxW = 32;                 // mask words per key (the summary is 32 bits)
 constexpr int kW64Bits = 7;               // kW64: cache_bits <= 7 (<= 128 keys x 64 words)
+constexpr int kKeysW64 = 1 << kW64Bits;
 constexpr int kMaxRounds = 32;
 constexpr uint8_t kKnown = 1, kPendCopy = 2, kPendLookup = 3;
 constexpr uint32_t kDropOff = 0xffffffc0u;  // buffer offset past any stream: loads return 0
@@ -145,8 +146,8 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
   // block's array is not the loads' target)
   __shared__ __attribute__((aligned(16))) uint32_t val0[kBlock];
   __shared__ __attribute__((aligned(16))) uint32_t val1[kBlock];
-  __shared__ int16_t ref[kBlock];                // pending copy: source pointer (pointer jumping)
-  __shared__ uint8_t st[kBlock];                 // kKnown / kPendCopy / kPendLookup
+  __shared__ __attribute__((aligned(16))) int16_t ref[kBlock];  // pending copy: source pointer (pointer jumping)
+  __shared__ __attribute__((aligned(16))) uint8_t st[kBlock];  // kKnown / kPendCopy / kPendLookup
   __shared__ __attribute__((aligned(16))) uint32_t wsum[kWaves];  // updaters per wave of the block
   __shared__ int first_pend[2];                  // per round parity: first pending copy (local)
   // this window goes serial; one flag per block parity: with no barrier at a block's end, a
@@ -530,6 +531,8 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
       ps |= code << (2 * j) | (~kind & 1u) << (8 + j);  // updaters: kinds 0 (literal) and 2 (copy)
       nearm |= (uint32_t)(is_copy & !inb & !farc) << j;
       v[j] = vcur[wave * kWavePx + 64 * j + lane];
+      // (kW64: a lookup's value register and vcur entry hold its key until it resolves)
+      if (kW64 && is_cache) v[j] = pl & (uint32_t)(nkeys - 1) & (kKeysW64 - 1);
       aux[j] = is_cache ? pl & (kSlots - 1) : pl;
     }
     K7_T(8);
@@ -618,7 +621,7 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
     // step 1, the last reader of vprv, since the rank barrier)
     load_lits(tk_nxt, vprv);
     // in-block copies: sources and every pixel's state for the pointer jumping (rare in C5)
-    if (blk_pc) {
+    if (blk_pc || (kW64 && blk_pl)) {
       // Runs of distance-1 copies (run-length coding, CopyBlock32b with dist 1: every pixel of the
       // run equals the one before it) point straight at their root -- the last pixel before them
       // that is not such a copy -- from a block-wide max-scan of root positions, so the pointer
@@ -653,12 +656,251 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
       *reinterpret_cast<uint2*>(&ref[li0]) = make_uint2(rfw[0], rfw[1]);
       *reinterpret_cast<uint32_t*>(&st[li0]) = stw;
     }
+    int serial_from = kBlock;  // local pixel where the serial path takes over
+    if constexpr (kW64) {
+      // ---- Dense blocks (the small-cache instantiation: alpha planes and flat content, nearly
+      //      every pixel a copy and a few lookups).  No ranks and no masks:
+      //  R  pointer jumping over the in-block copies with the lookups as roots: every copy ends
+      //     known or pointing at a lookup -- whose value is not known yet, but whose hash is: a
+      //     slot only ever holds values of its own hash (the one exception, a never-written slot
+      //     k != 0, sends the block to the serial path), so the lookup and the copies of it insert
+      //     under its key.
+      //  H  every inserting pixel's hash is now known: per wave and key, the last such pixel.
+      //  L  a lookup's source is the last pixel before it that inserts under its key (its own
+      //     wave's lanes, else the earlier waves' H entries) -- or, with none in the block, the
+      //     slot as the blocks before left it.
+      //  J  pointer jumping again until every pixel is known (lookups and copies of lookups).
+      //  T  each key's last pixel in the block writes its slot.
+      uint32_t* const lastp = reinterpret_cast<uint32_t*>(mask);  // [wave][key]: 1 + local pixel, 0 none
+      static_assert(sizeof(mask) >= kWaves * kKeysW64 * 4, "lastp");
+      // One pointer-jumping step over my pending copies (their sources gathered first, as
+      // independent LDS reads; the hand-off protocol of the rounds below): a known source gives
+      // its value, a pending copy its link, a pending lookup stops the copy.  The four slots'
+      // values, states and links go back as one store each (the values before the states).
+      // Returns whether a copy of mine took a link.
+      auto jump_round = [&]() -> bool {
+        uint32_t pcm = 0;
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) pcm |= (uint32_t)(pk(ps, j) == kPC) << j;
+        if (!__any(pcm != 0)) return false;
+        bool still = false;
+        if (pcm) {
+          const uint2 rw = *reinterpret_cast<const uint2*>(&ref[li0]);
+          int rv[kPer] = {(int16_t)(rw.x & 0xffffu), (int16_t)(rw.x >> 16), (int16_t)(rw.y & 0xffffu),
+                          (int16_t)(rw.y >> 16)};
+          int src[kPer];
+          uint32_t ss[kPer], xs[kPer];
+          int nref[kPer];
+          // four consecutive sources from an aligned pixel (copies at a distance of a multiple of
+          // four: the row above in the alpha planes): one vector read per array -- the strided
+          // scalar reads of the lanes conflict in the LDS banks
+          const bool vec = pcm == 0xfu && (rv[0] & 3) == 0 && rv[1] == rv[0] + 1 && rv[2] == rv[0] + 2 && rv[3] == rv[0] + 3;
+          if (vec) {
+            // (one asm block, states first: as plain reads the compiler merged them with the scalar
+            // path's into reads of a merged address, whose lost alias information made the waitcnt
+            // pass wait vmcnt(0) for the next block's staged literals at every round)
+            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+            typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+            uint32_t s4;
+            u32x4 x4;
+            u32x2 r4;
+            asm volatile("ds_read_b32 %0, %3\n\tds_read_b128 %1, %4\n\tds_read_b64 %2, %5\n\ts_waitcnt lgkmcnt(0)"
+                         : "=&v"(s4), "=&v"(x4), "=&v"(r4)
+                         : "v"(lds_addr(&st[rv[0]])), "v"(lds_addr(&vcur[rv[0]])), "v"(lds_addr(&ref[rv[0]]))
+                         : "memory");
+            ss[0] = s4 & 0xffu, ss[1] = (s4 >> 8) & 0xffu, ss[2] = (s4 >> 16) & 0xffu, ss[3] = s4 >> 24;
+            xs[0] = x4.x, xs[1] = x4.y, xs[2] = x4.z, xs[3] = x4.w;
+            nref[0] = (int16_t)(r4.x & 0xffffu), nref[1] = (int16_t)(r4.x >> 16), nref[2] = (int16_t)(r4.y & 0xffffu),
+            nref[3] = (int16_t)(r4.y >> 16);
+          } else {
+#pragma unroll
+            for (int j = 0; j < kPer; ++j) src[j] = (pcm >> j) & 1u ? rv[j] : li0 + j;
+#pragma unroll
+            for (int j = 0; j < kPer; ++j) ss[j] = st[src[j]];
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int j = 0; j < kPer; ++j) xs[j] = vcur[src[j]];
+#pragma unroll
+            for (int j = 0; j < kPer; ++j) nref[j] = ref[src[j]];
+          }
+          uint32_t stw = 0;
+#pragma unroll
+          for (int j = 0; j < kPer; ++j) {
+            if ((pcm >> j) & 1u) {
+              if (ss[j] == kKnown) {
+                set_known(ps, j);
+                v[j] = xs[j];
+              } else if (ss[j] == kPendCopy) {
+                rv[j] = nref[j];  // (a stale or fresh link: both lie on the chain)
+                still = true;
+              }
+            }
+            const uint32_t c = pk(ps, j);
+            stw |= (uint32_t)(c == kPC ? kPendCopy : c == kPL ? kPendLookup : kKnown) << (8 * j);
+          }
+          *reinterpret_cast<uint4*>(&vcur[li0]) = make_uint4(v[0], v[1], v[2], v[3]);
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          *reinterpret_cast<uint32_t*>(&st[li0]) = stw;
+          *reinterpret_cast<uint2*>(&ref[li0]) =
+              make_uint2((uint32_t)(uint16_t)rv[0] | (uint32_t)rv[1] << 16, (uint32_t)(uint16_t)rv[2] | (uint32_t)rv[3] << 16);
+        }
+        return still;
+      };
+      auto jump_rounds = [&]() {
+        for (int r = 0;; ++r) {
+          if (r == kMaxRounds) {  // (uniform)
+            K7_COUNT(10, 1);
+            slow[b & 1] = 1;
+            break;
+          }
+          K7_COUNT(2, 1);
+          if (!sync_or(jump_round())) break;
+        }
+      };
+      // R (the setup's ref / st stores are complete first)
+      if (blk_pc) {
+        bar();
+        jump_rounds();
+      }
+      K7_T(5);
+      // H: the hash each pixel inserts under (known updaters: of the value; lookups and copies
+      // of one: the key), and per wave and key the last pixel -- the lanes of one key combined
+      // while a key still gathers four lanes (a dense wave is mostly one key), the rest by ds_max
+      uint32_t hk[kPer], hm = 0;
+      if (nkeys) {
+        uint32_t pcm = 0;
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) pcm |= (uint32_t)(pk(ps, j) == kPC) << j;
+        uint32_t lk[kPer] = {0u, 0u, 0u, 0u};
+        if (__any(pcm != 0)) {  // a copy of a lookup: the key in the lookup's vcur entry
+          const uint2 rw = *reinterpret_cast<const uint2*>(&ref[li0]);
+          const int rv[kPer] = {(int16_t)(rw.x & 0xffffu), (int16_t)(rw.x >> 16), (int16_t)(rw.y & 0xffffu),
+                                (int16_t)(rw.y >> 16)};
+#pragma unroll
+          for (int j = 0; j < kPer; ++j) lk[j] = vcur[(pcm >> j) & 1u ? rv[j] : li0 + j];
+        }
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+          const uint32_t c = pk(ps, j);
+          hk[j] = c == kPK ? hash_px(v[j], shift) : c == kPL ? v[j] : lk[j] & (kKeysW64 - 1);
+          hm |= (uint32_t)(c != kPK || is_upd(ps, j)) << j;
+        }
+        uint32_t pend = hm;
+        for (int it = 0; it < 8; ++it) {
+          const uint64_t bm = __ballot(pend != 0);
+          if (bm == 0) break;
+          const int lead = __builtin_ctzll(bm);
+          const int jf = __builtin_ctz(pend | 0x10u);
+          const uint32_t kf = jf == 0 ? hk[0] : jf == 1 ? hk[1] : jf == 2 ? hk[2] : hk[3];
+          const uint32_t kl = (uint32_t)__builtin_amdgcn_readlane((int)kf, lead);
+          uint32_t mm = 0;
+#pragma unroll
+          for (int j = 0; j < kPer; ++j) mm |= (uint32_t)(((pend >> j) & 1u) && hk[j] == kl) << j;
+          const uint64_t mb = __ballot(mm != 0);
+          if (lane == 63 - __builtin_clzll(mb))
+            ds_write_u32(&lastp[wave * kKeysW64 + kl], (uint32_t)(li0 + 31 - __builtin_clz(mm)) + 1u);
+          pend &= ~mm;
+          if (__builtin_popcountll(mb) < 4) break;
+        }
+#pragma unroll
+        for (int j = 0; j < kPer; ++j)
+          if ((pend >> j) & 1u) ds_max_u32(&lastp[wave * kKeysW64 + hk[j]], (uint32_t)(li0 + j) + 1u);
+      }
+      bar();  // (also orders step 1's far-copy values before the next block's reads)
+      K7_T(11);
+      // L: the wave's lookups one at a time (wave-uniform loop; most waves hold none)
+      if (blk_pl && nkeys) {
+        uint32_t lm = 0;
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) lm |= (uint32_t)(pk(ps, j) == kPL) << j;
+        while (true) {
+          const uint64_t bm = __ballot(lm != 0);
+          if (bm == 0) break;
+          const int lead = __builtin_ctzll(bm);
+          const int jf = __builtin_ctz(lm | 0x10u);
+          const uint32_t kf = jf == 0 ? v[0] : jf == 1 ? v[1] : jf == 2 ? v[2] : v[3];  // (a lookup's key)
+          const int j0 = __builtin_amdgcn_readlane(jf, lead);
+          const uint32_t kl = (uint32_t)__builtin_amdgcn_readlane((int)kf, lead);
+          const int pos = wave * kWavePx + kPer * lead + j0;
+          uint32_t mm = 0;  // my pixels before it that insert under its key
+#pragma unroll
+          for (int j = 0; j < kPer; ++j) mm |= (uint32_t)(((hm >> j) & 1u) && hk[j] == kl && li0 + j < pos) << j;
+          const uint64_t mb = __ballot(mm != 0);
+          int p;
+          if (mb) {
+            p = __builtin_amdgcn_readlane(li0 + 31 - __builtin_clz(mm | 1u), 63 - __builtin_clzll(mb));
+          } else {  // the earlier waves' last pixels of the key: lane w < wave reads wave w's
+            const uint32_t x = lane < wave ? lastp[lane * kKeysW64 + kl] : 0u;
+            const uint64_t wb = __ballot(x != 0u);
+            p = wb ? (int)__builtin_amdgcn_readlane((int)x, 63 - __builtin_clzll(wb)) - 1 : -1;
+          }
+          if (lane == lead) {
+            // pixel p: known (its value), a lookup (a copy of it now), or a copy of a lookup (a
+            // copy of that lookup) -- its state as R left it or as L has since made it, either
+            // way a pointer along the chain
+            const uint32_t sp = p >= 0 ? st[p] : kKnown;
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const uint32_t xp = vcur[p >= 0 ? p : 0];
+            const int rp = ref[p >= 0 ? p : 0];
+            if (p >= 0 && sp != kKnown) {
+              ps ^= (kPL ^ kPC) << (2 * j0);
+              ref[pos] = (int16_t)(sp == kPendLookup ? p : rp);
+              __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+              st[pos] = kPendCopy;
+            } else if (p >= 0) {
+#pragma unroll
+              for (int j = 0; j < kPer; ++j) v[j] = j == j0 ? xp : v[j];
+              set_known(ps, j0);
+              vcur[pos] = xp;
+              __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+              st[pos] = kKnown;
+            } else {  // the slot as the blocks before left it
+              const uint2 rec = slotrec[kl];
+              if (kl != 0u && !((slot_set[kl >> 5] >> (kl & 31)) & 1u)) {
+                K7_COUNT(9, 1);
+                slow[b & 1] = 1;
+              }
+#pragma unroll
+              for (int j = 0; j < kPer; ++j) v[j] = j == j0 ? rec.y : v[j];
+              set_known(ps, j0);
+              vcur[pos] = rec.y;
+              __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+              st[pos] = kKnown;
+            }
+            lm &= ~(1u << j0);
+          }
+        }
+        K7_T(12);
+        // J
+        uint32_t pcm = 0;
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) pcm |= (uint32_t)(pk(ps, j) == kPC) << j;
+        if (sync_or(pcm != 0)) jump_rounds();
+      }
+      K7_T(13);
+      // T (after a barrier: every pixel known, every lookup done with the table)
+      const bool go_serial = slow[b & 1] != 0;
+      if (nkeys && tid < nkeys) {
+        uint32_t x[kWaves];
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) x[w] = lastp[w * kKeysW64 + tid];
+        int p = -1;
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) p = x[w] ? (int)x[w] - 1 : p;
+        if (p >= 0 && !go_serial) {
+          slotrec[tid].y = vcur[p];
+          ds_or_b32(&slot_set[tid >> 5], 1u << (tid & 31));
+        }
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) lastp[w * kKeysW64 + tid] = 0u;
+      }
+      if (go_serial) serial_from = 0;
+    } else {
     // updaters of the block before pixel j (recomputed at each use: four live ranks cost registers)
     const int r0 = woff + excl;
     auto R = [&](int j) { return r0 + __builtin_popcount((ps >> 8) & ((1u << j) - 1u)); };
     const int nwin = kWaves / wpw;
     const int myq = wave / wpw;
-    int serial_from = kBlock;  // local pixel where the serial path takes over
     for (int q = 0; q < nwin; ++q) {
       const bool in_win = myq == q;
       const int rb = prefix(q * wpw);  // updaters before the window
@@ -991,6 +1233,7 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
       K7_T(13);
     }
     K7_T(5);
+    }
     // ---- the exact serial path: DecodeImageData's order, one pixel at a time, from the start
     //      of the window that could not be resolved, on the table as the windows before it left
     //      it.  Literal and older-copy values are in vcur from step 1; everything else is
