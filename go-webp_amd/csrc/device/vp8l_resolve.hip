@@ -69,6 +69,7 @@ constexpr int kMaxW = 32;                 // mask words per key (the summary is 
 constexpr int kW64Bits = 7;               // kW64: cache_bits <= 7 (<= 128 keys x 64 words)
 constexpr int kKeysW64 = 1 << kW64Bits;
 constexpr int kMaxRounds = 32;
+constexpr int kWalk = 8;                  // dense blocks: links a pending copy walks per round
 constexpr uint8_t kKnown = 1, kPendCopy = 2, kPendLookup = 3;
 constexpr uint32_t kDropOff = 0xffffffc0u;  // buffer offset past any stream: loads return 0
 
@@ -643,7 +644,14 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
       if (lane == 63) rscan[wave] = sc;
       int root = __builtin_amdgcn_update_dpp(-1, sc, 0x138, 0xf, 0xf, false);  // wave_shr:1: lanes before me
       bar();
-      for (int w = 0; w < wave; ++w) root = max(root, rscan[w]);  // (wave-uniform loop)
+      {  // the earlier waves' last roots: lane w < wave reads wave w's, a max over row 0's lanes
+        int x = lane < wave ? rscan[lane & 15] : -1;
+        x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x111, 0xf, 0xf, false));  // row_shr:1
+        x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x112, 0xf, 0xf, false));  // row_shr:2
+        x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x114, 0xf, 0xf, false));  // row_shr:4
+        x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x118, 0xf, 0xf, false));  // row_shr:8
+        root = max(root, __builtin_amdgcn_readlane(x, 15));
+      }
       uint32_t stw = 0, rfw[2] = {0u, 0u};
 #pragma unroll
       for (int j = 0; j < kPer; ++j) {
@@ -658,6 +666,7 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
     }
     int serial_from = kBlock;  // local pixel where the serial path takes over
     if constexpr (kW64) {
+      K7_T(6);
       // ---- Dense blocks (the small-cache instantiation: alpha planes and flat content, nearly
       //      every pixel a copy and a few lookups).  No ranks and no masks:
       //  R  pointer jumping over the in-block copies with the lookups as roots: every copy ends
@@ -723,7 +732,7 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
 #pragma unroll
             for (int j = 0; j < kPer; ++j) nref[j] = ref[src[j]];
           }
-          uint32_t stw = 0;
+          uint32_t walk = 0;  // slots whose source was a pending copy: walking on along the chain
 #pragma unroll
           for (int j = 0; j < kPer; ++j) {
             if ((pcm >> j) & 1u) {
@@ -732,9 +741,39 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
                 v[j] = xs[j];
               } else if (ss[j] == kPendCopy) {
                 rv[j] = nref[j];  // (a stale or fresh link: both lie on the chain)
-                still = true;
+                walk |= 1u << j;
               }
             }
+          }
+          // the chain further, link by link within the round (the links are static, or shortcuts
+          // other lanes have since taken): most chains end within the first round, which leaves
+          // one barrier per phase instead of one per link doubling
+          for (int h = 0; h < kWalk && walk; ++h) {
+#pragma unroll
+            for (int j = 0; j < kPer; ++j) ss[j] = (walk >> j) & 1u ? st[rv[j]] : 0u;
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int j = 0; j < kPer; ++j) xs[j] = (walk >> j) & 1u ? vcur[rv[j]] : 0u;
+#pragma unroll
+            for (int j = 0; j < kPer; ++j) nref[j] = (walk >> j) & 1u ? ref[rv[j]] : 0;
+#pragma unroll
+            for (int j = 0; j < kPer; ++j) {
+              if (!((walk >> j) & 1u)) continue;
+              if (ss[j] == kKnown) {
+                set_known(ps, j);
+                v[j] = xs[j];
+                walk &= ~(1u << j);
+              } else if (ss[j] == kPendCopy) {
+                rv[j] = nref[j];
+              } else {  // a lookup: the copy points at it
+                walk &= ~(1u << j);
+              }
+            }
+          }
+          still = walk != 0;
+          uint32_t stw = 0;
+#pragma unroll
+          for (int j = 0; j < kPer; ++j) {
             const uint32_t c = pk(ps, j);
             stw |= (uint32_t)(c == kPC ? kPendCopy : c == kPL ? kPendLookup : kKnown) << (8 * j);
           }
@@ -880,19 +919,25 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
       K7_T(13);
       // T (after a barrier: every pixel known, every lookup done with the table)
       const bool go_serial = slow[b & 1] != 0;
-      if (nkeys && tid < nkeys) {
-        uint32_t x[kWaves];
-#pragma unroll
-        for (int w = 0; w < kWaves; ++w) x[w] = lastp[w * kKeysW64 + tid];
-        int p = -1;
-#pragma unroll
-        for (int w = 0; w < kWaves; ++w) p = x[w] ? (int)x[w] - 1 : p;
-        if (p >= 0 && !go_serial) {
-          slotrec[tid].y = vcur[p];
-          ds_or_b32(&slot_set[tid >> 5], 1u << (tid & 31));
+      // (one lane per key and wave, a key's sixteen in one DPP row: spread over the waves, not a
+      // chain of reads in one, which the other waves waited for at the next block's rank barrier)
+      if (nkeys) {
+        const int tot = nkeys * kWaves;
+        for (int e0 = 0; e0 < tot; e0 += kThreads) {
+          if (e0 + wave * 64 >= tot) break;  // (wave-uniform: whole rows of sixteen lanes)
+          const int e = e0 + tid, k = e >> 4, w = e & 15;
+          const bool ok = e < tot;
+          uint32_t x = ok ? lastp[w * kKeysW64 + k] : 0u;
+          if (ok) lastp[w * kKeysW64 + k] = 0u;
+          x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false));  // row_shr:1
+          x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false));  // row_shr:2
+          x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false));  // row_shr:4
+          x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false));  // row_shr:8
+          if (ok && (lane & 15) == 15 && x != 0u && !go_serial) {
+            slotrec[k].y = vcur[x - 1u];
+            ds_or_b32(&slot_set[k >> 5], 1u << (k & 31));
+          }
         }
-#pragma unroll
-        for (int w = 0; w < kWaves; ++w) lastp[w * kKeysW64 + tid] = 0u;
       }
       if (go_serial) serial_from = 0;
     } else {

@@ -30,11 +30,11 @@ def main():
     ms = b.kernel_ms()
     L.wg_debug_k7_stats(st, 1)
     blocks, serial, rounds, windows = st[0], st[1], st[2], st[3]
-    # (the 64-word instantiation's dense blocks reuse the slots: 5 R jumping, 11 H last pixels, 12 L
+    # (the 64-word instantiation's dense blocks reuse the slots: 6 far copies + setup, 5 R jumping, 11 H last pixels, 12 L
     # lookups, 13 J jumping, 7 T slot table + end of block)
     phases = ((8, "classify (lit wait)"), (15, "prev-block copies+store"), (14, "issue next loads"), (4, "ranks + barrier"),
               (11, "registration | H"), (12, "lookups | L"), (5, "copies (rounds b) | R"),
-              (13, "slot table | J"), (6, "serial path"), (7, "store + pipeline | T"))
+              (13, "slot table | J"), (6, "serial path | setup"), (7, "store + pipeline | T"))
     tot = sum(st[i] for i, _ in phases)
     print(f"frames {n}: K7 {ms[4]:.3f} ms; blocks {blocks}, windows/block {windows / blocks:.3f}, "
           f"rounds/window {rounds / max(windows, 1):.3f}, serial windows {serial}")
