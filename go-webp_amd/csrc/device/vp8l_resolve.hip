@@ -276,7 +276,17 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
   const int a_ncb = (D.a_width + 15) >> 4;
   const __amdgpu_buffer_rsrc_t at_rs = __builtin_amdgcn_make_buffer_rsrc(
       D.atile, 0, kAlpha == 2 ? ((D.a_height - 1 + 63) >> 6) * a_ncb * 1024 : 0, 0x00020000);
-  auto store_alpha = [&](int pos0, const uint32_t* ov) {
+  auto div_cw = [&](int p) {  // (a multiply-shift: the host's magic number, p < 2^28)
+    return (int)(((uint64_t)(uint32_t)p * D.a_cw_m) >> (28 + D.a_cw_s));
+  };
+  // (kAlpha) row and column of this thread's first pixel of the block store_block writes next:
+  // stepped by a block's rows and columns per store instead of a division per block
+  int a_y = 0, a_x = 0, a_q = 0, a_r = 0;
+  if constexpr (kAlpha != 0) {
+    a_q = div_cw(kBlock), a_r = kBlock - a_q * D.a_cw;
+    a_y = div_cw(li0), a_x = li0 - a_y * D.a_cw;
+  }
+  auto store_alpha = [&](int pos0, const int yc, const int xc, const uint32_t* ov) {
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
     const int cw = D.a_cw, W = D.a_width, cb = D.a_cbits;
@@ -285,10 +295,6 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
       const int r = y - 1;
       return (uint32_t)((((r >> 6) * a_ncb + (x >> 4)) << 10) + ((r & 63) << 4) + (x & 15));
     };
-    auto div_cw = [&](int p) {  // (a multiply-shift: the host's magic number, p < 2^28)
-      return (int)(((uint64_t)(uint32_t)p * D.a_cw_m) >> (28 + D.a_cw_s));
-    };
-    const int yc = div_cw(pos0), xc = pos0 - yc * cw;
     const uint32_t g0 = (ov[0] >> 8) & 0xffu, g1 = (ov[1] >> 8) & 0xffu, g2 = (ov[2] >> 8) & 0xffu, g3 = (ov[3] >> 8) & 0xffu;
     const int x0 = xc << cb, nbytes = kPer << cb;
     const bool tiled = kAlpha == 2 && yc >= 1;
@@ -334,8 +340,10 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
     if constexpr (kAlpha != 0) {
       if (pos0 < n) {
         const uint32_t ov[kPer] = {o.x, o.y, o.z, o.w};
-        store_alpha(pos0, ov);
+        store_alpha(pos0, a_y, a_x, ov);
       }
+      a_x += a_r, a_y += a_q;
+      if (a_x >= D.a_cw) a_x -= D.a_cw, ++a_y;
     }
   };
   // LDS atomics without return as inline asm: the waitcnt pass makes every LDS atomic wait
@@ -566,6 +574,36 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
     const int excl = count_below(b0) + 2 * count_below(b1) + 4 * count_below(b2);
     const bool wave_far = __any(cm != 0u);
     const bool wave_pl = kW64 && __any((~ps & (ps >> 1) & 0x55u) != 0u);  // (kW64) a cache lookup, code kPL
+    // Runs of distance-1 copies (run-length coding, CopyBlock32b with dist 1: every pixel of the run
+    // equals the one before it) point straight at their root -- the last pixel before them that is
+    // not such a copy -- from a block-wide max-scan of root positions, so the pointer jumping below
+    // meets no chain of a run's length (alpha planes and flat lossless content are mostly runs) but
+    // only the short chains of the other distances.  Pixel 0 of a block is never an in-block copy,
+    // so a root always exists.  The wave's part depends on the tokens alone: kW64 sends its last root
+    // out before the rank barrier, which orders it for the setup (a wave without in-block copies ends
+    // on a root); the 32-word instantiation scans in the setup behind a barrier of its own (measured:
+    // the early scan cost C5's K7 2 %, its values live across the rank barrier in a 128-VGPR kernel).
+    auto run_scan = [&](uint32_t& runm, int& root) {  // root: the last root before my first pixel
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) runm |= (uint32_t)(pk(ps, j) == kPC && aux[j] == 1u) << j;
+      const uint32_t nonrun = ~runm & 0xfu;
+      int sc = nonrun ? li0 + 31 - __builtin_clz(nonrun) : -1;  // my last root
+      sc = max(sc, __builtin_amdgcn_update_dpp(-1, sc, 0x111, 0xf, 0xf, false));  // row_shr:1
+      sc = max(sc, __builtin_amdgcn_update_dpp(-1, sc, 0x112, 0xf, 0xf, false));  // row_shr:2
+      sc = max(sc, __builtin_amdgcn_update_dpp(-1, sc, 0x114, 0xf, 0xf, false));  // row_shr:4
+      sc = max(sc, __builtin_amdgcn_update_dpp(-1, sc, 0x118, 0xf, 0xf, false));  // row_shr:8
+      sc = lane >= 16 ? max(sc, __builtin_amdgcn_readlane(sc, 15)) : sc;
+      sc = lane >= 32 ? max(sc, __builtin_amdgcn_readlane(sc, 31)) : sc;
+      sc = lane >= 48 ? max(sc, __builtin_amdgcn_readlane(sc, 47)) : sc;
+      if (lane == 63) rscan[wave] = sc;
+      root = __builtin_amdgcn_update_dpp(-1, sc, 0x138, 0xf, 0xf, false);  // wave_shr:1: lanes before me
+    };
+    uint32_t runm_w = 0;
+    int root_w = -1;
+    if constexpr (kW64) {
+      if (wave_pc) run_scan(runm_w, root_w);
+      else if (lane == 63) rscan[wave] = li0 + kPer - 1;
+    }
     if (lane == 0)
       wsum[wave] = (uint32_t)(__builtin_popcountll(b0) + 2 * __builtin_popcountll(b1) + 4 * __builtin_popcountll(b2)) |
                    (wave_far ? 0x10000u : 0u) | (wave_pc ? 0x20000u : 0u) | (wave_pl ? 0x40000u : 0u);
@@ -623,27 +661,25 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
     load_lits(tk_nxt, vprv);
     // in-block copies: sources and every pixel's state for the pointer jumping (rare in C5)
     if (blk_pc || (kW64 && blk_pl)) {
-      // Runs of distance-1 copies (run-length coding, CopyBlock32b with dist 1: every pixel of the
-      // run equals the one before it) point straight at their root -- the last pixel before them
-      // that is not such a copy -- from a block-wide max-scan of root positions, so the pointer
-      // jumping below meets no chain of a run's length (log2 of it in rounds, two barriers each;
-      // alpha planes and flat lossless content are mostly runs) but only the short chains of the
-      // other distances.  Pixel 0 of a block is never an in-block copy, so a root always exists.
-      uint32_t runm = 0;
+      uint32_t runm = runm_w;
+      int root = root_w;
+      if constexpr (!kW64) {  // (written out as before the kW64 change: the same machine code)
+        runm = 0;
 #pragma unroll
-      for (int j = 0; j < kPer; ++j) runm |= (uint32_t)(pk(ps, j) == kPC && aux[j] == 1u) << j;
-      const uint32_t nonrun = ~runm & 0xfu;
-      int sc = nonrun ? li0 + 31 - __builtin_clz(nonrun) : -1;  // my last root
-      sc = max(sc, __builtin_amdgcn_update_dpp(-1, sc, 0x111, 0xf, 0xf, false));  // row_shr:1
-      sc = max(sc, __builtin_amdgcn_update_dpp(-1, sc, 0x112, 0xf, 0xf, false));  // row_shr:2
-      sc = max(sc, __builtin_amdgcn_update_dpp(-1, sc, 0x114, 0xf, 0xf, false));  // row_shr:4
-      sc = max(sc, __builtin_amdgcn_update_dpp(-1, sc, 0x118, 0xf, 0xf, false));  // row_shr:8
-      sc = lane >= 16 ? max(sc, __builtin_amdgcn_readlane(sc, 15)) : sc;
-      sc = lane >= 32 ? max(sc, __builtin_amdgcn_readlane(sc, 31)) : sc;
-      sc = lane >= 48 ? max(sc, __builtin_amdgcn_readlane(sc, 47)) : sc;
-      if (lane == 63) rscan[wave] = sc;
-      int root = __builtin_amdgcn_update_dpp(-1, sc, 0x138, 0xf, 0xf, false);  // wave_shr:1: lanes before me
-      bar();
+        for (int j = 0; j < kPer; ++j) runm |= (uint32_t)(pk(ps, j) == kPC && aux[j] == 1u) << j;
+        const uint32_t nonrun = ~runm & 0xfu;
+        int sc = nonrun ? li0 + 31 - __builtin_clz(nonrun) : -1;  // my last root
+        sc = max(sc, __builtin_amdgcn_update_dpp(-1, sc, 0x111, 0xf, 0xf, false));  // row_shr:1
+        sc = max(sc, __builtin_amdgcn_update_dpp(-1, sc, 0x112, 0xf, 0xf, false));  // row_shr:2
+        sc = max(sc, __builtin_amdgcn_update_dpp(-1, sc, 0x114, 0xf, 0xf, false));  // row_shr:4
+        sc = max(sc, __builtin_amdgcn_update_dpp(-1, sc, 0x118, 0xf, 0xf, false));  // row_shr:8
+        sc = lane >= 16 ? max(sc, __builtin_amdgcn_readlane(sc, 15)) : sc;
+        sc = lane >= 32 ? max(sc, __builtin_amdgcn_readlane(sc, 31)) : sc;
+        sc = lane >= 48 ? max(sc, __builtin_amdgcn_readlane(sc, 47)) : sc;
+        if (lane == 63) rscan[wave] = sc;
+        root = __builtin_amdgcn_update_dpp(-1, sc, 0x138, 0xf, 0xf, false);  // wave_shr:1: lanes before me
+        bar();
+      }
       {  // the earlier waves' last roots: lane w < wave reads wave w's, a max over row 0's lanes
         int x = lane < wave ? rscan[lane & 15] : -1;
         x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x111, 0xf, 0xf, false));  // row_shr:1
