@@ -841,8 +841,14 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
       // H: the hash each pixel inserts under (known updaters: of the value; lookups and copies
       // of one: the key), and per wave and key the last pixel -- the lanes of one key combined
       // while a key still gathers four lanes (a dense wave is mostly one key), the rest by ds_max
-      uint32_t hk[kPer], hm = 0;
-      if (nkeys) {
+      uint32_t hk[kPer] = {0u, 0u, 0u, 0u}, hm = 0;
+      // a flat wave (every pixel a known updater of one value: most of an alpha plane's waves) has
+      // one hash, computed once, and its last pixel as the key's (no lookup of its own reads hk)
+      const uint32_t v0u = (uint32_t)__builtin_amdgcn_readfirstlane((int)v[0]);
+      const bool flat = nkeys && __all((ps & 0xfffu) == 0xf00u && v[0] == v0u && v[1] == v0u && v[2] == v0u && v[3] == v0u);
+      if (flat) {
+        if (lane == 63) ds_write_u32(&lastp[wave * kKeysW64 + hash_px(v0u, shift)], (uint32_t)(li0 + kPer));
+      } else if (nkeys) {
         uint32_t pcm = 0;
 #pragma unroll
         for (int j = 0; j < kPer; ++j) pcm |= (uint32_t)(pk(ps, j) == kPC) << j;
