@@ -181,4 +181,10 @@ CASES = [
     # lookups read what they left
     ("w64_quiet_blocks", 6 * 4096 + 17, 4, dict(p_lit=0.1, p_copy=0.8, dist=(1, "w", 3), run=30, width=900,
                                                 palette=40, quiet=((4096, 3 * 4096), (4 * 4096 + 100, 5 * 4096 + 7)))),
+    # round 6's rank-free dense blocks (cache bits <= 7): copies of lookups (a lookup's key is their
+    # hash before its value is known), lookups whose last pixel of the key is such a copy or another
+    # lookup, and the copy / lookup chain walked across rounds
+    ("w64_lookup_dense", 3 * 4096 + 41, 3, dict(p_lit=0.01, p_copy=0.7, dist=(1, 2, "w", "near"), run=6, width=500,
+                                                palette=10)),
+    ("w64_chain", 2 * 4096 + 3, 4, dict(chain=True, palette=24)),
 ]
