@@ -18,7 +18,8 @@
 // for k != 0 (a stream no encoder writes) -- that case takes the exact serial path below.
 //
 // Geometry.  One 1024-thread workgroup per stream, walking the image in blocks of 4096 pixels
-// (4 consecutive per thread) in scan order; the cache (up to 2048 slots) lives in LDS.  The
+// (4 consecutive per thread) in scan order; the cache (up to 2048 slots) lives in LDS.  Two ways to
+// resolve a block: dense blocks (cache_bits <= 7, below: kW64) need no ranks; the others do.  The
 // updaters of a block get RANKS (their order in the block, a block-wide prefix count: known
 // before any value is, since whether a pixel is an updater depends on its token only).  Per
 // key, a bitmask over ranks marks the block's updaters with that hash, so a lookup at pixel i
@@ -111,18 +112,13 @@ __device__ unsigned long long g_k7_wave[kWaves][16];  // per wave (lane 0): the 
 #endif
 
 // kW64 (streams with cache_bits <= 7, none included, chosen by the host): the instantiation for
-// dense updaters -- alpha planes and flat content, where nearly every pixel is a copy.
-//  * 64 mask words per key under a 64-bit summary, so a window holds 4096 ranks: every block is
-//    one window (at 32 words such a block ran as two windows of eight waves, each idling through
-//    the other's rounds).  The summaries of its <= 128 keys live in summ's first 1 KB as 64-bit
-//    words; stores that are not registrations are masked off (ranks reach uval's dummy slots).
-//  * Registration by consecutive ranks with the lanes of one key combined (reg_pass / reg_run):
-//    same-address LDS atomics serialize lane by lane, and a run of copies puts a wave's 64 lanes
-//    on one key.  Copies resolved in a round flag their ranks and register in one such pass.
-//  * The rounds' copy step gathers its four slots' states, values and links as independent LDS
-//    reads, and takes one first_pend min per wave.
-// C5-like streams (cache_bits 10, ~143 updaters per block) keep the 32-word instantiation, whose
-// code is unchanged by these (measured: the dense paths cost C5's K7 7 %, and gain c3a's 28 %).
+// dense blocks -- alpha planes and flat content, nearly every pixel a copy, a few lookups -- which
+// resolve without ranks or masks (round 6; the block body's dense branch, steps R H L J T there):
+// copies pointer-jump with the lookups as roots (a slot only holds values of its own hash, so a
+// lookup and its copies insert under its key before the value is known), a per-wave last pixel
+// per key gives each lookup its source, and the chains are walked several links per round.
+// C5-like streams (cache_bits 10, ~143 updaters per block among ~3,950 lookups) keep the 32-word
+// instantiation: rank masks suit sparse updaters (its machine code is unchanged by the dense path).
 // kSingle: the one stream `single` passed by value (the stage entry wg_vp8l_resolve_device; err may
 // be null there: bad tokens then only resolve to 0, the serial path's rule); else stream
 // blockIdx.x of `descs`.  (Two instantiations: a descriptor chosen at run time between the two
@@ -164,9 +160,8 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
   const int n = D.n_px, cache_bits = D.cache_bits;
   const int nkeys = cache_bits > 0 ? 1 << cache_bits : 0;
   const int shift = 32 - cache_bits;
-  const int W = kW64 ? 64 : cache_bits > 0 ? min(kMaxW, kMaskWords >> cache_bits) : 1;  // mask words per key
+  const int W = cache_bits > 0 ? min(kMaxW, kMaskWords >> cache_bits) : 1;  // mask words per key (32-word path)
   const int cap = 64 * W;                                                              // ranks per window
-  uint64_t* const summ64 = reinterpret_cast<uint64_t*>(summ);  // (kW64: key k's summary)
   // Buffer descriptors: out-of-range loads return 0 with no branch, so the prefetches below are
   // straight-line code and the waitcnt pass can count them precisely (a load under a lane
   // branch makes it wait for every outstanding load at the join).
@@ -360,8 +355,7 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
   auto reg_hash = [&](int r, uint32_t x) {
     const uint32_t h = hash_px(x, shift);
     ds_or_b64(&mask[h * W + (r >> 6)], 1ull << (r & 63));
-    if (kW64) ds_or_b64(&summ64[h], 1ull << (r >> 6));
-    else ds_or_b32(&summ[h], 1u << (r >> 6));
+    ds_or_b32(&summ[h], 1u << (r >> 6));
     ds_max_u32(&slotrec[h].x, (uint32_t)r + 1u);
   };
   // step 3 for one registered updater: if it is its key's last in the window, write the slot
@@ -371,13 +365,8 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
   auto table_update = [&](int r, uint32_t x, bool go_serial) {
     const uint32_t h = hash_px(x, shift);
     if (slotrec[h].x == (uint32_t)r + 1u) {
-      if (kW64) {
-        // (the masks and summaries are cleared by the whole workgroup after the table: a key's
-        // last updater walking up to 64 words alone made the block's last wave the slowest)
-      } else {
-        for (uint32_t sm = summ[h]; sm; sm &= sm - 1) mask[h * W + __builtin_ctz(sm)] = 0;
-        summ[h] = 0;
-      }
+      for (uint32_t sm = summ[h]; sm; sm &= sm - 1) mask[h * W + __builtin_ctz(sm)] = 0;
+      summ[h] = 0;
       if (!go_serial) {
         slotrec[h] = make_uint2(0u, x);
         ds_or_b32(&slot_set[h >> 5], 1u << (h & 31));
@@ -394,71 +383,6 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   };
 
-  // Rank flags of a wave's updaters (waves with in-block copies): 2 = value known, to register;
-  // 3 = registered; 0 = pending.  They live in the straddle scratch: a wave sets and consumes its
-  // own ranks' flags within step 2 or within one round's (b), between barriers, and rewrites them
-  // first (the lookups (a) use the scratch in between).
-  uint8_t* const rflag = reinterpret_cast<uint8_t*>(sscr);
-  static_assert(sizeof(sscr) >= kBlock, "rflag: one byte per rank");
-  // Registration of a wave's updaters with CONSECUTIVE ranks rbase + lane (the lanes with `valid`).
-  // Dense runs of updaters (alpha planes, flat content: every pixel a copy) put many lanes on one
-  // key, and same-address LDS atomics serialize lane by lane; so in a dense pass (wave-uniform)
-  // the lanes of one key combine first -- their rank bits are the key's lane ballot shifted by
-  // rbase, one mask OR per word, one summary OR, one max -- key by key while a key still gathers
-  // four lanes; the rest register one lane at a time.
-  auto reg_run = [&](bool valid, int rbase, int r, uint32_t x, bool dense) {
-    const uint32_t h = hash_px(x, shift);
-    bool pend = valid;
-    if (dense) {
-      for (int it = 0; it < 8; ++it) {
-        const uint64_t pm = __ballot(pend);
-        if (pm == 0) break;
-        const int lead = __builtin_ctzll(pm);
-        const uint32_t hl = (uint32_t)__builtin_amdgcn_readlane((int)h, lead);
-        const uint64_t m = __ballot(pend && h == hl);
-        if (lane == lead) {
-          const int w0 = rbase >> 6, sh = rbase & 63;
-          const uint64_t lo = m << sh, hi = sh ? m >> (64 - sh) : 0ull;
-          if (lo) ds_or_b64(&mask[hl * W + w0], lo);
-          if (hi) ds_or_b64(&mask[hl * W + w0 + 1], hi);
-          if (kW64) {
-            ds_or_b64(&summ64[hl], (lo ? 1ull << w0 : 0ull) | (hi ? 2ull << w0 : 0ull));
-          } else {
-            ds_or_b32(&summ[hl], (lo ? 1u << w0 : 0u) | (hi ? 2u << w0 : 0u));
-          }
-          ds_max_u32(&slotrec[hl].x, (uint32_t)(rbase + 63 - __builtin_clzll(m)) + 1u);
-        }
-        pend = pend && h != hl;
-        if (__builtin_popcountll(m) < 4) break;
-      }
-    }
-    if (pend) reg_hash(r, x);
-  };
-  // this wave's updaters of ranks [r0w, r0w + cnt) (its whole range in the window): all of them,
-  // or (flagged) those flagged 2, which become 3
-  auto reg_pass = [&](int r0w, int cnt, bool flagged) {
-    wave_sync();
-    const bool dense = cnt >= 64;
-    for (int i0 = 0; i0 < cnt; i0 += 64) {
-      const int r = r0w + i0 + lane;
-      bool valid = i0 + lane < cnt;
-      if (flagged) {
-        valid = valid && rflag[valid ? r : 0] == 2;
-        if (valid) rflag[r] = 3;
-      }
-      reg_run(valid, r0w + i0, r, uval[valid ? r : 0], dense);
-    }
-  };
-  // one ds_min per wave for a pending position that grows with the lane (the lowest lane's wins)
-  auto wave_min_pos = [&](int* p, int pos) {
-    const uint64_t m = __ballot(pos < kBlock);
-    if (m) {
-      const int lead = __builtin_ctzll(m);
-      const int x = __builtin_amdgcn_readlane(pos, lead);
-      if (lane == lead) ds_min_i32(p, x);
-    }
-  };
-
   // A lookup whose key has window updaters on both sides of it: the highest bit of the key's
   // rank mask below rr (the window updaters before the pixel), from the summary's top one or
   // two words; ~0 if none.
@@ -466,13 +390,7 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
     const int wt = (rr - 1) >> 6;
     int w1, w2;
     bool h1, h2;  // the top / second non-empty words below the pixel exist
-    if (kW64) {
-      const uint64_t sm = rr <= 0 ? 0ull : summ64[k] & (wt >= 63 ? ~0ull : (2ull << wt) - 1ull);
-      w1 = sm ? 63 - __builtin_clzll(sm) : 0;
-      const uint64_t sm2 = sm & ~(1ull << w1);
-      w2 = sm2 ? 63 - __builtin_clzll(sm2) : 0;
-      h1 = sm != 0, h2 = sm2 != 0;
-    } else {
+    {
       const uint32_t sm = rr <= 0 ? 0u : summ[k] & (wt >= 31 ? ~0u : (2u << wt) - 1u);
       w1 = sm ? 31 - __builtin_clz(sm) : 0;
       const uint32_t sm2 = sm & ~(1u << w1);
@@ -997,33 +915,7 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
       //         wave's ranks [woff - rb, woff - rb + my_wc) -- or per pixel slot when the wave
       //         has in-block copies, whose ranks lie in the same range unregistered
       const bool pc = in_win && my_pc;
-      if constexpr (kW64) {
-        // Dense updaters (the small-cache instantiation): the value stores as inline asm (a plain
-        // LDS store here is the first LDS access after the next block's literal loads into LDS,
-        // and the waitcnt pass -- which cannot tell uval from their target -- would wait vmcnt(0)
-        // for them and the two-ahead token loads, every block; uval is read after bar()'s
-        // lgkmcnt(0), or by this wave in order), registration by consecutive ranks combined per
-        // key (a wave with in-block copies flags its known updaters first), one first_pend min
-        // per wave.
-#pragma unroll
-        for (int j = 0; j < kPer; ++j)
-          if (in_win && is_upd(ps, j) && pk(ps, j) == kPK) ds_write_u32(&uval[R(j) - rb], v[j]);
-        if (in_win && nkeys && blk_pl) {
-          if (wave_pc) {
-#pragma unroll
-            for (int j = 0; j < kPer; ++j)
-              if (is_upd(ps, j)) rflag[R(j) - rb] = pk(ps, j) == kPK ? 2 : 0;
-          }
-          reg_pass(woff - rb, my_wc, wave_pc);
-        }
-        if (in_win && wave_pc) {
-          int fp = kBlock;
-#pragma unroll
-          for (int j = kPer - 1; j >= 0; --j)
-            if (pk(ps, j) == kPC) fp = li0 + j;
-          wave_min_pos(&first_pend[0], fp);
-        }
-      } else {
+      {
 #pragma unroll
         for (int j = 0; j < kPer; ++j)
           uval[in_win && is_upd(ps, j) && pk(ps, j) == kPK ? R(j) - rb : uval_dummy] = v[j];
@@ -1054,12 +946,6 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
       // carries none of it.
       auto lookups = [&](const int fp, auto kRoundsC) __attribute__((always_inline)) {
         constexpr bool kRounds = decltype(kRoundsC)::value;
-        if constexpr (kW64) {  // (dense streams: most waves hold no lookup at all)
-          uint32_t any_pl = 0;
-#pragma unroll
-          for (int j = 0; j < kPer; ++j) any_pl |= (uint32_t)(pk(ps, j) == kPL);
-          if (!__any(any_pl)) return;
-        }
         // (a) lookups before the first pending copy: the key's last updater in the window if it
         //     precedes the pixel, none (the slot as the previous window left it), or -- it
         //     straddles the pixel -- the highest mask bit below the pixel's rank count
@@ -1172,72 +1058,7 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
         bar();
         // (b) pending copies: take a known source's value and register, else jump one link back
         bool still = false;  // a copy of mine still pending
-        if constexpr (kW64) {
-          uint32_t pcm = 0;    // my pending copies (slot bits)
-#pragma unroll
-          for (int j = 0; j < kPer; ++j) pcm |= (uint32_t)(pk(ps, j) == kPC) << j;
-          const bool wpend = __any(pcm != 0);  // (later rounds: most waves have nothing pending)
-          const bool regs = nkeys && blk_pl;  // copies register as they resolve (lookups follow)
-          if (in_win && wpend && regs) {  // this wave's rank flags (the scratch held lookups)
-#pragma unroll
-            for (int j = 0; j < kPer; ++j)
-              if (is_upd(ps, j)) rflag[R(j) - rb] = 0;
-          }
-          int myfp = kBlock;  // my first copy still pending
-          bool got = false;   // a copy of mine resolved (to register)
-          if (in_win && pcm) {
-            // Gather first, apply after: the four slots' source pointers (one 8-byte read), their
-            // states, values and links as independent LDS reads in flight together -- not four
-            // chains of three dependent reads.  The hand-off from other waves is st / vcur in LDS,
-            // whose DS operations a wave issues and the LDS performs in order: a writer's vcur store
-            // lands before its st store, and a reader's vcur load is issued after its st load, so a
-            // state read as known comes with the value; the fences only stop the compiler
-            // (wavefront scope: no instruction; a workgroup release would also wait vmcnt(0) for the
-            // next block's staged literal loads into LDS).  A slot whose source is an earlier slot of
-            // this lane sees that slot's state from before the round: it jumps instead of resolving,
-            // and resolves a round later.
-            const uint2 rw = *reinterpret_cast<const uint2*>(&ref[li0]);
-            const int rv[kPer] = {(int16_t)(rw.x & 0xffffu), (int16_t)(rw.x >> 16), (int16_t)(rw.y & 0xffffu),
-                                  (int16_t)(rw.y >> 16)};
-            int src[kPer];
-            uint32_t ss[kPer], xs[kPer];
-            int nref[kPer];
-#pragma unroll
-            for (int j = 0; j < kPer; ++j) src[j] = (pcm >> j) & 1u ? rv[j] : li0 + j;
-#pragma unroll
-            for (int j = 0; j < kPer; ++j) ss[j] = st[src[j]];
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-            for (int j = 0; j < kPer; ++j) xs[j] = vcur[src[j]];
-#pragma unroll
-            for (int j = 0; j < kPer; ++j) nref[j] = ref[src[j]];
-#pragma unroll
-            for (int j = 0; j < kPer; ++j) {
-              const int li = li0 + j;
-              if (!((pcm >> j) & 1u)) continue;
-              if (ss[j] == kKnown) {
-                const uint32_t x = xs[j];
-                set_known(ps, j);
-                v[j] = x;
-                vcur[li] = x;
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                st[li] = kKnown;
-                uval[R(j) - rb] = x;
-                if (regs) rflag[R(j) - rb] = 2;
-                got = true;
-              } else {
-                if (ss[j] == kPendCopy) ref[li] = (int16_t)nref[j];  // (a stale or fresh link: both lie on the chain)
-                myfp = min(myfp, li);
-                still = true;
-              }
-            }
-          }
-          if (in_win && wpend) {
-            wave_min_pos(&first_pend[(r + 1) & 1], myfp);
-            // the copies resolved this round register by rank (consecutive across lanes: combined per key)
-            if (regs && __any(got)) reg_pass(woff - rb, my_wc, true);
-          }
-        } else if (in_win) {
+        if (in_win) {
 #pragma unroll
           for (int j = 0; j < kPer; ++j) {
             const int li = li0 + j;
@@ -1266,32 +1087,6 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
       }
       bar();  // every lookup has read the slot table; the masks are complete
       const bool go_serial = slow[b & 1] != 0;
-      if constexpr (kW64) {
-        // a block without lookups registered nothing: each key's last updater (slotrec.x) from one
-        // pass over the ranks, combined per key like reg_run
-        if (!blk_pl && nkeys && !go_serial) {
-          if (in_win) {
-            for (int i0 = 0; i0 < my_wc; i0 += 64) {
-              const int r = woff - rb + i0 + lane;
-              const bool valid = i0 + lane < my_wc;
-              const uint32_t h = hash_px(uval[valid ? r : 0], shift);
-              bool pend = valid;
-              for (int it = 0; it < 8; ++it) {
-                const uint64_t pm = __ballot(pend);
-                if (pm == 0) break;
-                const int lead = __builtin_ctzll(pm);
-                const uint32_t hl = (uint32_t)__builtin_amdgcn_readlane((int)h, lead);
-                const uint64_t m = __ballot(pend && h == hl);
-                if (lane == lead) ds_max_u32(&slotrec[hl].x, (uint32_t)(woff - rb + i0 + 63 - __builtin_clzll(m)) + 1u);
-                pend = pend && h != hl;
-                if (__builtin_popcountll(m) < 4) break;
-              }
-              if (pend) ds_max_u32(&slotrec[h].x, (uint32_t)r + 1u);
-            }
-          }
-          bar();
-        }
-      }
       // ---- 3. each key's last updater writes its slot and clears the key's masks
       // the window's updaters packed 64 to a wave by rank (uval is complete after the barrier):
       // C5's ~143 per block take three waves' single pass instead of a sparse pass in each of
@@ -1300,10 +1095,6 @@ __global__ void __launch_bounds__(1024) vp8l_resolve_kernel(const LLTokDesc* __r
       if (in_win && nkeys) {
         const int wtot = prefix(q * wpw + wpw) - rb, wi = wave - q * wpw;
         for (int i = wi * 64 + lane; i < wtot; i += wpw * 64) table_update(i, uval[i], go_serial);
-      }
-      if constexpr (kW64) {  // every key's masks and summary, spread over the workgroup (lookups are done)
-        for (int i = tid; i < nkeys * W; i += kThreads) mask[i] = 0;
-        for (int i = tid; i < nkeys; i += kThreads) summ64[i] = 0;
       }
       if (tid == 0) first_pend[0] = first_pend[1] = kBlock;
       if (go_serial) {
